@@ -1,0 +1,40 @@
+"""Loader for the in-tree native extension ``_pconv_native``.
+
+``import torch`` comes first on purpose: torch ships its own
+``libamdhip64.so.7`` / ``librccl.so.1``; loading them first makes the
+extension (linked against the same sonames) bind to the copies torch already
+mapped instead of pulling a second HIP runtime into the process.
+
+The extension is REQUIRED: there is no silent Python fallback for the GPU
+path.  If it is missing, build it with ``python -c "import __graft_entry__ as g;
+g.build()"`` (or ``make -C <pkg>/csrc``).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+import torch  # noqa: F401  -- see module docstring
+
+_ERR = None
+try:
+    native = importlib.import_module(__package__ + "._pconv_native")
+except ImportError as e:  # pragma: no cover - exercised only on broken builds
+    native = None
+    _ERR = e
+
+
+def native_available() -> bool:
+    return native is not None
+
+
+def require_native():
+    """Return the extension module or raise a loud, actionable error."""
+    if native is None:
+        here = os.path.dirname(os.path.abspath(__file__))
+        raise ImportError(
+            f"pconv native extension not built (looked in {here}): run "
+            f"`make -C {os.path.join(here, 'csrc')}` or __graft_entry__.build(). "
+            f"Original error: {_ERR}"
+        )
+    return native

@@ -1,0 +1,43 @@
+// `conv` application: single-GPU, CPU and multi-GPU (native fork launcher) runs.
+//
+// Reference drivers: cuda/main.c:10-53 (parse, time, read, GPU_convolution,
+// write blur_<name>, print "Execution time: %.3f sec") and
+// mpi/mpi_convolution.c:17-286 (mpiexec -n P; MPI-IO band reads; loop timing
+// between MPI_Barrier/MPI_Wtime; max over ranks printed as "%f").
+//
+// Multi-GPU: `conv ... --gpus N` forks N worker processes BEFORE any HIP call
+// (one process per GPU, like mpiexec).  Workers share an anonymous mmap used
+// to hand out the RCCL unique id, as a barrier, and to collect per-rank loop
+// times (the reference's Send/Recv max-gather).  Each worker preads only its
+// band (+ ghost rows) and pwrites only its band of the pre-sized output file.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "pconv/cli.hpp"
+
+namespace pconv {
+
+struct AppReport {
+  double loop_s = 0;       // max over ranks of the rep-loop time
+  double e2e_s = 0;        // end-to-end wall time (incl. I/O and device init)
+  double mpix_per_s = 0;   // W*H*reps / loop_s / 1e6
+  int gpus = 1;
+  int halo = 1, fuse = 1;
+  int launches = 0, exchanges = 0;
+  int64_t mismatches = -1; // --check result (-1 = not checked)
+  std::string kernel;
+  std::string output;
+};
+
+// Runs the CLI (argv as given).  Returns the process exit code.
+int conv_main(int argc, char** argv);
+
+// Library entry: run a parsed config in this process (1 GPU or CPU), or via
+// the fork launcher when cfg.gpus > 1.
+AppReport run_app(const CliConfig& cfg);
+
+std::string report_json(const CliConfig& cfg, const AppReport& r);
+
+}  // namespace pconv

@@ -1,0 +1,57 @@
+// Command-line contract.
+//
+// Reference: `Usage()` (mpi/mpi_convolution.c:328-348) and `Initialization()`
+// (cuda/functions.c:10-29): exactly 5 positional arguments
+//   image.raw width height repetitions {grey|rgb}
+// parsed with atoi (no validation), error text "Error Input!" + usage line and
+// exit(EXIT_FAILURE) / MPI_Abort.  pconv keeps the positional contract
+// bit-compatible (same order, same type words, same error text) and adds
+// optional flags AFTER it.  Numbers are validated strictly.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "pconv/common.hpp"
+#include "pconv/kernels.hpp"
+
+namespace pconv {
+
+enum class Backend { Hip, Cpu, Omp };
+enum class TimeFormat { Auto, Cuda, Mpi, Both };
+
+struct CliConfig {
+  std::string image;
+  int64_t width = 0, height = 0;
+  int reps = 0;
+  Channels channels = Channels::Grey;
+
+  Backend backend = Backend::Hip;
+  int gpus = 1;
+  std::string filter = "gaussian";
+  int halo = 0;   // 0 = auto
+  int fuse = 0;   // 0 = auto
+  bool overlap = true;
+  bool graph = false;
+  KernelVariant variant = KernelVariant::Auto;
+  std::string out;  // "" = blur_<name>
+  bool synthetic = false;
+  uint64_t seed = 0;
+  bool check = false;
+  bool json = false;
+  int threads = 0;
+  TimeFormat format = TimeFormat::Auto;
+  int checkpoint_every = 0;
+  bool explain = false;
+  double timeout_s = 600.0;
+  bool quiet = false;
+};
+
+// Parse argv.  Throws pconv::Error with the message to print on bad input.
+CliConfig parse_cli(const std::vector<std::string>& args);
+// The reference usage text (cuda/functions.c:26 form).
+std::string usage_text(const std::string& prog);
+// Full option help.
+std::string help_text(const std::string& prog);
+
+}  // namespace pconv

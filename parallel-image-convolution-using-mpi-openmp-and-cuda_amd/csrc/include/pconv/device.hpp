@@ -1,0 +1,104 @@
+// HIP runtime layer: RAII device/pinned buffers, streams, events, checks.
+//
+// Replaces the reference's synchronous pageable copies, cudaMalloc inside the
+// timed region and deprecated cudaThreadSynchronize
+// (cuda/cuda_convolution.cu:56-101): buffers are allocated once and reused,
+// host staging is pinned (hipHostMalloc) so copies are async DMA, and all
+// ordering is expressed with streams + events.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <utility>
+
+#include "pconv/common.hpp"
+
+#define PCONV_HIP_CHECK(expr)                                                                  \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      ::pconv::raise_error(__FILE__, __LINE__, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+namespace pconv {
+
+int device_count();
+void set_device(int device);
+std::string device_name(int device);
+
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  explicit DeviceBuffer(size_t bytes);
+  ~DeviceBuffer();
+  DeviceBuffer(DeviceBuffer&& o) noexcept { *this = std::move(o); }
+  DeviceBuffer& operator=(DeviceBuffer&& o) noexcept;
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  uint8_t* data() const { return ptr_; }
+  size_t size() const { return bytes_; }
+
+ private:
+  uint8_t* ptr_ = nullptr;
+  size_t bytes_ = 0;
+};
+
+class PinnedBuffer {
+ public:
+  PinnedBuffer() = default;
+  explicit PinnedBuffer(size_t bytes);
+  ~PinnedBuffer();
+  PinnedBuffer(PinnedBuffer&& o) noexcept { *this = std::move(o); }
+  PinnedBuffer& operator=(PinnedBuffer&& o) noexcept;
+  PinnedBuffer(const PinnedBuffer&) = delete;
+  PinnedBuffer& operator=(const PinnedBuffer&) = delete;
+  uint8_t* data() const { return ptr_; }
+  size_t size() const { return bytes_; }
+
+ private:
+  uint8_t* ptr_ = nullptr;
+  size_t bytes_ = 0;
+};
+
+class Stream {
+ public:
+  Stream() = default;
+  static Stream create(int priority = 0);
+  ~Stream();
+  Stream(Stream&& o) noexcept : s_(o.s_) { o.s_ = nullptr; }
+  Stream& operator=(Stream&& o) noexcept {
+    std::swap(s_, o.s_);
+    return *this;
+  }
+  hipStream_t get() const { return s_; }
+  void sync() const;
+
+ private:
+  hipStream_t s_ = nullptr;
+};
+
+class Event {
+ public:
+  Event() = default;
+  static Event create(bool timing = false);
+  ~Event();
+  Event(Event&& o) noexcept : e_(o.e_) { o.e_ = nullptr; }
+  Event& operator=(Event&& o) noexcept {
+    std::swap(e_, o.e_);
+    return *this;
+  }
+  hipEvent_t get() const { return e_; }
+  void record(hipStream_t s) const;
+  void wait_on(hipStream_t s) const;  // make stream s wait for this event
+  void sync() const;
+  // milliseconds between two recorded timing events
+  static float elapsed_ms(const Event& a, const Event& b);
+
+ private:
+  hipEvent_t e_ = nullptr;
+};
+
+}  // namespace pconv

@@ -1,0 +1,162 @@
+// Device engine: one row band of the image resident on one GPU.
+//
+// Replaces GPU_convolution() (cuda/cuda_convolution.cu:49-102) and the MPI
+// rank's rep loop (mpi/mpi_convolution.c:151-240):
+//   * two device frames (ping-pong) with zero pad columns and `halo` ghost
+//     rows, allocated once and reused across runs (no malloc in the loop);
+//   * a compute stream and a communication stream; the interior launch of an
+//     exchange phase overlaps the halo exchange, the boundary launches wait on
+//     an event (schedule.hpp);
+//   * the newest result is always the `src` frame after a run — the reference
+//     copied back the stale buffer for odd reps;
+//   * optional hipGraph capture of a whole rep loop (launch-bound small images);
+//   * hipEvent loop timing + host wall timing per run.
+// A whole single-GPU image is simply the band {y0=0, rows=H, no neighbours}.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <map>
+#include <memory>
+#include <tuple>
+#include <vector>
+
+#include "pconv/device.hpp"
+#include "pconv/filter.hpp"
+#include "pconv/image.hpp"
+#include "pconv/kernels.hpp"
+#include "pconv/partition.hpp"
+#include "pconv/schedule.hpp"
+
+namespace pconv {
+
+class BandEngine;
+
+// Moves ghost rows between bands.  `exchange` is enqueued on `stream` and
+// must fill ghost rows [-depth, 0) from band.up and [rows, rows+depth) from
+// band.down of engine.src_frame(), sending the matching owned rows.
+class HaloTransport {
+ public:
+  virtual ~HaloTransport() = default;
+  virtual void exchange(BandEngine& e, int64_t depth, hipStream_t stream) = 0;
+  virtual const char* name() const = 0;
+};
+
+struct EngineOptions {
+  int device = 0;
+  int halo_depth = 1;      // D
+  int fuse = 1;            // T (reps per launch; > 1 needs the temporal kernel)
+  bool overlap = true;     // interior || halo
+  bool use_graph = false;  // capture the rep loop into a hipGraph (no transport)
+  KernelVariant variant = KernelVariant::Auto;
+};
+
+struct RunStats {
+  double loop_ms = 0;      // hipEvent time of the rep loop (device)
+  double wall_ms = 0;      // host wall time of the enqueue+sync
+  int launches = 0;
+  int exchanges = 0;
+};
+
+class BandEngine {
+ public:
+  BandEngine(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt);
+  ~BandEngine();
+
+  const ImageGeom& geom() const { return geom_; }
+  const Band& band() const { return band_; }
+  const Filter& filter() const { return filter_; }
+  const FrameLayout& layout() const { return lay_; }
+  const EngineOptions& options() const { return opt_; }
+  hipStream_t compute_stream() const { return cs_.get(); }
+  hipStream_t comm_stream() const { return ms_.get(); }
+
+  void set_transport(std::shared_ptr<HaloTransport> t) { transport_ = std::move(t); }
+
+  // Frame pointers at (owned row 0, data column 0).
+  uint8_t* src_frame() const { return frame_[cur_].data() + lay_.offset(0); }
+  uint8_t* dst_frame() const { return frame_[cur_ ^ 1].data() + lay_.offset(0); }
+
+  // Copy frame-local rows [r_begin, r_end) from host (pointer at row r_begin).
+  // Rows in the ghost zone are accepted (pre-loaded halos).  Async on the
+  // compute stream; `host` should be pinned for true async DMA.
+  void upload_rows(const uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end);
+  // Same from a device pointer (e.g. a torch CUDA tensor).
+  void upload_rows_device(const uint8_t* dev, int64_t dev_pitch, int64_t r_begin, int64_t r_end);
+  // Declare whether the ghost rows currently hold valid neighbour data.
+  void set_halo_valid(bool v) { halo_valid_ = v; }
+  // Copy owned rows [r_begin, r_end) of the newest result to host / device.
+  void download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end);
+  void download_rows_device(uint8_t* dev, int64_t dev_pitch, int64_t r_begin, int64_t r_end);
+
+  // Make the compute stream wait for work already queued on `s` / make `s`
+  // wait for everything queued on the compute stream.
+  void wait_stream(hipStream_t s);
+  void signal_stream(hipStream_t s);
+
+  // Enqueue `reps` repetitions (async).  stats filled after synchronize().
+  void run(int reps);
+  // Phase-by-phase execution for multi-band emulation on one device.
+  std::vector<Phase> plan(int reps) const;
+  void exec_exchange(const Phase& p);
+  void exec_compute(const Phase& p);
+
+  void synchronize();
+  const RunStats& last_stats() const { return stats_; }
+
+  // Zero both frames (ghost rows, pads and data).
+  void clear();
+
+ private:
+  void enqueue_phase(const Phase& p);
+  void launch(const LaunchSpec& l, hipStream_t s);
+
+  ImageGeom geom_;
+  Band band_;
+  Filter filter_;
+  EngineOptions opt_;
+  FrameLayout lay_;
+  DeviceBuffer frame_[2];
+  int cur_ = 0;
+  bool halo_valid_ = false;
+  Stream cs_, ms_;
+  Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_;
+  std::shared_ptr<HaloTransport> transport_;
+  RunStats stats_;
+  double wall_t0_ = 0;
+  bool timing_pending_ = false;
+  // hipGraph cache: (reps, start buffer) -> executable graph
+  std::map<std::pair<int, int>, hipGraphExec_t> graphs_;
+};
+
+// N row bands of one image on ONE device, halos moved by D2D copies.  Used to
+// validate the decomposition + schedule on a 1-GPU box: the
+// result must equal the single-band result bit for bit.
+class LocalCluster {
+ public:
+  LocalCluster(const ImageGeom& geom, int bands, const Filter& filter, const EngineOptions& opt);
+  int size() const { return static_cast<int>(engines_.size()); }
+  BandEngine& engine(int i) { return *engines_.at(i); }
+  // Host image (contiguous) in/out.
+  void upload(const uint8_t* host, bool preload_halo);
+  void run(int reps);
+  void download(uint8_t* host);
+  void synchronize();
+
+ private:
+  ImageGeom geom_;
+  std::vector<std::unique_ptr<BandEngine>> engines_;
+};
+
+// Transport used by LocalCluster (neighbour engines live on the same device).
+class LocalTransport : public HaloTransport {
+ public:
+  explicit LocalTransport(std::vector<BandEngine*> peers) : peers_(std::move(peers)) {}
+  void exchange(BandEngine& e, int64_t depth, hipStream_t stream) override;
+  const char* name() const override { return "local-d2d"; }
+
+ private:
+  std::vector<BandEngine*> peers_;
+};
+
+}  // namespace pconv

@@ -1,0 +1,64 @@
+// Device stencil kernels (CDNA4 / gfx950) — host-side launch interface.
+//
+// Reference kernels: kernelConvolutionforGrey / kernelConvolutionforRGB
+// (cuda/cuda_convolution.cu:9-47): one thread per pixel with lanes walking
+// down ROWS (uncoalesced), FP64 /16.0, border ring never written, RGB grid 3x
+// too wide with out-of-bounds accesses.
+//
+// pconv kernels treat a row as a byte vector (RGB = 3W bytes, horizontal tap
+// stride = CH bytes), so one template serves grey/RGB/RGBA:
+//   * lanes walk along a row, 16 bytes per lane (dwordx4 loads/stores);
+//   * the gaussian runs in packed 16-bit integer SIMD (v_perm_b32 byte
+//     unpack, v_pk_add_u16 / v_pk_mad_u16, shift, v_perm_b32 repack), exactly
+//     reproducing the float32 reference;
+//   * each lane marches down RPT rows keeping the horizontal sums of the last
+//     two rows in registers (every input row is loaded and unpacked once);
+//   * the temporal-blocked kernel fuses `steps` repetitions in one launch
+//     (see stencil_temporal in kernels.hip).
+// The frame's zero pad (image.hpp) provides the boundary; no edge branches.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+#include "pconv/filter.hpp"
+#include "pconv/image.hpp"
+
+namespace pconv {
+
+struct StencilLaunch {
+  const uint8_t* src = nullptr;  // frame: owned row 0, data column 0
+  uint8_t* dst = nullptr;        // same layout as src
+  int64_t pitch = 0;
+  int64_t row_bytes = 0;
+  int64_t r0 = 0, r1 = 0;        // output rows [r0, r1) in frame-local numbering
+  int64_t frame_lo = 0;          // first readable frame row (= -halo)
+  int64_t frame_hi = 0;          // one past the last readable frame row (= rows + halo)
+  int steps = 1;                 // fused repetitions (temporal blocking) in this launch
+  int64_t g_row0 = 0;            // global image row of frame row 0
+  int64_t height = 0;            // global image height (rows outside are zero each step)
+};
+
+enum class KernelVariant : int {
+  Auto = 0,      // pick by filter / steps
+  Binomial = 1,  // packed-u16 gaussian, 1 step per launch
+  Temporal = 2,  // packed-u16 gaussian, `steps` fused in registers
+  Int9 = 3,      // generic int-exact 9-tap
+  Float9 = 4,    // generic float32 9-tap (reference rounding)
+};
+
+const char* kernel_variant_name(KernelVariant v);
+
+// Largest `steps` the temporal kernel accepts.
+constexpr int kMaxFusedSteps = 16;
+
+// Enqueue one stencil launch on `stream`.  Validates the geometry against the
+// frame before launching (no out-of-frame access is possible).
+void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream,
+                    KernelVariant v = KernelVariant::Auto);
+
+// Whether `v` (or Auto) can fuse `steps` > 1 for this filter.
+bool supports_fusion(const Filter& f, KernelVariant v);
+
+}  // namespace pconv

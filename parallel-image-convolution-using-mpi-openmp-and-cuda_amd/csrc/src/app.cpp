@@ -1,0 +1,371 @@
+// `conv` application (see app.hpp).
+#include "pconv/app.hpp"
+
+#include <sys/mman.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cinttypes>
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+#include <thread>
+
+#include "pconv/cpu_stencil.hpp"
+#include "pconv/device.hpp"
+#include "pconv/engine.hpp"
+#include "pconv/raw_io.hpp"
+#include "pconv/rccl_comm.hpp"
+
+namespace pconv {
+
+namespace {
+
+constexpr int kMaxRanks = 64;
+constexpr int kAutoHaloCap = 64;
+
+ImageGeom geom_of(const CliConfig& c) {
+  ImageGeom g;
+  g.width = c.width;
+  g.height = c.height;
+  g.channels = c.channels;
+  g.validate();
+  return g;
+}
+
+std::string out_path(const CliConfig& c) { return c.out.empty() ? output_path_for(c.image) : c.out; }
+
+void load_rows(const CliConfig& c, const ImageGeom& g, int64_t y0, int64_t rows, uint8_t* dst, int64_t pitch) {
+  if (c.synthetic)
+    synth_rows(g, c.seed, y0, rows, dst, pitch);
+  else
+    read_rows(c.image, g, y0, rows, dst, pitch);
+}
+
+EngineOptions engine_options(const CliConfig& c, const ImageGeom& g, int world, int device) {
+  const Filter f = Filter::by_name(c.filter);
+  EngineOptions o;
+  o.device = device;
+  o.variant = c.variant;
+  o.overlap = c.overlap;
+  o.use_graph = c.graph && world == 1;
+  const bool fusable = supports_fusion(f, c.variant);
+  o.fuse = c.fuse > 0 ? c.fuse : (fusable ? 8 : 1);
+  if (!fusable) o.fuse = 1;
+  o.fuse = std::max(1, std::min(o.fuse, std::max(1, c.reps)));
+  if (c.halo > 0) {
+    o.halo_depth = c.halo;
+  } else if (world > 1) {
+    // Deep ghost zone: fewest exchanges, bounded redundant compute.
+    const int64_t min_rows = g.height / world;
+    o.halo_depth = static_cast<int>(std::min<int64_t>({std::max(1, c.reps), kAutoHaloCap, min_rows}));
+  } else {
+    o.halo_depth = o.fuse;
+  }
+  o.halo_depth = std::max(o.halo_depth, o.fuse);
+  return o;
+}
+
+int64_t compare_with_oracle(const CliConfig& c, const ImageGeom& g, const uint8_t* result) {
+  std::vector<uint8_t> in(static_cast<size_t>(g.bytes())), ref(static_cast<size_t>(g.bytes()));
+  load_rows(c, g, 0, g.height, in.data(), g.row_bytes());
+  cpu_convolve(Filter::by_name(c.filter), g, in.data(), ref.data(), c.reps, CpuBackend::OpenMP, c.threads);
+  int64_t bad = 0;
+  for (size_t i = 0; i < ref.size(); ++i) bad += ref[i] != result[i];
+  return bad;
+}
+
+// ------------------------------------------------------------------ CPU
+AppReport run_cpu(const CliConfig& c) {
+  const double t0 = wall_seconds();
+  const ImageGeom g = geom_of(c);
+  if (!c.synthetic) validate_input_file(c.image, g);
+  std::vector<uint8_t> img(static_cast<size_t>(g.bytes()));
+  load_rows(c, g, 0, g.height, img.data(), g.row_bytes());
+  const Filter f = Filter::by_name(c.filter);
+  const CpuBackend be = c.backend == Backend::Omp ? CpuBackend::OpenMP : CpuBackend::Serial;
+  AppReport r;
+  r.kernel = be == CpuBackend::OpenMP ? "cpu-omp" : "cpu-serial";
+  const double l0 = wall_seconds();
+  int done = 0;
+  const int chunk = c.checkpoint_every > 0 ? c.checkpoint_every : std::max(1, c.reps);
+  while (done < c.reps) {
+    const int k = std::min(chunk, c.reps - done);
+    cpu_convolve(f, g, img.data(), img.data(), k, be, c.threads);
+    done += k;
+    if (c.checkpoint_every > 0 && done < c.reps) write_image(out_path(c) + ".rep" + std::to_string(done), g, img.data());
+  }
+  r.loop_s = wall_seconds() - l0;
+  r.output = out_path(c);
+  write_image(r.output, g, img.data());
+  if (c.check) r.mismatches = compare_with_oracle(c, g, img.data());
+  r.e2e_s = wall_seconds() - t0;
+  return r;
+}
+
+// ------------------------------------------------------------------ 1 GPU
+AppReport run_gpu1(const CliConfig& c) {
+  const double t0 = wall_seconds();
+  const ImageGeom g = geom_of(c);
+  if (!c.synthetic) validate_input_file(c.image, g);
+  const Filter f = Filter::by_name(c.filter);
+  set_device(0);
+  PinnedBuffer host(static_cast<size_t>(g.bytes()));
+  load_rows(c, g, 0, g.height, host.data(), g.row_bytes());
+  const EngineOptions o = engine_options(c, g, 1, 0);
+  BandEngine eng(g, row_band(g.height, 1, 0), f, o);
+  if (c.explain) std::fprintf(stderr, "%s", describe_plan(eng.plan(c.reps)).c_str());
+  eng.upload_rows(host.data(), g.row_bytes(), 0, g.height);
+  eng.synchronize();
+  AppReport r;
+  r.output = out_path(c);
+  const double l0 = wall_seconds();
+  int done = 0;
+  const int chunk = c.checkpoint_every > 0 ? c.checkpoint_every : std::max(1, c.reps);
+  while (done < c.reps) {
+    const int k = std::min(chunk, c.reps - done);
+    eng.run(k);
+    eng.synchronize();
+    r.launches += eng.last_stats().launches;
+    done += k;
+    if (c.checkpoint_every > 0 && done < c.reps) {
+      eng.download_rows(host.data(), g.row_bytes(), 0, g.height);
+      eng.synchronize();
+      write_image(r.output + ".rep" + std::to_string(done), g, host.data());
+    }
+  }
+  r.loop_s = wall_seconds() - l0;
+  eng.download_rows(host.data(), g.row_bytes(), 0, g.height);
+  eng.synchronize();
+  write_image(r.output, g, host.data());
+  r.e2e_s = wall_seconds() - t0;
+  r.halo = eng.options().halo_depth;
+  r.fuse = eng.options().fuse;
+  r.kernel = kernel_variant_name(eng.options().variant);
+  if (c.check) r.mismatches = compare_with_oracle(c, g, host.data());
+  return r;
+}
+
+// ------------------------------------------------------------------ N GPUs
+struct SharedState {
+  std::atomic<int> id_ready;
+  uint8_t id[kUniqueIdBytes];
+  std::atomic<int> arrived;
+  std::atomic<int> generation;
+  std::atomic<int> failed;
+  double loop_s[kMaxRanks];
+  int launches[kMaxRanks];
+  int exchanges[kMaxRanks];
+  char error[512];
+};
+
+void shm_barrier(SharedState* s, int world, double timeout_s) {
+  const int gen = s->generation.load();
+  if (s->arrived.fetch_add(1) + 1 == world) {
+    s->arrived.store(0);
+    s->generation.fetch_add(1);
+    return;
+  }
+  const double t0 = wall_seconds();
+  while (s->generation.load() == gen) {
+    if (s->failed.load()) PCONV_FAIL("peer rank failed");
+    if (wall_seconds() - t0 > timeout_s) PCONV_FAIL("barrier timed out");
+    std::this_thread::yield();
+  }
+}
+
+void run_rank(const CliConfig& c, SharedState* sh, int rank) {
+  set_error_rank(rank);
+  const ImageGeom g = geom_of(c);
+  const int world = c.gpus;
+  const int ndev = device_count();
+  PCONV_CHECK(ndev >= world, "need " + std::to_string(world) + " GPUs, " + std::to_string(ndev) + " visible");
+  const int device = rank;
+  set_device(device);
+  const Filter f = Filter::by_name(c.filter);
+  const Band b = row_band(g.height, world, rank);
+  const EngineOptions o = engine_options(c, g, world, device);
+  BandEngine eng(g, b, f, o);
+  if (c.explain && rank == 0) std::fprintf(stderr, "%s", describe_plan(eng.plan(c.reps)).c_str());
+  const int64_t d = eng.layout().halo;
+  // Ghost rows come straight from the file (free here): first phase needs no exchange.
+  const int64_t above = std::min<int64_t>(d, b.y0);
+  const int64_t below = std::min<int64_t>(d, g.height - (b.y0 + b.rows));
+  const int64_t rb = g.row_bytes();
+  PinnedBuffer host(static_cast<size_t>((b.rows + above + below) * rb));
+  load_rows(c, g, b.y0 - above, b.rows + above + below, host.data(), rb);
+
+  if (rank == 0) {
+    const auto id = rccl_unique_id();
+    std::memcpy(sh->id, id.data(), kUniqueIdBytes);
+    sh->id_ready.store(1);
+  } else {
+    const double t0 = wall_seconds();
+    while (!sh->id_ready.load()) {
+      if (sh->failed.load()) PCONV_FAIL("peer rank failed");
+      if (wall_seconds() - t0 > c.timeout_s) PCONV_FAIL("timed out waiting for the RCCL unique id");
+      std::this_thread::yield();
+    }
+  }
+  std::vector<uint8_t> id(sh->id, sh->id + kUniqueIdBytes);
+  auto comm = std::make_shared<RcclComm>(id, rank, world, device);
+  eng.set_transport(std::make_shared<RcclTransport>(comm));
+
+  eng.upload_rows(host.data(), rb, -above, b.rows + below);
+  eng.set_halo_valid(true);
+  eng.synchronize();
+  shm_barrier(sh, world, c.timeout_s);  // MPI_Barrier before the timer (mpi_convolution.c:151)
+  const double l0 = wall_seconds();
+  eng.run(c.reps);
+  comm->wait(eng.compute_stream(), c.timeout_s);
+  comm->wait(eng.comm_stream(), c.timeout_s);
+  eng.synchronize();
+  sh->loop_s[rank] = wall_seconds() - l0;
+  sh->launches[rank] = eng.last_stats().launches;
+  sh->exchanges[rank] = eng.last_stats().exchanges;
+  eng.download_rows(host.data(), rb, 0, b.rows);
+  eng.synchronize();
+  write_rows(out_path(c), g, b.y0, b.rows, host.data(), rb);
+  shm_barrier(sh, world, c.timeout_s);
+}
+
+AppReport run_multi(const CliConfig& c) {
+  const double t0 = wall_seconds();
+  const ImageGeom g = geom_of(c);
+  PCONV_CHECK(c.gpus <= kMaxRanks, "too many ranks");
+  PCONV_CHECK(g.height >= c.gpus, "image has fewer rows than ranks");
+  if (!c.synthetic) validate_input_file(c.image, g);
+  create_output(out_path(c), g);  // sized + truncated once, ranks pwrite their bands
+  void* mem = mmap(nullptr, sizeof(SharedState), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+  PCONV_CHECK(mem != MAP_FAILED, "mmap shared state failed");
+  auto* sh = new (mem) SharedState();
+  sh->id_ready = 0;
+  sh->arrived = 0;
+  sh->generation = 0;
+  sh->failed = 0;
+  std::fflush(stdout);
+  std::fflush(stderr);
+  std::vector<pid_t> kids;
+  for (int r = 0; r < c.gpus; ++r) {
+    const pid_t pid = fork();
+    PCONV_CHECK(pid >= 0, "fork failed");
+    if (pid == 0) {
+      int code = 0;
+      try {
+        run_rank(c, sh, r);
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "%s\n", e.what());
+        if (!sh->failed.exchange(1)) std::snprintf(sh->error, sizeof(sh->error), "%s", e.what());
+        code = 1;
+      }
+      std::fflush(stdout);
+      std::fflush(stderr);
+      _exit(code);
+    }
+    kids.push_back(pid);
+  }
+  bool ok = true;
+  for (pid_t p : kids) {
+    int st = 0;
+    waitpid(p, &st, 0);
+    ok = ok && WIFEXITED(st) && WEXITSTATUS(st) == 0;
+  }
+  AppReport r;
+  r.gpus = c.gpus;
+  r.output = out_path(c);
+  if (!ok) {
+    std::string msg = sh->error[0] ? sh->error : "a worker process died";
+    munmap(mem, sizeof(SharedState));
+    PCONV_FAIL("multi-GPU run failed: " + msg);
+  }
+  for (int i = 0; i < c.gpus; ++i) {
+    r.loop_s = std::max(r.loop_s, sh->loop_s[i]);  // max over ranks, like the reference
+    r.launches = std::max(r.launches, sh->launches[i]);
+    r.exchanges = std::max(r.exchanges, sh->exchanges[i]);
+  }
+  munmap(mem, sizeof(SharedState));
+  const EngineOptions o = engine_options(c, g, c.gpus, 0);
+  r.halo = o.halo_depth;
+  r.fuse = o.fuse;
+  r.kernel = kernel_variant_name(o.variant);
+  if (c.check) {
+    std::vector<uint8_t> out(static_cast<size_t>(g.bytes()));
+    read_image(r.output, g, out.data());
+    r.mismatches = compare_with_oracle(c, g, out.data());
+  }
+  r.e2e_s = wall_seconds() - t0;
+  return r;
+}
+
+}  // namespace
+
+AppReport run_app(const CliConfig& c) {
+  AppReport r;
+  if (c.backend != Backend::Hip)
+    r = run_cpu(c);
+  else if (c.gpus > 1)
+    r = run_multi(c);
+  else
+    r = run_gpu1(c);
+  r.gpus = c.backend == Backend::Hip ? c.gpus : 0;
+  const double px = static_cast<double>(c.width) * static_cast<double>(c.height) * c.reps;
+  r.mpix_per_s = r.loop_s > 0 ? px / r.loop_s / 1e6 : 0.0;
+  return r;
+}
+
+std::string report_json(const CliConfig& c, const AppReport& r) {
+  std::ostringstream os;
+  const double px = static_cast<double>(c.width) * static_cast<double>(c.height) * c.reps;
+  os << "{\"width\": " << c.width << ", \"height\": " << c.height << ", \"channels\": \""
+     << channels_name(c.channels) << "\", \"reps\": " << c.reps << ", \"filter\": \"" << c.filter
+     << "\", \"backend\": \"" << (c.backend == Backend::Hip ? "hip" : c.backend == Backend::Omp ? "omp" : "cpu")
+     << "\", \"gpus\": " << r.gpus << ", \"kernel\": \"" << r.kernel << "\", \"halo\": " << r.halo
+     << ", \"fuse\": " << r.fuse << ", \"launches\": " << r.launches << ", \"exchanges\": " << r.exchanges
+     << ", \"loop_s\": " << r.loop_s << ", \"e2e_s\": " << r.e2e_s << ", \"loop_mpix_per_s\": " << r.mpix_per_s
+     << ", \"e2e_mpix_per_s\": " << (r.e2e_s > 0 ? px / r.e2e_s / 1e6 : 0.0)
+     << ", \"mismatches\": " << r.mismatches << ", \"output\": \"" << r.output << "\"}";
+  return os.str();
+}
+
+int conv_main(int argc, char** argv) {
+  std::vector<std::string> args(argv, argv + argc);
+  const std::string prog = argc > 0 ? argv[0] : "conv";
+  for (const auto& a : args)
+    if (a == "-h" || a == "--help") {
+      std::fputs(help_text(prog).c_str(), stdout);
+      return 0;
+    }
+  CliConfig c;
+  try {
+    c = parse_cli(args);
+  } catch (const Error& e) {
+    const std::string m = e.what();
+    if (m.size() >= 5 && m.compare(m.size() - 5, 5, "usage") == 0)
+      std::fputs(usage_text(prog).c_str(), stderr);
+    else
+      std::fprintf(stderr, "%s: %s\n%s", prog.c_str(), m.c_str(), usage_text(prog).c_str());
+    return EXIT_FAILURE;
+  }
+  try {
+    const AppReport r = run_app(c);
+    if (!c.quiet) {
+      TimeFormat fmt = c.format;
+      if (fmt == TimeFormat::Auto) fmt = (c.backend == Backend::Hip && c.gpus == 1) ? TimeFormat::Cuda : TimeFormat::Mpi;
+      if (fmt == TimeFormat::Mpi || fmt == TimeFormat::Both) std::printf("%f\n", r.loop_s);
+      if (fmt == TimeFormat::Cuda || fmt == TimeFormat::Both) std::printf("Execution time: %.3f sec\n", r.e2e_s);
+    }
+    if (c.json) std::printf("%s\n", report_json(c, r).c_str());
+    if (c.check) {
+      std::fprintf(stderr, "check: %" PRId64 " mismatching bytes vs CPU oracle\n", r.mismatches);
+      if (r.mismatches != 0) return 2;
+    }
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "%s: %s\n", prog.c_str(), e.what());
+    return EXIT_FAILURE;
+  }
+  return EXIT_SUCCESS;
+}
+
+}  // namespace pconv

@@ -1,0 +1,133 @@
+// CLI parsing (see cli.hpp).
+#include "pconv/cli.hpp"
+
+#include <cerrno>
+#include <climits>
+#include <cstdlib>
+
+namespace pconv {
+
+namespace {
+
+int64_t parse_int(const std::string& s, const char* what, int64_t lo, int64_t hi) {
+  if (s.empty()) PCONV_FAIL(std::string("invalid ") + what + ": empty");
+  errno = 0;
+  char* end = nullptr;
+  const long long v = std::strtoll(s.c_str(), &end, 10);
+  if (errno != 0 || end == s.c_str() || *end != '\0')
+    PCONV_FAIL(std::string("invalid ") + what + " '" + s + "': not an integer");
+  if (v < lo || v > hi)
+    PCONV_FAIL(std::string("invalid ") + what + " '" + s + "': must be in [" + std::to_string(lo) + ", " +
+               std::to_string(hi) + "]");
+  return v;
+}
+
+}  // namespace
+
+std::string usage_text(const std::string& prog) {
+  return "Error Input!\n" + prog + " image_name width height repetitions [rgb/grey].\n";
+}
+
+std::string help_text(const std::string& prog) {
+  return "usage: " + prog +
+         " image.raw width height repetitions {grey,rgb,rgba} [options]\n"
+         "  --backend {hip,cpu,omp}   compute backend (default hip)\n"
+         "  --gpus N                  row-band decomposition over N GPUs, one process each (RCCL halos)\n"
+         "  --filter {gaussian,box,edge}  3x3 filter (default gaussian)\n"
+         "  --halo D                  ghost rows exchanged at once (default: auto)\n"
+         "  --fuse T                  repetitions fused per kernel launch (default: auto)\n"
+         "  --no-overlap              do not overlap halo exchange with interior compute\n"
+         "  --graph                   capture the repetition loop in a hipGraph (1 GPU)\n"
+         "  --kernel {auto,binomial,temporal,int9,float9}\n"
+         "  --out PATH                output file (default: blur_<image> next to the input)\n"
+         "  --synthetic SEED          use a deterministic random image instead of reading the file\n"
+         "  --check                   verify the result against the CPU oracle\n"
+         "  --json                    print a JSON metrics line\n"
+         "  --threads N               OpenMP threads for --backend omp\n"
+         "  --format {cuda,mpi,both}  timing line(s) to print (default: cuda for 1 GPU, mpi otherwise)\n"
+         "  --checkpoint-every K      write <out>.rep<N> every K repetitions\n"
+         "  --explain                 print the halo/launch schedule\n"
+         "  --timeout S               RCCL watchdog timeout in seconds (default 600)\n"
+         "  --quiet                   suppress the timing lines\n";
+}
+
+CliConfig parse_cli(const std::vector<std::string>& args) {
+  // Reference contract: argc == 6 and argv[5] in {grey, rgb}; anything else
+  // prints usage_text and exits with EXIT_FAILURE.
+  if (args.size() < 6) PCONV_FAIL("usage");
+  CliConfig c;
+  c.image = args[1];
+  const std::string& type = args[5];
+  if (type != "grey" && type != "rgb" && type != "rgba") PCONV_FAIL("usage");
+  c.channels = parse_channels(type);
+  c.width = parse_int(args[2], "width", 1, int64_t(1) << 30);
+  c.height = parse_int(args[3], "height", 1, int64_t(1) << 30);
+  c.reps = static_cast<int>(parse_int(args[4], "repetitions", 0, INT_MAX));
+  for (size_t i = 6; i < args.size(); ++i) {
+    const std::string& a = args[i];
+    auto next = [&](const char* what) -> std::string {
+      if (i + 1 >= args.size()) PCONV_FAIL(std::string("missing value for ") + what);
+      return args[++i];
+    };
+    if (a == "--backend") {
+      const std::string v = next("--backend");
+      if (v == "hip") c.backend = Backend::Hip;
+      else if (v == "cpu") c.backend = Backend::Cpu;
+      else if (v == "omp") c.backend = Backend::Omp;
+      else PCONV_FAIL("invalid --backend '" + v + "' (hip|cpu|omp)");
+    } else if (a == "--gpus") {
+      c.gpus = static_cast<int>(parse_int(next("--gpus"), "--gpus", 1, 64));
+    } else if (a == "--filter") {
+      c.filter = next("--filter");
+      if (c.filter != "gaussian" && c.filter != "box" && c.filter != "edge")
+        PCONV_FAIL("invalid --filter '" + c.filter + "' (gaussian|box|edge)");
+    } else if (a == "--halo") {
+      c.halo = static_cast<int>(parse_int(next("--halo"), "--halo", 1, 1 << 20));
+    } else if (a == "--fuse") {
+      c.fuse = static_cast<int>(parse_int(next("--fuse"), "--fuse", 1, kMaxFusedSteps));
+    } else if (a == "--no-overlap") {
+      c.overlap = false;
+    } else if (a == "--graph") {
+      c.graph = true;
+    } else if (a == "--kernel") {
+      const std::string v = next("--kernel");
+      if (v == "auto") c.variant = KernelVariant::Auto;
+      else if (v == "binomial") c.variant = KernelVariant::Binomial;
+      else if (v == "temporal") c.variant = KernelVariant::Temporal;
+      else if (v == "int9") c.variant = KernelVariant::Int9;
+      else if (v == "float9") c.variant = KernelVariant::Float9;
+      else PCONV_FAIL("invalid --kernel '" + v + "'");
+    } else if (a == "--out") {
+      c.out = next("--out");
+    } else if (a == "--synthetic") {
+      c.synthetic = true;
+      c.seed = static_cast<uint64_t>(parse_int(next("--synthetic"), "--synthetic", 0, INT64_MAX));
+    } else if (a == "--check") {
+      c.check = true;
+    } else if (a == "--json") {
+      c.json = true;
+    } else if (a == "--threads") {
+      c.threads = static_cast<int>(parse_int(next("--threads"), "--threads", 1, 4096));
+    } else if (a == "--format") {
+      const std::string v = next("--format");
+      if (v == "cuda") c.format = TimeFormat::Cuda;
+      else if (v == "mpi") c.format = TimeFormat::Mpi;
+      else if (v == "both") c.format = TimeFormat::Both;
+      else PCONV_FAIL("invalid --format '" + v + "' (cuda|mpi|both)");
+    } else if (a == "--checkpoint-every") {
+      c.checkpoint_every = static_cast<int>(parse_int(next("--checkpoint-every"), "--checkpoint-every", 1, INT_MAX));
+    } else if (a == "--explain") {
+      c.explain = true;
+    } else if (a == "--timeout") {
+      c.timeout_s = static_cast<double>(parse_int(next("--timeout"), "--timeout", 1, 86400));
+    } else if (a == "--quiet") {
+      c.quiet = true;
+    } else {
+      PCONV_FAIL("unknown option '" + a + "'");
+    }
+  }
+  if (c.backend != Backend::Hip && c.gpus != 1) PCONV_FAIL("--gpus requires --backend hip");
+  return c;
+}
+
+}  // namespace pconv

@@ -1,0 +1,151 @@
+// CPU stencil oracle + OpenMP backend (see cpu_stencil.hpp).
+//
+// Compiled with -ffp-contract=off: the float path must be multiply-then-add
+// with one rounding each, in row-major tap order, like the x86 gcc reference
+// (mpi/mpi_convolution.c:303-307, :313-318).
+#include "pconv/cpu_stencil.hpp"
+
+#include <omp.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+namespace pconv {
+
+namespace {
+
+inline uint8_t sat_trunc(float v) {
+  // float -> uint8_t truncation; out-of-range values (only possible for custom
+  // filters with negative taps) saturate instead of the reference's UB.
+  if (!(v > 0.0f)) return 0;
+  if (v >= 255.0f) return 255;
+  return static_cast<uint8_t>(static_cast<int>(v));
+}
+
+template <int CH>
+void row_binomial(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* o, int64_t n) {
+  // (Σ tap·p) >> 4 with taps [1,2,1]⊗[1,2,1]: vertical then horizontal.
+  for (int64_t x = 0; x < n; ++x) {
+    const int l = a[x - CH] + 2 * b[x - CH] + c[x - CH];
+    const int m = a[x] + 2 * b[x] + c[x];
+    const int r = a[x + CH] + 2 * b[x + CH] + c[x + CH];
+    o[x] = static_cast<uint8_t>((l + 2 * m + r) >> 4);
+  }
+}
+
+template <int CH>
+void row_int(const Filter& f, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* o, int64_t n) {
+  const int* t = f.taps.data();
+  const int s = f.shift;
+  for (int64_t x = 0; x < n; ++x) {
+    const int acc = t[0] * a[x - CH] + t[1] * a[x] + t[2] * a[x + CH] + t[3] * b[x - CH] + t[4] * b[x] +
+                    t[5] * b[x + CH] + t[6] * c[x - CH] + t[7] * c[x] + t[8] * c[x + CH];
+    o[x] = static_cast<uint8_t>(std::min(acc >> s, 255));
+  }
+}
+
+template <int CH>
+void row_float(const Filter& f, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* o, int64_t n) {
+  const float* w = f.weights.data();
+  for (int64_t x = 0; x < n; ++x) {
+    const uint8_t* rows[3] = {a, b, c};
+    float acc = 0.0f;
+    for (int k = 0; k < 3; ++k)
+      for (int l = 0; l < 3; ++l) {
+        const float p = static_cast<float>(rows[k][x + (l - 1) * CH]);
+        const float prod = p * w[k * 3 + l];
+        acc = acc + prod;
+      }
+    o[x] = sat_trunc(acc);
+  }
+}
+
+template <int CH>
+void step_rows(const Filter& f, const FrameLayout& lay, const uint8_t* src, uint8_t* dst, int64_t r0, int64_t r1,
+               CpuBackend be) {
+  const int64_t n = lay.row_bytes;
+  auto body = [&](int64_t r) {
+    const uint8_t* a = src + lay.offset(r - 1);
+    const uint8_t* b = src + lay.offset(r);
+    const uint8_t* c = src + lay.offset(r + 1);
+    uint8_t* o = dst + lay.offset(r);
+    if (f.binomial121)
+      row_binomial<CH>(a, b, c, o, n);
+    else if (f.int_exact)
+      row_int<CH>(f, a, b, c, o, n);
+    else
+      row_float<CH>(f, a, b, c, o, n);
+  };
+  if (be == CpuBackend::OpenMP) {
+#pragma omp parallel for schedule(static)
+    for (int64_t r = r0; r < r1; ++r) body(r);
+  } else {
+    for (int64_t r = r0; r < r1; ++r) body(r);
+  }
+}
+
+}  // namespace
+
+void cpu_step(const Filter& f, Channels ch, const FrameLayout& lay, const uint8_t* src_frame, uint8_t* dst_frame,
+              int64_t r0, int64_t r1, CpuBackend be) {
+  PCONV_CHECK(r0 >= -lay.halo + 1 && r1 <= lay.rows + lay.halo - 1 && r0 <= r1, "cpu_step: rows out of frame");
+  switch (ch) {
+    case Channels::Grey: step_rows<1>(f, lay, src_frame, dst_frame, r0, r1, be); break;
+    case Channels::Rgb: step_rows<3>(f, lay, src_frame, dst_frame, r0, r1, be); break;
+    case Channels::Rgba: step_rows<4>(f, lay, src_frame, dst_frame, r0, r1, be); break;
+  }
+}
+
+void cpu_fused_launch(const Filter& f, Channels ch, const FrameLayout& lay, const uint8_t* src_frame,
+                      uint8_t* dst_frame, int64_t lo, int64_t hi, int steps, int64_t g_row0, int64_t height,
+                      CpuBackend be) {
+  PCONV_CHECK(steps >= 1 && lo <= hi, "cpu_fused_launch: bad arguments");
+  PCONV_CHECK(lo - steps >= -lay.halo && hi + steps <= lay.rows + lay.halo, "cpu_fused_launch: rows exceed frame");
+  if (lo == hi) return;
+  if (steps == 1) {
+    // Single step never writes rows outside the image: clip like the kernels' caller.
+    const int64_t a = std::max(lo, -g_row0), b = std::min(hi, height - g_row0);
+    if (a < b) cpu_step(f, ch, lay, src_frame, dst_frame, a, b, be);
+    return;
+  }
+  const size_t n = static_cast<size_t>(lay.bytes());
+  std::vector<uint8_t> A(src_frame, src_frame + n), B(src_frame, src_frame + n);
+  uint8_t* cur = A.data();
+  uint8_t* nxt = B.data();
+  for (int j = 1; j <= steps; ++j) {
+    const int64_t ext = steps - j;
+    const int64_t a = std::max(lo - ext, -g_row0), b = std::min(hi + ext, height - g_row0);
+    if (a < b) cpu_step(f, ch, lay, cur, nxt, a, b, be);
+    std::swap(cur, nxt);
+  }
+  for (int64_t r = lo; r < hi; ++r) {
+    const bool inside = g_row0 + r >= 0 && g_row0 + r < height;
+    if (inside)
+      std::memcpy(dst_frame + lay.offset(r), cur + lay.offset(r), lay.row_bytes);
+    else
+      std::memset(dst_frame + lay.offset(r), 0, lay.row_bytes);
+  }
+}
+
+void cpu_convolve(const Filter& f, const ImageGeom& geom, const uint8_t* in, uint8_t* out, int reps, CpuBackend be,
+                  int threads) {
+  geom.validate();
+  PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
+  const int64_t rb = geom.row_bytes();
+  const FrameLayout lay = FrameLayout::make(rb, geom.height, 1);
+  std::vector<uint8_t> fa(static_cast<size_t>(lay.bytes()), 0), fb(static_cast<size_t>(lay.bytes()), 0);
+  for (int64_t r = 0; r < geom.height; ++r) std::memcpy(fa.data() + lay.offset(r), in + r * rb, rb);
+  const int saved = omp_get_max_threads();
+  if (be == CpuBackend::OpenMP && threads > 0) omp_set_num_threads(threads);
+  uint8_t* src = fa.data();
+  uint8_t* dst = fb.data();
+  for (int t = 0; t < reps; ++t) {
+    cpu_step(f, geom.channels, lay, src, dst, 0, geom.height, be);
+    std::swap(src, dst);  // newest result is always in `src` (fixes SURVEY §A3)
+  }
+  if (be == CpuBackend::OpenMP && threads > 0) omp_set_num_threads(saved);
+  for (int64_t r = 0; r < geom.height; ++r) std::memcpy(out + r * rb, src + lay.offset(r), rb);
+}
+
+}  // namespace pconv

@@ -1,0 +1,93 @@
+// HIP runtime RAII wrappers (see device.hpp).
+#include "pconv/device.hpp"
+
+namespace pconv {
+
+int device_count() {
+  int n = 0;
+  PCONV_HIP_CHECK(hipGetDeviceCount(&n));
+  return n;
+}
+
+void set_device(int device) {
+  const int n = device_count();
+  PCONV_CHECK(device >= 0 && device < n,
+              "device " + std::to_string(device) + " out of range (" + std::to_string(n) + " visible)");
+  PCONV_HIP_CHECK(hipSetDevice(device));
+}
+
+std::string device_name(int device) {
+  hipDeviceProp_t p;
+  PCONV_HIP_CHECK(hipGetDeviceProperties(&p, device));
+  return std::string(p.name) + " (" + p.gcnArchName + ")";
+}
+
+DeviceBuffer::DeviceBuffer(size_t bytes) : bytes_(bytes) {
+  if (bytes) {
+    void* p = nullptr;
+    PCONV_HIP_CHECK(hipMalloc(&p, bytes));
+    ptr_ = static_cast<uint8_t*>(p);
+  }
+}
+
+DeviceBuffer::~DeviceBuffer() {
+  if (ptr_) (void)hipFree(ptr_);
+}
+
+DeviceBuffer& DeviceBuffer::operator=(DeviceBuffer&& o) noexcept {
+  std::swap(ptr_, o.ptr_);
+  std::swap(bytes_, o.bytes_);
+  return *this;
+}
+
+PinnedBuffer::PinnedBuffer(size_t bytes) : bytes_(bytes) {
+  if (bytes) {
+    void* p = nullptr;
+    PCONV_HIP_CHECK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    ptr_ = static_cast<uint8_t*>(p);
+  }
+}
+
+PinnedBuffer::~PinnedBuffer() {
+  if (ptr_) (void)hipHostFree(ptr_);
+}
+
+PinnedBuffer& PinnedBuffer::operator=(PinnedBuffer&& o) noexcept {
+  std::swap(ptr_, o.ptr_);
+  std::swap(bytes_, o.bytes_);
+  return *this;
+}
+
+Stream Stream::create(int priority) {
+  Stream s;
+  PCONV_HIP_CHECK(hipStreamCreateWithPriority(&s.s_, hipStreamNonBlocking, priority));
+  return s;
+}
+
+Stream::~Stream() {
+  if (s_) (void)hipStreamDestroy(s_);
+}
+
+void Stream::sync() const { PCONV_HIP_CHECK(hipStreamSynchronize(s_)); }
+
+Event Event::create(bool timing) {
+  Event e;
+  PCONV_HIP_CHECK(hipEventCreateWithFlags(&e.e_, timing ? hipEventDefault : hipEventDisableTiming));
+  return e;
+}
+
+Event::~Event() {
+  if (e_) (void)hipEventDestroy(e_);
+}
+
+void Event::record(hipStream_t s) const { PCONV_HIP_CHECK(hipEventRecord(e_, s)); }
+void Event::wait_on(hipStream_t s) const { PCONV_HIP_CHECK(hipStreamWaitEvent(s, e_, 0)); }
+void Event::sync() const { PCONV_HIP_CHECK(hipEventSynchronize(e_)); }
+
+float Event::elapsed_ms(const Event& a, const Event& b) {
+  float ms = 0.f;
+  PCONV_HIP_CHECK(hipEventElapsedTime(&ms, a.e_, b.e_));
+  return ms;
+}
+
+}  // namespace pconv

@@ -1,0 +1,275 @@
+// BandEngine / LocalCluster (see engine.hpp).
+#include "pconv/engine.hpp"
+
+#include <algorithm>
+#include <thread>
+
+namespace pconv {
+
+namespace {
+
+PlanConfig engine_plan_config(const ImageGeom& geom, const Band& band, const Filter& f, const EngineOptions& opt) {
+  PlanConfig c;
+  c.fuse = supports_fusion(f, opt.variant) ? opt.fuse : 1;
+  c.halo_depth = opt.halo_depth;
+  c.overlap = opt.overlap;
+  // Every rank must derive the same D and T: clamp against the smallest band.
+  const int64_t min_rows = band.world > 1 ? geom.height / band.world : 0;
+  return normalize_plan_config(c, min_rows, kMaxFusedSteps);
+}
+
+}  // namespace
+
+BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt)
+    : geom_(geom), band_(band), filter_(filter), opt_(opt) {
+  geom_.validate();
+  PCONV_CHECK(band.rows >= 1 && band.y0 >= 0 && band.y0 + band.rows <= geom.height, "band outside image");
+  const PlanConfig c = engine_plan_config(geom_, band_, filter_, opt_);
+  opt_.fuse = c.fuse;
+  opt_.halo_depth = c.halo_depth;
+  set_device(opt_.device);
+  lay_ = FrameLayout::make(geom_.row_bytes(), band_.rows, std::max(1, opt_.halo_depth));
+  for (auto& f : frame_) {
+    f = DeviceBuffer(static_cast<size_t>(lay_.bytes()));
+    PCONV_HIP_CHECK(hipMemset(f.data(), 0, f.size()));
+  }
+  cs_ = Stream::create(0);
+  ms_ = Stream::create(-1);  // communication gets the higher priority
+  ev_ready_ = Event::create();
+  ev_halo_ = Event::create();
+  ev_sync_ = Event::create();
+  ev_t0_ = Event::create(true);
+  ev_t1_ = Event::create(true);
+  PCONV_HIP_CHECK(hipDeviceSynchronize());
+}
+
+BandEngine::~BandEngine() {
+  for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+  if (cs_.get()) (void)hipStreamSynchronize(cs_.get());
+  if (ms_.get()) (void)hipStreamSynchronize(ms_.get());
+}
+
+void BandEngine::clear() {
+  synchronize();
+  for (auto& f : frame_) PCONV_HIP_CHECK(hipMemset(f.data(), 0, f.size()));
+  halo_valid_ = false;
+}
+
+void BandEngine::upload_rows(const uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end) {
+  PCONV_CHECK(r_begin >= -lay_.halo && r_end <= lay_.rows + lay_.halo && r_begin <= r_end,
+              "upload_rows: rows outside frame");
+  PCONV_CHECK(host_pitch >= lay_.row_bytes, "upload_rows: host pitch < row bytes");
+  // Rows beyond the global image edge must stay zero.
+  PCONV_CHECK(band_.y0 + r_begin >= 0 && band_.y0 + r_end <= geom_.height, "upload_rows: rows outside image");
+  if (r_end == r_begin) return;
+  PCONV_HIP_CHECK(hipMemcpy2DAsync(src_frame() + r_begin * lay_.pitch, lay_.pitch, host, host_pitch, lay_.row_bytes,
+                                   r_end - r_begin, hipMemcpyHostToDevice, cs_.get()));
+}
+
+void BandEngine::upload_rows_device(const uint8_t* dev, int64_t dev_pitch, int64_t r_begin, int64_t r_end) {
+  PCONV_CHECK(r_begin >= -lay_.halo && r_end <= lay_.rows + lay_.halo && r_begin <= r_end,
+              "upload_rows_device: rows outside frame");
+  PCONV_CHECK(band_.y0 + r_begin >= 0 && band_.y0 + r_end <= geom_.height, "upload_rows_device: rows outside image");
+  if (r_end == r_begin) return;
+  PCONV_HIP_CHECK(hipMemcpy2DAsync(src_frame() + r_begin * lay_.pitch, lay_.pitch, dev, dev_pitch, lay_.row_bytes,
+                                   r_end - r_begin, hipMemcpyDeviceToDevice, cs_.get()));
+}
+
+void BandEngine::download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end) {
+  PCONV_CHECK(r_begin >= 0 && r_end <= lay_.rows && r_begin <= r_end, "download_rows: rows outside band");
+  if (r_end == r_begin) return;
+  PCONV_HIP_CHECK(hipMemcpy2DAsync(host, host_pitch, src_frame() + r_begin * lay_.pitch, lay_.pitch, lay_.row_bytes,
+                                   r_end - r_begin, hipMemcpyDeviceToHost, cs_.get()));
+}
+
+void BandEngine::download_rows_device(uint8_t* dev, int64_t dev_pitch, int64_t r_begin, int64_t r_end) {
+  PCONV_CHECK(r_begin >= 0 && r_end <= lay_.rows && r_begin <= r_end, "download_rows_device: rows outside band");
+  if (r_end == r_begin) return;
+  PCONV_HIP_CHECK(hipMemcpy2DAsync(dev, dev_pitch, src_frame() + r_begin * lay_.pitch, lay_.pitch, lay_.row_bytes,
+                                   r_end - r_begin, hipMemcpyDeviceToDevice, cs_.get()));
+}
+
+void BandEngine::wait_stream(hipStream_t s) {
+  ev_sync_.record(s);
+  ev_sync_.wait_on(cs_.get());
+}
+
+void BandEngine::signal_stream(hipStream_t s) {
+  ev_sync_.record(cs_.get());
+  ev_sync_.wait_on(s);
+}
+
+std::vector<Phase> BandEngine::plan(int reps) const {
+  PlanConfig c = engine_plan_config(geom_, band_, filter_, opt_);
+  c.halo_preloaded = halo_valid_;
+  return plan_band(band_, reps, c);
+}
+
+void BandEngine::launch(const LaunchSpec& l, hipStream_t s) {
+  StencilLaunch a;
+  a.src = src_frame();
+  a.dst = dst_frame();
+  a.pitch = lay_.pitch;
+  a.row_bytes = lay_.row_bytes;
+  a.r0 = l.lo;
+  a.r1 = l.hi;
+  a.frame_lo = -lay_.halo;
+  a.frame_hi = lay_.rows + lay_.halo;
+  a.steps = l.steps;
+  a.g_row0 = band_.y0;
+  a.height = geom_.height;
+  launch_stencil(filter_, geom_.channels, a, s, opt_.variant);
+  ++stats_.launches;
+}
+
+void BandEngine::enqueue_phase(const Phase& p) {
+  if (p.exchange_depth > 0) {
+    PCONV_CHECK(transport_ != nullptr, "band has neighbours but no halo transport is attached");
+    ev_ready_.record(cs_.get());
+    ev_ready_.wait_on(ms_.get());
+    transport_->exchange(*this, p.exchange_depth, ms_.get());
+    ev_halo_.record(ms_.get());
+    for (const auto& l : p.launches)
+      if (!l.after_halo) launch(l, cs_.get());
+    ev_halo_.wait_on(cs_.get());
+    for (const auto& l : p.launches)
+      if (l.after_halo) launch(l, cs_.get());
+    ++stats_.exchanges;
+  } else {
+    for (const auto& l : p.launches) launch(l, cs_.get());
+  }
+  cur_ ^= 1;
+}
+
+void BandEngine::run(int reps) {
+  PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
+  const std::vector<Phase> ph = plan(reps);
+  stats_ = RunStats{};
+  wall_t0_ = wall_seconds();
+  ev_t0_.record(cs_.get());
+  const bool graph = opt_.use_graph && !transport_ && !ph.empty();
+  if (graph) {
+    const auto key = std::make_pair(reps, cur_);
+    auto it = graphs_.find(key);
+    const int start = cur_;
+    if (it == graphs_.end()) {
+      hipGraph_t g = nullptr;
+      PCONV_HIP_CHECK(hipStreamBeginCapture(cs_.get(), hipStreamCaptureModeThreadLocal));
+      for (const auto& p : ph) enqueue_phase(p);
+      PCONV_HIP_CHECK(hipStreamEndCapture(cs_.get(), &g));
+      hipGraphExec_t ex = nullptr;
+      PCONV_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      PCONV_HIP_CHECK(hipGraphDestroy(g));
+      it = graphs_.emplace(key, ex).first;
+    } else {
+      for (const auto& p : ph) {
+        stats_.launches += static_cast<int>(p.launches.size());
+        cur_ ^= 1;
+      }
+    }
+    (void)start;
+    PCONV_HIP_CHECK(hipGraphLaunch(it->second, cs_.get()));
+  } else {
+    for (const auto& p : ph) enqueue_phase(p);
+  }
+  ev_t1_.record(cs_.get());
+  timing_pending_ = true;
+  halo_valid_ = false;
+}
+
+void BandEngine::exec_exchange(const Phase& p) {
+  if (p.exchange_depth <= 0) return;
+  PCONV_CHECK(transport_ != nullptr, "band has neighbours but no halo transport is attached");
+  transport_->exchange(*this, p.exchange_depth, cs_.get());
+  ++stats_.exchanges;
+}
+
+void BandEngine::exec_compute(const Phase& p) {
+  for (const auto& l : p.launches) launch(l, cs_.get());
+  cur_ ^= 1;
+}
+
+void BandEngine::synchronize() {
+  cs_.sync();
+  ms_.sync();
+  if (timing_pending_) {
+    stats_.loop_ms = Event::elapsed_ms(ev_t0_, ev_t1_);
+    stats_.wall_ms = (wall_seconds() - wall_t0_) * 1e3;
+    timing_pending_ = false;
+  }
+}
+
+// --------------------------------------------------------------- LocalCluster
+
+void LocalTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream) {
+  const FrameLayout& L = e.layout();
+  const Band& b = e.band();
+  const int64_t pitch = L.pitch;
+  uint8_t* mine = e.src_frame() - kPadLeft;  // row 0, pitch-aligned start
+  if (b.up >= 0) {
+    BandEngine& p = *peers_.at(b.up);
+    PCONV_CHECK(p.layout().pitch == pitch && p.band().rows >= depth, "local halo: incompatible peer");
+    const uint8_t* from = p.src_frame() - kPadLeft + (p.band().rows - depth) * pitch;
+    PCONV_HIP_CHECK(hipMemcpyAsync(mine - depth * pitch, from, depth * pitch, hipMemcpyDeviceToDevice, stream));
+  }
+  if (b.down >= 0) {
+    BandEngine& p = *peers_.at(b.down);
+    PCONV_CHECK(p.layout().pitch == pitch && p.band().rows >= depth, "local halo: incompatible peer");
+    const uint8_t* from = p.src_frame() - kPadLeft;
+    PCONV_HIP_CHECK(hipMemcpyAsync(mine + b.rows * pitch, from, depth * pitch, hipMemcpyDeviceToDevice, stream));
+  }
+}
+
+LocalCluster::LocalCluster(const ImageGeom& geom, int bands, const Filter& filter, const EngineOptions& opt)
+    : geom_(geom) {
+  const auto bs = row_bands(geom.height, bands);
+  std::vector<BandEngine*> peers;
+  for (const auto& b : bs) {
+    engines_.push_back(std::make_unique<BandEngine>(geom, b, filter, opt));
+    peers.push_back(engines_.back().get());
+  }
+  auto t = std::make_shared<LocalTransport>(peers);
+  for (auto& e : engines_) e->set_transport(t);
+}
+
+void LocalCluster::upload(const uint8_t* host, bool preload_halo) {
+  const int64_t rb = geom_.row_bytes();
+  for (auto& e : engines_) {
+    const Band& b = e->band();
+    const int64_t d = e->layout().halo;
+    int64_t rb0 = 0, re = b.rows;
+    if (preload_halo) {
+      rb0 = -std::min<int64_t>(d, b.y0);
+      re = b.rows + std::min<int64_t>(d, geom_.height - (b.y0 + b.rows));
+    }
+    e->upload_rows(host + (b.y0 + rb0) * rb, rb, rb0, re);
+    e->set_halo_valid(preload_halo);
+  }
+  synchronize();
+}
+
+void LocalCluster::run(int reps) {
+  std::vector<std::vector<Phase>> plans;
+  for (auto& e : engines_) plans.push_back(e->plan(reps));
+  const size_t n = plans.front().size();
+  for (const auto& p : plans) PCONV_CHECK(p.size() == n, "local cluster: band plans diverge");
+  for (size_t i = 0; i < n; ++i) {
+    for (size_t k = 0; k < engines_.size(); ++k) engines_[k]->exec_exchange(plans[k][i]);
+    synchronize();
+    for (size_t k = 0; k < engines_.size(); ++k) engines_[k]->exec_compute(plans[k][i]);
+    synchronize();
+  }
+  for (auto& e : engines_) e->set_halo_valid(false);
+}
+
+void LocalCluster::download(uint8_t* host) {
+  const int64_t rb = geom_.row_bytes();
+  for (auto& e : engines_) e->download_rows(host + e->band().y0 * rb, rb, 0, e->band().rows);
+  synchronize();
+}
+
+void LocalCluster::synchronize() {
+  for (auto& e : engines_) e->synchronize();
+}
+
+}  // namespace pconv

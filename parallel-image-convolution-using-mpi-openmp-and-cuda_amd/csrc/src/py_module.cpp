@@ -1,0 +1,429 @@
+// Python bindings (pybind11) for the native engine: module `_pconv_native`.
+//
+// Buffers cross the boundary either as Python buffer-protocol objects (numpy
+// arrays, host memory) or as raw integer addresses (torch.Tensor.data_ptr()
+// of CUDA tensors or pinned host tensors) — no torch C++ ABI dependency.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "pconv/app.hpp"
+#include "pconv/cpu_stencil.hpp"
+#include "pconv/device.hpp"
+#include "pconv/engine.hpp"
+#include "pconv/kernels.hpp"
+#include "pconv/partition.hpp"
+#include "pconv/raw_io.hpp"
+#include "pconv/rccl_comm.hpp"
+#include "pconv/schedule.hpp"
+
+namespace py = pybind11;
+using namespace pconv;
+
+namespace {
+
+struct HostView {
+  uint8_t* ptr;
+  int64_t size;
+};
+
+HostView host_view(py::buffer b, bool writable) {
+  py::buffer_info info = b.request(writable);
+  PCONV_CHECK(info.itemsize == 1, "expected a uint8 buffer");
+  // Must be C-contiguous.
+  int64_t expect = 1;
+  for (int i = info.ndim - 1; i >= 0; --i) {
+    PCONV_CHECK(info.strides[i] == expect, "expected a C-contiguous buffer");
+    expect *= info.shape[i];
+  }
+  return {static_cast<uint8_t*>(info.ptr), static_cast<int64_t>(info.size)};
+}
+
+ImageGeom make_geom(int64_t w, int64_t h, const std::string& ch) {
+  ImageGeom g;
+  g.width = w;
+  g.height = h;
+  g.channels = parse_channels(ch);
+  g.validate();
+  return g;
+}
+
+KernelVariant parse_variant(const std::string& s) {
+  if (s == "auto") return KernelVariant::Auto;
+  if (s == "binomial") return KernelVariant::Binomial;
+  if (s == "temporal") return KernelVariant::Temporal;
+  if (s == "int9") return KernelVariant::Int9;
+  if (s == "float9") return KernelVariant::Float9;
+  PCONV_FAIL("unknown kernel variant '" + s + "'");
+}
+
+Filter make_filter(py::object f) {
+  if (py::isinstance<py::str>(f)) return Filter::by_name(f.cast<std::string>());
+  return f.cast<Filter>();
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_pconv_native, m) {
+  m.doc() = "pconv native engine: CDNA4 HIP stencil kernels, HIP runtime, RCCL halos, CPU oracle";
+
+  py::register_exception<Error>(m, "NativeError", PyExc_RuntimeError);
+
+  // ---------------------------------------------------------------- filters
+  py::class_<Filter>(m, "Filter")
+      .def_static("gaussian", &Filter::gaussian)
+      .def_static("box", &Filter::box)
+      .def_static("edge", &Filter::edge)
+      .def_static("by_name", &Filter::by_name)
+      .def_static("custom", &Filter::custom, py::arg("taps"), py::arg("divisor"), py::arg("name") = "custom")
+      .def_readonly("name", &Filter::name)
+      .def_readonly("taps", &Filter::taps)
+      .def_readonly("divisor", &Filter::divisor)
+      .def_readonly("weights", &Filter::weights)
+      .def_readonly("int_exact", &Filter::int_exact)
+      .def_readonly("shift", &Filter::shift)
+      .def_readonly("binomial121", &Filter::binomial121)
+      .def("__repr__", [](const Filter& f) { return "Filter(" + f.name + "/" + std::to_string(f.divisor) + ")"; });
+
+  // ---------------------------------------------------------------- geometry
+  m.def(
+      "frame_layout",
+      [](int64_t row_bytes, int64_t rows, int64_t halo) {
+        const FrameLayout l = FrameLayout::make(row_bytes, rows, halo);
+        return py::dict(py::arg("row_bytes") = l.row_bytes, py::arg("rows") = l.rows, py::arg("halo") = l.halo,
+                        py::arg("pitch") = l.pitch, py::arg("bytes") = l.bytes(), py::arg("pad_left") = kPadLeft);
+      },
+      py::arg("row_bytes"), py::arg("rows"), py::arg("halo"));
+
+  py::class_<Band>(m, "Band")
+      .def(py::init<>())
+      .def_readwrite("rank", &Band::rank)
+      .def_readwrite("world", &Band::world)
+      .def_readwrite("y0", &Band::y0)
+      .def_readwrite("rows", &Band::rows)
+      .def_readwrite("up", &Band::up)
+      .def_readwrite("down", &Band::down)
+      .def("__repr__", [](const Band& b) {
+        return "Band(rank=" + std::to_string(b.rank) + ", y0=" + std::to_string(b.y0) + ", rows=" +
+               std::to_string(b.rows) + ", up=" + std::to_string(b.up) + ", down=" + std::to_string(b.down) + ")";
+      });
+  m.def("row_band", &row_band, py::arg("height"), py::arg("world"), py::arg("rank"));
+  m.def("row_bands", &row_bands, py::arg("height"), py::arg("world"));
+  m.def("reference_rows_division", &reference_rows_division);
+
+  // ---------------------------------------------------------------- schedule
+  py::class_<LaunchSpec>(m, "LaunchSpec")
+      .def_readonly("steps", &LaunchSpec::steps)
+      .def_readonly("lo", &LaunchSpec::lo)
+      .def_readonly("hi", &LaunchSpec::hi)
+      .def_readonly("after_halo", &LaunchSpec::after_halo);
+  py::class_<Phase>(m, "Phase")
+      .def_readonly("exchange_depth", &Phase::exchange_depth)
+      .def_readonly("steps", &Phase::steps)
+      .def_readonly("launches", &Phase::launches);
+  m.def(
+      "plan_band",
+      [](const Band& b, int reps, int halo_depth, int fuse, bool overlap, bool halo_preloaded) {
+        PlanConfig c;
+        c.halo_depth = halo_depth;
+        c.fuse = fuse;
+        c.overlap = overlap;
+        c.halo_preloaded = halo_preloaded;
+        return plan_band(b, reps, c);
+      },
+      py::arg("band"), py::arg("reps"), py::arg("halo_depth") = 1, py::arg("fuse") = 1, py::arg("overlap") = true,
+      py::arg("halo_preloaded") = false);
+  m.def(
+      "normalize_plan",
+      [](int halo_depth, int fuse, int64_t min_band_rows, int max_fuse) {
+        PlanConfig c;
+        c.halo_depth = halo_depth;
+        c.fuse = fuse;
+        c = normalize_plan_config(c, min_band_rows, max_fuse);
+        return py::make_tuple(c.halo_depth, c.fuse);
+      },
+      py::arg("halo_depth"), py::arg("fuse"), py::arg("min_band_rows"), py::arg("max_fuse") = kMaxFusedSteps);
+  m.def("describe_plan", &describe_plan);
+  m.attr("MAX_FUSED_STEPS") = kMaxFusedSteps;
+
+  // ---------------------------------------------------------------- CPU oracle
+  m.def(
+      "cpu_convolve",
+      [](py::buffer in, py::buffer out, int64_t w, int64_t h, const std::string& ch, int reps, py::object filter,
+         bool omp, int threads) {
+        const ImageGeom g = make_geom(w, h, ch);
+        const HostView a = host_view(in, false), b = host_view(out, true);
+        PCONV_CHECK(a.size == g.bytes() && b.size == g.bytes(), "buffer size does not match the image geometry");
+        const Filter f = make_filter(filter);
+        py::gil_scoped_release nogil;
+        cpu_convolve(f, g, a.ptr, b.ptr, reps, omp ? CpuBackend::OpenMP : CpuBackend::Serial, threads);
+      },
+      py::arg("src"), py::arg("dst"), py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("reps"),
+      py::arg("filter") = "gaussian", py::arg("omp") = false, py::arg("threads") = 0);
+  m.def(
+      "cpu_fused_launch",
+      [](py::object filter, const std::string& ch, int64_t row_bytes, int64_t rows, int64_t halo, py::buffer src,
+         py::buffer dst, int64_t lo, int64_t hi, int steps, int64_t g_row0, int64_t height, bool omp) {
+        const FrameLayout lay = FrameLayout::make(row_bytes, rows, halo);
+        const HostView a = host_view(src, false), b = host_view(dst, true);
+        PCONV_CHECK(a.size == lay.bytes() && b.size == lay.bytes(), "frame buffer size mismatch");
+        const Filter f = make_filter(filter);
+        py::gil_scoped_release nogil;
+        cpu_fused_launch(f, parse_channels(ch), lay, a.ptr, b.ptr, lo, hi, steps, g_row0, height,
+                         omp ? CpuBackend::OpenMP : CpuBackend::Serial);
+      },
+      py::arg("filter"), py::arg("channels"), py::arg("row_bytes"), py::arg("rows"), py::arg("halo"), py::arg("src"),
+      py::arg("dst"), py::arg("lo"), py::arg("hi"), py::arg("steps"), py::arg("g_row0"), py::arg("height"),
+      py::arg("omp") = false);
+
+  // ---------------------------------------------------------------- raw I/O
+  m.def("output_path_for", &output_path_for, py::arg("path"), py::arg("prefix") = "blur_");
+  m.def(
+      "read_raw",
+      [](const std::string& path, py::buffer dst, int64_t w, int64_t h, const std::string& ch) {
+        const ImageGeom g = make_geom(w, h, ch);
+        const HostView b = host_view(dst, true);
+        PCONV_CHECK(b.size == g.bytes(), "buffer size does not match the image geometry");
+        read_image(path, g, b.ptr);
+      },
+      py::arg("path"), py::arg("dst"), py::arg("width"), py::arg("height"), py::arg("channels"));
+  m.def(
+      "read_raw_rows",
+      [](const std::string& path, py::buffer dst, int64_t w, int64_t h, const std::string& ch, int64_t y0,
+         int64_t rows) {
+        const ImageGeom g = make_geom(w, h, ch);
+        const HostView b = host_view(dst, true);
+        PCONV_CHECK(b.size >= rows * g.row_bytes(), "buffer too small");
+        validate_input_file(path, g);
+        read_rows(path, g, y0, rows, b.ptr, g.row_bytes());
+      },
+      py::arg("path"), py::arg("dst"), py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("y0"),
+      py::arg("rows"));
+  m.def(
+      "write_raw",
+      [](const std::string& path, py::buffer src, int64_t w, int64_t h, const std::string& ch) {
+        const ImageGeom g = make_geom(w, h, ch);
+        const HostView b = host_view(src, false);
+        PCONV_CHECK(b.size == g.bytes(), "buffer size does not match the image geometry");
+        write_image(path, g, b.ptr);
+      },
+      py::arg("path"), py::arg("src"), py::arg("width"), py::arg("height"), py::arg("channels"));
+  m.def(
+      "create_output",
+      [](const std::string& path, int64_t w, int64_t h, const std::string& ch) {
+        create_output(path, make_geom(w, h, ch));
+      },
+      py::arg("path"), py::arg("width"), py::arg("height"), py::arg("channels"));
+  m.def(
+      "write_raw_rows",
+      [](const std::string& path, py::buffer src, int64_t w, int64_t h, const std::string& ch, int64_t y0,
+         int64_t rows) {
+        const ImageGeom g = make_geom(w, h, ch);
+        const HostView b = host_view(src, false);
+        PCONV_CHECK(b.size >= rows * g.row_bytes(), "buffer too small");
+        write_rows(path, g, y0, rows, b.ptr, g.row_bytes());
+      },
+      py::arg("path"), py::arg("src"), py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("y0"),
+      py::arg("rows"));
+  m.def(
+      "synth_rows",
+      [](py::buffer dst, int64_t w, int64_t h, const std::string& ch, uint64_t seed, int64_t y0, int64_t rows) {
+        const ImageGeom g = make_geom(w, h, ch);
+        const HostView b = host_view(dst, true);
+        PCONV_CHECK(b.size >= rows * g.row_bytes(), "buffer too small");
+        py::gil_scoped_release nogil;
+        synth_rows(g, seed, y0, rows, b.ptr, g.row_bytes());
+      },
+      py::arg("dst"), py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("seed"), py::arg("y0"),
+      py::arg("rows"));
+
+  // ---------------------------------------------------------------- CLI
+  m.def("conv_main", [](std::vector<std::string> argv) {
+    std::vector<char*> ptrs;
+    for (auto& s : argv) ptrs.push_back(s.data());
+    py::gil_scoped_release nogil;
+    return conv_main(static_cast<int>(ptrs.size()), ptrs.data());
+  });
+
+  // ---------------------------------------------------------------- device
+  m.def("device_count", &device_count);
+  m.def("device_name", &device_name);
+  m.def("set_device", &set_device);
+
+  py::class_<PinnedBuffer>(m, "PinnedBuffer", py::buffer_protocol())
+      .def(py::init<size_t>())
+      .def_property_readonly("ptr", [](const PinnedBuffer& b) { return reinterpret_cast<uintptr_t>(b.data()); })
+      .def("__len__", &PinnedBuffer::size)
+      .def_buffer([](PinnedBuffer& b) -> py::buffer_info {
+        return py::buffer_info(b.data(), 1, py::format_descriptor<uint8_t>::format(), 1,
+                               {static_cast<py::ssize_t>(b.size())}, {1});
+      });
+
+  m.def(
+      "launch_stencil",
+      [](py::object filter, const std::string& ch, uintptr_t src, uintptr_t dst, int64_t pitch, int64_t row_bytes,
+         int64_t r0, int64_t r1, int64_t frame_lo, int64_t frame_hi, int steps, int64_t g_row0, int64_t height,
+         uintptr_t stream, const std::string& variant) {
+        StencilLaunch a;
+        a.src = reinterpret_cast<const uint8_t*>(src);
+        a.dst = reinterpret_cast<uint8_t*>(dst);
+        a.pitch = pitch;
+        a.row_bytes = row_bytes;
+        a.r0 = r0;
+        a.r1 = r1;
+        a.frame_lo = frame_lo;
+        a.frame_hi = frame_hi;
+        a.steps = steps;
+        a.g_row0 = g_row0;
+        a.height = height;
+        launch_stencil(make_filter(filter), parse_channels(ch), a, reinterpret_cast<hipStream_t>(stream),
+                       parse_variant(variant));
+      },
+      py::arg("filter"), py::arg("channels"), py::arg("src"), py::arg("dst"), py::arg("pitch"), py::arg("row_bytes"),
+      py::arg("r0"), py::arg("r1"), py::arg("frame_lo"), py::arg("frame_hi"), py::arg("steps") = 1,
+      py::arg("g_row0") = 0, py::arg("height") = (int64_t(1) << 40), py::arg("stream") = 0,
+      py::arg("variant") = "auto");
+  m.def("supports_fusion",
+        [](py::object filter, const std::string& v) { return supports_fusion(make_filter(filter), parse_variant(v)); },
+        py::arg("filter"), py::arg("variant") = "auto");
+
+  // ---------------------------------------------------------------- engine
+  py::class_<RunStats>(m, "RunStats")
+      .def_readonly("loop_ms", &RunStats::loop_ms)
+      .def_readonly("wall_ms", &RunStats::wall_ms)
+      .def_readonly("launches", &RunStats::launches)
+      .def_readonly("exchanges", &RunStats::exchanges);
+
+  py::class_<HaloTransport, std::shared_ptr<HaloTransport>>(m, "HaloTransport")
+      .def_property_readonly("name", &HaloTransport::name);
+
+  py::class_<BandEngine>(m, "BandEngine")
+      .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
+                       int device, int halo, int fuse, bool overlap, bool graph, const std::string& variant) {
+             EngineOptions o;
+             o.device = device;
+             o.halo_depth = halo;
+             o.fuse = fuse;
+             o.overlap = overlap;
+             o.use_graph = graph;
+             o.variant = parse_variant(variant);
+             const ImageGeom g = make_geom(w, h, ch);
+             return std::make_unique<BandEngine>(g, row_band(h, world, rank), make_filter(filter), o);
+           }),
+           py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
+           py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
+           py::arg("overlap") = true, py::arg("graph") = false, py::arg("variant") = "auto")
+      .def_property_readonly("band", &BandEngine::band)
+      .def_property_readonly("halo", [](const BandEngine& e) { return e.layout().halo; })
+      .def_property_readonly("fuse", [](const BandEngine& e) { return e.options().fuse; })
+      .def_property_readonly("pitch", [](const BandEngine& e) { return e.layout().pitch; })
+      .def_property_readonly("row_bytes", [](const BandEngine& e) { return e.layout().row_bytes; })
+      .def_property_readonly("compute_stream",
+                             [](const BandEngine& e) { return reinterpret_cast<uintptr_t>(e.compute_stream()); })
+      .def_property_readonly("src_ptr", [](const BandEngine& e) { return reinterpret_cast<uintptr_t>(e.src_frame()); })
+      .def("plan", &BandEngine::plan, py::arg("reps"))
+      .def(
+          "upload",
+          [](BandEngine& e, py::buffer host, int64_t r_begin, int64_t r_end) {
+            const HostView v = host_view(host, false);
+            PCONV_CHECK(v.size >= (r_end - r_begin) * e.layout().row_bytes, "host buffer too small");
+            e.upload_rows(v.ptr, e.layout().row_bytes, r_begin, r_end);
+          },
+          py::arg("host"), py::arg("r_begin"), py::arg("r_end"))
+      .def(
+          "upload_ptr",
+          [](BandEngine& e, uintptr_t ptr, int64_t pitch, int64_t r_begin, int64_t r_end, bool device) {
+            if (device)
+              e.upload_rows_device(reinterpret_cast<const uint8_t*>(ptr), pitch, r_begin, r_end);
+            else
+              e.upload_rows(reinterpret_cast<const uint8_t*>(ptr), pitch, r_begin, r_end);
+          },
+          py::arg("ptr"), py::arg("pitch"), py::arg("r_begin"), py::arg("r_end"), py::arg("device") = false)
+      .def(
+          "download",
+          [](BandEngine& e, py::buffer host, int64_t r_begin, int64_t r_end) {
+            const HostView v = host_view(host, true);
+            PCONV_CHECK(v.size >= (r_end - r_begin) * e.layout().row_bytes, "host buffer too small");
+            e.download_rows(v.ptr, e.layout().row_bytes, r_begin, r_end);
+          },
+          py::arg("host"), py::arg("r_begin"), py::arg("r_end"))
+      .def(
+          "download_ptr",
+          [](BandEngine& e, uintptr_t ptr, int64_t pitch, int64_t r_begin, int64_t r_end, bool device) {
+            if (device)
+              e.download_rows_device(reinterpret_cast<uint8_t*>(ptr), pitch, r_begin, r_end);
+            else
+              e.download_rows(reinterpret_cast<uint8_t*>(ptr), pitch, r_begin, r_end);
+          },
+          py::arg("ptr"), py::arg("pitch"), py::arg("r_begin"), py::arg("r_end"), py::arg("device") = false)
+      .def("set_halo_valid", &BandEngine::set_halo_valid)
+      .def("wait_stream", [](BandEngine& e, uintptr_t s) { e.wait_stream(reinterpret_cast<hipStream_t>(s)); })
+      .def("signal_stream", [](BandEngine& e, uintptr_t s) { e.signal_stream(reinterpret_cast<hipStream_t>(s)); })
+      .def("run", &BandEngine::run, py::arg("reps"), py::call_guard<py::gil_scoped_release>())
+      .def("synchronize", &BandEngine::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("clear", &BandEngine::clear)
+      .def_property_readonly("stats", &BandEngine::last_stats)
+      .def(
+          "process",
+          [](BandEngine& e, uintptr_t in_ptr, int64_t in_r0, int64_t in_r1, uintptr_t out_ptr, int reps) {
+            // Serving step: H2D (rows [in_r0, in_r1), ghost rows allowed), reps, D2H of
+            // the owned rows; host pointers pinned.  Releases the GIL throughout.
+            py::gil_scoped_release nogil;
+            const int64_t rb = e.layout().row_bytes;
+            e.upload_rows(reinterpret_cast<const uint8_t*>(in_ptr), rb, in_r0, in_r1);
+            e.set_halo_valid(in_r0 < 0 || in_r1 > e.band().rows);
+            e.run(reps);
+            e.download_rows(reinterpret_cast<uint8_t*>(out_ptr), rb, 0, e.band().rows);
+            e.synchronize();
+          },
+          py::arg("in_ptr"), py::arg("in_r0"), py::arg("in_r1"), py::arg("out_ptr"), py::arg("reps"))
+      .def("attach_rccl", [](BandEngine& e, std::shared_ptr<RcclComm> c) {
+        e.set_transport(std::make_shared<RcclTransport>(std::move(c)));
+      });
+
+  py::class_<LocalCluster>(m, "LocalCluster")
+      .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int bands, int device, int halo,
+                       int fuse, const std::string& variant) {
+             EngineOptions o;
+             o.device = device;
+             o.halo_depth = halo;
+             o.fuse = fuse;
+             o.variant = parse_variant(variant);
+             return std::make_unique<LocalCluster>(make_geom(w, h, ch), bands, make_filter(filter), o);
+           }),
+           py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
+           py::arg("bands") = 2, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
+           py::arg("variant") = "auto")
+      .def("upload",
+           [](LocalCluster& c, py::buffer host, bool preload_halo) {
+             c.upload(host_view(host, false).ptr, preload_halo);
+           },
+           py::arg("host"), py::arg("preload_halo") = false)
+      .def("run", &LocalCluster::run, py::call_guard<py::gil_scoped_release>())
+      .def("download", [](LocalCluster& c, py::buffer host) { c.download(host_view(host, true).ptr); })
+      .def("exchanges", [](LocalCluster& c) { return c.engine(0).last_stats().exchanges; })
+      .def_property_readonly("size", &LocalCluster::size);
+
+  // ---------------------------------------------------------------- RCCL
+  m.def("rccl_unique_id", []() {
+    const auto v = rccl_unique_id();
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+  });
+  m.def("rccl_version", &rccl_version);
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init([](py::bytes id, int rank, int world, int device) {
+             const std::string s = id;
+             std::vector<uint8_t> v(s.begin(), s.end());
+             py::gil_scoped_release nogil;
+             return std::make_shared<RcclComm>(v, rank, world, device);
+           }),
+           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world", &RcclComm::world)
+      .def("allreduce_max", &RcclComm::allreduce_max, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_sum", &RcclComm::allreduce_sum, py::call_guard<py::gil_scoped_release>())
+      .def("barrier", &RcclComm::barrier, py::call_guard<py::gil_scoped_release>());
+
+  m.def("set_error_rank", &set_error_rank);
+}

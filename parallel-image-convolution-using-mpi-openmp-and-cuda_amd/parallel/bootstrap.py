@@ -1,0 +1,96 @@
+"""Process-group bootstrap (one process per GPU).
+
+Reference: ``MPI_Init`` / ``MPI_Comm_size`` / ``MPI_Comm_rank``
+(``mpi/mpi_convolution.c:23-25``) and six ``MPI_Bcast`` of the configuration
+(``:65-70``).  Here the launcher is ``torch.distributed.run`` (RANK,
+WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT in the environment); the control
+plane is a ``gloo`` process group (CPU: barriers, config/unique-id broadcast,
+max-reduction of timings) and the data plane is a native RCCL communicator
+(halo rows over xGMI) created from a unique id broadcast over that group.
+Every rank parses the same argv, so no configuration broadcast is needed.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .._native import require_native
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    initialized_here: bool = False
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world > 1
+
+
+def env_context() -> DistContext:
+    return DistContext(
+        rank=int(os.environ.get("RANK", "0")),
+        world=int(os.environ.get("WORLD_SIZE", "1")),
+        local_rank=int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))),
+    )
+
+
+def init_distributed(backend: str = "gloo", timeout_s: float = 600.0) -> DistContext:
+    """Initialise torch.distributed from the environment if WORLD_SIZE > 1."""
+    ctx = env_context()
+    if ctx.world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        import datetime
+
+        dist.init_process_group(backend=backend, rank=ctx.rank, world_size=ctx.world,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+        ctx.initialized_here = True
+    require_native().set_error_rank(ctx.rank)
+    return ctx
+
+
+def broadcast_bytes(data: Optional[bytes], src: int = 0, group=None) -> bytes:
+    """Broadcast a small byte string from ``src`` over the (gloo) group."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        assert data is not None
+        return data
+    obj = [data]
+    dist.broadcast_object_list(obj, src=src, group=group)
+    return obj[0]
+
+
+def make_rccl_comm(device: int, group=None):
+    """Create the native RCCL communicator for this rank (collective)."""
+    n = require_native()
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    uid = n.rccl_unique_id() if rank == 0 else None
+    uid = broadcast_bytes(uid, 0, group)
+    return n.RcclComm(uid, rank, world, device)
+
+
+def max_over_ranks(value: float, group=None) -> float:
+    """Max of a float over ranks (the reference's Send/Recv max-gather,
+    ``mpi/mpi_convolution.c:264-275``)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def barrier(group=None) -> None:
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.barrier(group=group)
+
+
+def shutdown(ctx: DistContext) -> None:
+    if ctx.initialized_here and dist.is_initialized():
+        dist.destroy_process_group()

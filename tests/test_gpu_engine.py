@@ -1,0 +1,94 @@
+"""Engine-level GPU tests: convolve() on numpy and CUDA tensors, graphs,
+one-device multi-band emulation (LocalCluster), RCCL single-rank, CLI."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import CONV_BIN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (7, 3), (2520 // 8, 1920 // 8, 3), (61, 77, 3), (33, 50, 4), (100, 129)])
+@pytest.mark.parametrize("reps", [0, 1, 2, 7, 40])
+def test_convolve_hip_numpy(pconv_mod, rng, shape, reps):
+    img = rng.integers(0, 256, size=shape, dtype=np.uint8)
+    got = pconv_mod.convolve(img, reps, backend="hip")
+    assert np.array_equal(got, pconv_mod.numpy_convolve(img, reps))
+
+
+@pytest.mark.parametrize("filt", ["gaussian", "box", "edge"])
+def test_convolve_hip_tensor(pconv_mod, rng, filt):
+    import torch
+
+    img = rng.integers(0, 256, size=(45, 67, 3), dtype=np.uint8)
+    x = torch.from_numpy(img).cuda()
+    y = pconv_mod.convolve(x, 9, filter=filt)
+    assert y.is_cuda and y.dtype == torch.uint8
+    assert np.array_equal(y.cpu().numpy(), pconv_mod.numpy_convolve(img, 9, filt))
+    assert np.array_equal(x.cpu().numpy(), img)  # input untouched
+
+
+@pytest.mark.parametrize("fuse", [1, 2, 5, 8])
+@pytest.mark.parametrize("graph", [False, True])
+def test_engine_reuse_fuse_graph(pconv_mod, rng, fuse, graph):
+    eng = pconv_mod.Engine(53, 41, "rgb", device=0, fuse=fuse, graph=graph)
+    for reps in (1, 3, 8, 17, 8):
+        img = rng.integers(0, 256, size=(41, 53, 3), dtype=np.uint8)
+        assert np.array_equal(eng(img, reps), pconv_mod.numpy_convolve(img, reps)), (fuse, graph, reps)
+
+
+@pytest.mark.parametrize("bands", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("halo,fuse,preload", [(1, 1, False), (4, 1, True), (4, 4, False), (8, 4, True)])
+def test_local_cluster_bit_exact(pconv_mod, rng, bands, halo, fuse, preload):
+    n = pconv_mod.native
+    img = rng.integers(0, 256, size=(70, 45, 3), dtype=np.uint8)
+    cl = n.LocalCluster(45, 70, "rgb", "gaussian", bands, 0, halo, fuse)
+    for reps in (1, 6, 13):
+        cl.upload(img.reshape(-1), preload)
+        cl.run(reps)
+        out = np.empty_like(img)
+        cl.download(out.reshape(-1))
+        assert np.array_equal(out, pconv_mod.numpy_convolve(img, reps)), (bands, halo, fuse, reps)
+
+
+def test_local_cluster_float_filter(pconv_mod, rng):
+    n = pconv_mod.native
+    img = rng.integers(0, 256, size=(40, 31), dtype=np.uint8)
+    cl = n.LocalCluster(31, 40, "grey", "box", 4, 0, 3, 1)
+    cl.upload(img.reshape(-1), False)
+    cl.run(7)
+    out = np.empty_like(img)
+    cl.download(out.reshape(-1))
+    assert np.array_equal(out, pconv_mod.numpy_convolve(img, 7, "box"))
+
+
+def test_rccl_single_rank_and_dist_engine(pconv_mod):
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    n = pconv_mod.native
+    comm = n.RcclComm(n.rccl_unique_id(), 0, 1, 0)
+    assert comm.allreduce_max(3.5) == 3.5 and comm.allreduce_sum(2.0) == 2.0
+    comm.barrier()
+    blur = DistributedBlur(96, 50, "rgb", "gaussian", 12, rank=0, world=1, device=0)
+    blur.load_synthetic(3)
+    blur.step(12)
+    ref = pconv_mod.numpy_convolve(pconv_mod.synthetic_image(96, 50, "rgb", seed=3), 12)
+    assert np.array_equal(blur.output.reshape(ref.shape), ref)
+
+
+def test_cli_hip(pconv_mod, tmp_path, rng):
+    img = rng.integers(0, 256, size=(77, 61, 3), dtype=np.uint8)
+    pconv_mod.write_raw(str(tmp_path / "img.raw"), img)
+    for extra in ([], ["--graph"], ["--fuse", "3"], ["--gpus", "1", "--format", "both"]):
+        r = subprocess.run([CONV_BIN, "img.raw", "61", "77", "11", "rgb", "--check", "--json"] + extra,
+                           cwd=tmp_path, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert "Execution time:" in r.stdout
+        meta = json.loads(r.stdout.strip().splitlines()[-1])
+        assert meta["mismatches"] == 0
+        out = pconv_mod.read_raw(str(tmp_path / "blur_img.raw"), 61, 77, "rgb")
+        assert np.array_equal(out, pconv_mod.numpy_convolve(img, 11))

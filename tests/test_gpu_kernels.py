@@ -1,0 +1,97 @@
+"""HIP kernel numerics on a real MI355X: every variant vs the fp32-semantics
+oracles, odd sizes, partial row ranges, guard-band canaries (catches the
+out-of-bounds class of bug the reference's RGB kernel had)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GUARD = 4096
+CANARY = 0xA5
+CH = {"grey": 1, "rgb": 3, "rgba": 4}
+
+
+def _frame(native, torch, row_bytes, rows, halo):
+    lay = native.frame_layout(row_bytes, rows, halo)
+    buf = torch.full((lay["bytes"] + 2 * GUARD,), CANARY, dtype=torch.uint8, device="cuda")
+    buf[GUARD : GUARD + lay["bytes"]] = 0
+    return lay, buf
+
+
+def _rows(buf, lay, halo, rows):
+    v = buf[GUARD : GUARD + lay["bytes"]].view(rows + 2 * halo, lay["pitch"])
+    return v
+
+
+def _run_kernel(native, img, filt, variant, steps=1, r0=None, r1=None, halo=None):
+    import torch
+
+    h = img.shape[0]
+    row_bytes = img.size // h
+    halo = halo if halo is not None else max(1, steps)
+    lay, src = _frame(native, torch, row_bytes, h, halo)
+    _, dst = _frame(native, torch, row_bytes, h, halo)
+    sv = _rows(src, lay, halo, h)
+    sv[halo : halo + h, 16 : 16 + row_bytes] = torch.from_numpy(img.reshape(h, row_bytes)).cuda()
+    base = lay["pitch"] * halo + 16
+    r0 = 0 if r0 is None else r0
+    r1 = h if r1 is None else r1
+    native.launch_stencil(filt, {1: "grey", 3: "rgb", 4: "rgba"}[img.size // (h * img.shape[1])],
+                          src.data_ptr() + GUARD + base, dst.data_ptr() + GUARD + base, lay["pitch"], row_bytes,
+                          r0, r1, -halo, h + halo, steps, 0, h, torch.cuda.current_stream().cuda_stream, variant)
+    torch.cuda.synchronize()
+    d = dst.cpu().numpy()
+    assert (d[:GUARD] == CANARY).all() and (d[-GUARD:] == CANARY).all(), "write outside the frame"
+    dv = d[GUARD:-GUARD].reshape(h + 2 * halo, lay["pitch"])
+    assert (dv[:, :16] == 0).all() and (dv[:, 16 + row_bytes :] == 0).all(), "write into the pad columns"
+    outside = np.ones(h + 2 * halo, bool)
+    outside[halo + r0 : halo + r1] = False
+    assert (dv[outside] == 0).all(), "write outside the requested rows"
+    return dv[halo : halo + h, 16 : 16 + row_bytes].reshape(img.shape)
+
+
+SIZES = [(1, 1), (1, 5), (5, 1), (3, 3), (2, 16), (17, 16), (9, 33), (31, 100), (64, 65), (130, 257)]
+
+
+@pytest.mark.parametrize("channels", ["grey", "rgb", "rgba"])
+@pytest.mark.parametrize("filt,variant", [("gaussian", "auto"), ("gaussian", "binomial"), ("gaussian", "int9"),
+                                          ("gaussian", "float9"), ("box", "auto"), ("edge", "auto")])
+def test_single_step_matches_oracle(native, rng, channels, filt, variant):
+    from pconv.ops.reference import numpy_convolve
+
+    c = CH[channels]
+    for (h, w) in SIZES:
+        img = rng.integers(0, 256, size=(h, w, c) if c > 1 else (h, w), dtype=np.uint8)
+        got = _run_kernel(native, img, filt, variant)
+        assert np.array_equal(got, numpy_convolve(img, 1, filt)), (h, w)
+
+
+def test_extreme_values(native):
+    from pconv.ops.reference import numpy_convolve
+
+    for val in (0, 1, 15, 16, 128, 254, 255):
+        img = np.full((19, 23, 3), val, np.uint8)
+        for f in ("gaussian", "box", "edge"):
+            assert np.array_equal(_run_kernel(native, img, f, "auto"), numpy_convolve(img, 1, f))
+
+
+def test_partial_rows(native, rng):
+    from pconv.ops.reference import numpy_convolve
+
+    img = rng.integers(0, 256, size=(40, 37, 3), dtype=np.uint8)
+    ref = numpy_convolve(img, 1)
+    for r0, r1 in [(0, 1), (5, 6), (3, 29), (39, 40), (0, 40), (13, 14)]:
+        got = _run_kernel(native, img, "gaussian", "auto", r0=r0, r1=r1)
+        assert np.array_equal(got[r0:r1], ref[r0:r1])
+        assert (got[:r0] == 0).all() and (got[r1:] == 0).all()
+
+
+def test_shape_guard_rejects_out_of_frame(native):
+    import torch
+
+    lay, src = _frame(native, torch, 64, 8, 1)
+    _, dst = _frame(native, torch, 64, 8, 1)
+    base = lay["pitch"] + 16
+    with pytest.raises(RuntimeError, match="exceed frame"):
+        native.launch_stencil("gaussian", "grey", src.data_ptr() + GUARD + base, dst.data_ptr() + GUARD + base,
+                              lay["pitch"], 64, -1, 8, -1, 9, 1, 0, 1 << 40, 0, "auto")
