@@ -69,7 +69,10 @@ class BandEngine {
   const FrameLayout& layout() const { return lay_; }
   const EngineOptions& options() const { return opt_; }
   hipStream_t compute_stream() const { return cs_.get(); }
-  hipStream_t comm_stream() const { return ms_.get(); }
+  hipStream_t comm_stream() const { return comm_override_ ? comm_override_ : ms_.get(); }
+  // Share one communication stream between engines (pipeline slots): keeps
+  // every RCCL call of a rank on one stream, in issue order.
+  void set_comm_stream(hipStream_t s) { comm_override_ = s; }
 
   void set_transport(std::shared_ptr<HaloTransport> t) { transport_ = std::move(t); }
 
@@ -80,13 +83,16 @@ class BandEngine {
   // Copy frame-local rows [r_begin, r_end) from host (pointer at row r_begin).
   // Rows in the ghost zone are accepted (pre-loaded halos).  Async on the
   // compute stream; `host` should be pinned for true async DMA.
-  void upload_rows(const uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end);
+  // `stream` = nullptr means the compute stream.
+  void upload_rows(const uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end,
+                   hipStream_t stream = nullptr);
   // Same from a device pointer (e.g. a torch CUDA tensor).
   void upload_rows_device(const uint8_t* dev, int64_t dev_pitch, int64_t r_begin, int64_t r_end);
   // Declare whether the ghost rows currently hold valid neighbour data.
   void set_halo_valid(bool v) { halo_valid_ = v; }
   // Copy owned rows [r_begin, r_end) of the newest result to host / device.
-  void download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end);
+  void download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end,
+                     hipStream_t stream = nullptr);
   void download_rows_device(uint8_t* dev, int64_t dev_pitch, int64_t r_begin, int64_t r_end);
 
   // Make the compute stream wait for work already queued on `s` / make `s`
@@ -120,6 +126,7 @@ class BandEngine {
   int cur_ = 0;
   bool halo_valid_ = false;
   Stream cs_, ms_;
+  hipStream_t comm_override_ = nullptr;
   Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_;
   std::shared_ptr<HaloTransport> transport_;
   RunStats stats_;
@@ -127,6 +134,33 @@ class BandEngine {
   bool timing_pending_ = false;
   // hipGraph cache: (reps, start buffer) -> executable graph
   std::map<std::pair<int, int>, hipGraphExec_t> graphs_;
+};
+
+// Serving pipeline: S band engines ("slots") so that the H2D copy of image
+// k+1, the repetitions of image k and the D2H copy of image k-1 overlap on
+// three streams (the reference did copy -> compute -> copy, synchronous and
+// pageable, cuda/cuda_convolution.cu:60,94-96).  Slot reuse is ordered by
+// events; all slots of a rank share one communication stream.
+class BandPipeline {
+ public:
+  BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt, int slots);
+  ~BandPipeline();
+  int slots() const { return static_cast<int>(slots_.size()); }
+  BandEngine& slot(int i) { return *slots_.at(i); }
+  void set_transport(std::shared_ptr<HaloTransport> t);
+  // Enqueue one image: host_in holds frame rows [in_r0, in_r1) (ghost rows
+  // allowed), host_out receives the owned rows.  Host buffers must be pinned
+  // and must stay untouched until drain() (or until S later submits).
+  void submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps);
+  void drain();
+  int64_t submitted() const { return count_; }
+
+ private:
+  std::vector<std::unique_ptr<BandEngine>> slots_;
+  Stream h2d_, d2h_, comm_;
+  std::vector<Event> ev_up_, ev_done_, ev_free_;
+  std::vector<bool> used_;
+  int64_t count_ = 0;
 };
 
 // N row bands of one image on ONE device, halos moved by D2D copies.  Used to

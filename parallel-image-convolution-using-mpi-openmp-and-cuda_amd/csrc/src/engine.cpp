@@ -55,7 +55,8 @@ void BandEngine::clear() {
   halo_valid_ = false;
 }
 
-void BandEngine::upload_rows(const uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end) {
+void BandEngine::upload_rows(const uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end,
+                             hipStream_t stream) {
   PCONV_CHECK(r_begin >= -lay_.halo && r_end <= lay_.rows + lay_.halo && r_begin <= r_end,
               "upload_rows: rows outside frame");
   PCONV_CHECK(host_pitch >= lay_.row_bytes, "upload_rows: host pitch < row bytes");
@@ -63,7 +64,7 @@ void BandEngine::upload_rows(const uint8_t* host, int64_t host_pitch, int64_t r_
   PCONV_CHECK(band_.y0 + r_begin >= 0 && band_.y0 + r_end <= geom_.height, "upload_rows: rows outside image");
   if (r_end == r_begin) return;
   PCONV_HIP_CHECK(hipMemcpy2DAsync(src_frame() + r_begin * lay_.pitch, lay_.pitch, host, host_pitch, lay_.row_bytes,
-                                   r_end - r_begin, hipMemcpyHostToDevice, cs_.get()));
+                                   r_end - r_begin, hipMemcpyHostToDevice, stream ? stream : cs_.get()));
 }
 
 void BandEngine::upload_rows_device(const uint8_t* dev, int64_t dev_pitch, int64_t r_begin, int64_t r_end) {
@@ -75,11 +76,12 @@ void BandEngine::upload_rows_device(const uint8_t* dev, int64_t dev_pitch, int64
                                    r_end - r_begin, hipMemcpyDeviceToDevice, cs_.get()));
 }
 
-void BandEngine::download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end) {
+void BandEngine::download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end,
+                               hipStream_t stream) {
   PCONV_CHECK(r_begin >= 0 && r_end <= lay_.rows && r_begin <= r_end, "download_rows: rows outside band");
   if (r_end == r_begin) return;
   PCONV_HIP_CHECK(hipMemcpy2DAsync(host, host_pitch, src_frame() + r_begin * lay_.pitch, lay_.pitch, lay_.row_bytes,
-                                   r_end - r_begin, hipMemcpyDeviceToHost, cs_.get()));
+                                   r_end - r_begin, hipMemcpyDeviceToHost, stream ? stream : cs_.get()));
 }
 
 void BandEngine::download_rows_device(uint8_t* dev, int64_t dev_pitch, int64_t r_begin, int64_t r_end) {
@@ -125,10 +127,11 @@ void BandEngine::launch(const LaunchSpec& l, hipStream_t s) {
 void BandEngine::enqueue_phase(const Phase& p) {
   if (p.exchange_depth > 0) {
     PCONV_CHECK(transport_ != nullptr, "band has neighbours but no halo transport is attached");
+    hipStream_t ms = comm_stream();
     ev_ready_.record(cs_.get());
-    ev_ready_.wait_on(ms_.get());
-    transport_->exchange(*this, p.exchange_depth, ms_.get());
-    ev_halo_.record(ms_.get());
+    ev_ready_.wait_on(ms);
+    transport_->exchange(*this, p.exchange_depth, ms);
+    ev_halo_.record(ms);
     for (const auto& l : p.launches)
       if (!l.after_halo) launch(l, cs_.get());
     ev_halo_.wait_on(cs_.get());
@@ -191,12 +194,68 @@ void BandEngine::exec_compute(const Phase& p) {
 
 void BandEngine::synchronize() {
   cs_.sync();
-  ms_.sync();
+  PCONV_HIP_CHECK(hipStreamSynchronize(comm_stream()));
   if (timing_pending_) {
     stats_.loop_ms = Event::elapsed_ms(ev_t0_, ev_t1_);
     stats_.wall_ms = (wall_seconds() - wall_t0_) * 1e3;
     timing_pending_ = false;
   }
+}
+
+// --------------------------------------------------------------- BandPipeline
+
+BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt,
+                           int slots) {
+  PCONV_CHECK(slots >= 1 && slots <= 8, "pipeline slots must be in [1, 8]");
+  EngineOptions o = opt;
+  o.use_graph = false;  // copies/events interleave with the loop
+  for (int i = 0; i < slots; ++i) slots_.push_back(std::make_unique<BandEngine>(geom, band, filter, o));
+  h2d_ = Stream::create(0);
+  d2h_ = Stream::create(0);
+  comm_ = Stream::create(-1);
+  for (int i = 0; i < slots; ++i) {
+    ev_up_.push_back(Event::create());
+    ev_done_.push_back(Event::create());
+    ev_free_.push_back(Event::create());
+    slots_[i]->set_comm_stream(comm_.get());
+  }
+  used_.assign(slots, false);
+}
+
+BandPipeline::~BandPipeline() {
+  (void)hipStreamSynchronize(h2d_.get());
+  (void)hipStreamSynchronize(d2h_.get());
+  (void)hipStreamSynchronize(comm_.get());
+}
+
+void BandPipeline::set_transport(std::shared_ptr<HaloTransport> t) {
+  for (auto& s : slots_) s->set_transport(t);
+}
+
+void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
+  const int k = static_cast<int>(count_ % static_cast<int64_t>(slots_.size()));
+  BandEngine& e = *slots_[k];
+  // H2D into slot k once its previous image has been downloaded.
+  if (used_[k]) ev_free_[k].wait_on(h2d_.get());
+  e.upload_rows(host_in, e.layout().row_bytes, in_r0, in_r1, h2d_.get());
+  ev_up_[k].record(h2d_.get());
+  // reps on the slot's compute stream (halo exchanges on the shared comm stream)
+  ev_up_[k].wait_on(e.compute_stream());
+  e.set_halo_valid(in_r0 < 0 || in_r1 > e.band().rows);
+  e.run(reps);
+  ev_done_[k].record(e.compute_stream());
+  // D2H of the owned rows
+  ev_done_[k].wait_on(d2h_.get());
+  e.download_rows(host_out, e.layout().row_bytes, 0, e.band().rows, d2h_.get());
+  ev_free_[k].record(d2h_.get());
+  used_[k] = true;
+  ++count_;
+}
+
+void BandPipeline::drain() {
+  PCONV_HIP_CHECK(hipStreamSynchronize(h2d_.get()));
+  for (auto& s : slots_) s->synchronize();
+  PCONV_HIP_CHECK(hipStreamSynchronize(d2h_.get()));
 }
 
 // --------------------------------------------------------------- LocalCluster

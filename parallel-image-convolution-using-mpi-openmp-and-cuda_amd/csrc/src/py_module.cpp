@@ -63,6 +63,24 @@ Filter make_filter(py::object f) {
   return f.cast<Filter>();
 }
 
+// Halo transport implemented in Python (e.g. host-staged gloo messages for
+// several ranks sharing one GPU in tests).  The Python subclass implements
+// exchange_rows(row0_ptr, pitch, rows, up, down, depth, stream): fill ghost
+// rows [-depth, 0) / [rows, rows+depth) of the frame whose owned row 0 starts
+// at row0_ptr (pitch-aligned, pads included) and send the matching owned rows,
+// enqueued on (or synchronised with) `stream`.
+class PyHaloTransport : public HaloTransport {
+ public:
+  void exchange(BandEngine& e, int64_t depth, hipStream_t stream) override {
+    py::gil_scoped_acquire gil;
+    py::function f = py::get_override(static_cast<const HaloTransport*>(this), "exchange_rows");
+    PCONV_CHECK(static_cast<bool>(f), "HaloTransport subclass must implement exchange_rows()");
+    f(reinterpret_cast<uintptr_t>(e.src_frame() - kPadLeft), e.layout().pitch, e.band().rows, e.band().up,
+      e.band().down, depth, reinterpret_cast<uintptr_t>(stream));
+  }
+  const char* name() const override { return "python"; }
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_pconv_native, m) {
@@ -295,8 +313,25 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_readonly("launches", &RunStats::launches)
       .def_readonly("exchanges", &RunStats::exchanges);
 
-  py::class_<HaloTransport, std::shared_ptr<HaloTransport>>(m, "HaloTransport")
+  py::class_<HaloTransport, PyHaloTransport, std::shared_ptr<HaloTransport>>(m, "HaloTransport")
+      .def(py::init<>())
       .def_property_readonly("name", &HaloTransport::name);
+
+  m.def(
+      "memcpy_async",
+      [](uintptr_t dst, uintptr_t src, int64_t nbytes, const std::string& kind, uintptr_t stream) {
+        hipMemcpyKind k = kind == "h2d" ? hipMemcpyHostToDevice
+                          : kind == "d2h" ? hipMemcpyDeviceToHost
+                          : kind == "d2d" ? hipMemcpyDeviceToDevice
+                                          : hipMemcpyDefault;
+        PCONV_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src),
+                                       static_cast<size_t>(nbytes), k, reinterpret_cast<hipStream_t>(stream)));
+      },
+      py::arg("dst"), py::arg("src"), py::arg("nbytes"), py::arg("kind"), py::arg("stream") = 0);
+  m.def(
+      "stream_synchronize",
+      [](uintptr_t stream) { PCONV_HIP_CHECK(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream))); },
+      py::arg("stream"), py::call_guard<py::gil_scoped_release>());
 
   py::class_<BandEngine>(m, "BandEngine")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
@@ -378,9 +413,45 @@ PYBIND11_MODULE(_pconv_native, m) {
             e.synchronize();
           },
           py::arg("in_ptr"), py::arg("in_r0"), py::arg("in_r1"), py::arg("out_ptr"), py::arg("reps"))
-      .def("attach_rccl", [](BandEngine& e, std::shared_ptr<RcclComm> c) {
-        e.set_transport(std::make_shared<RcclTransport>(std::move(c)));
-      });
+      .def("attach_rccl",
+           [](BandEngine& e, std::shared_ptr<RcclComm> c) {
+             e.set_transport(std::make_shared<RcclTransport>(std::move(c)));
+           })
+      .def("attach_transport", [](BandEngine& e, std::shared_ptr<HaloTransport> t) { e.set_transport(std::move(t)); },
+           py::keep_alive<1, 2>());
+
+  py::class_<BandPipeline>(m, "BandPipeline")
+      .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
+                       int device, int halo, int fuse, bool overlap, const std::string& variant, int slots) {
+             EngineOptions o;
+             o.device = device;
+             o.halo_depth = halo;
+             o.fuse = fuse;
+             o.overlap = overlap;
+             o.variant = parse_variant(variant);
+             const ImageGeom g = make_geom(w, h, ch);
+             return std::make_unique<BandPipeline>(g, row_band(h, world, rank), make_filter(filter), o, slots);
+           }),
+           py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
+           py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
+           py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2)
+      .def_property_readonly("slots", &BandPipeline::slots)
+      .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
+      .def("attach_rccl",
+           [](BandPipeline& p, std::shared_ptr<RcclComm> c) {
+             p.set_transport(std::make_shared<RcclTransport>(std::move(c)));
+           })
+      .def("attach_transport", [](BandPipeline& p, std::shared_ptr<HaloTransport> t) { p.set_transport(std::move(t)); },
+           py::keep_alive<1, 2>())
+      .def(
+          "submit",
+          [](BandPipeline& p, uintptr_t in_ptr, int64_t in_r0, int64_t in_r1, uintptr_t out_ptr, int reps) {
+            py::gil_scoped_release nogil;
+            p.submit(reinterpret_cast<const uint8_t*>(in_ptr), in_r0, in_r1, reinterpret_cast<uint8_t*>(out_ptr), reps);
+          },
+          py::arg("in_ptr"), py::arg("in_r0"), py::arg("in_r1"), py::arg("out_ptr"), py::arg("reps"))
+      .def("drain", &BandPipeline::drain, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("submitted", &BandPipeline::submitted);
 
   py::class_<LocalCluster>(m, "LocalCluster")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int bands, int device, int halo,

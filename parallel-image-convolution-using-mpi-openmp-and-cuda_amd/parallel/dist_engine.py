@@ -5,9 +5,11 @@ block, reads it with MPI-IO, exchanges depth-1 halos with <=4 neighbours per
 rep and times the loop.  Here a rank owns a contiguous row band
 (``native.row_band``), its input rows arrive in pinned host memory (from the
 image, a file band read, or the synthetic generator), and the native
-``BandEngine`` runs the whole ``upload -> reps -> download`` step without
-returning to Python (``BandEngine.process``), with halo rows moved by the
-native RCCL transport on a second stream, overlapped with interior compute.
+``BandPipeline`` runs ``upload -> reps -> download`` per image without
+returning to Python, with halo rows moved by the native RCCL transport on a
+communication stream, overlapped with interior compute.  With ``slots > 1``
+consecutive images overlap (H2D of the next, compute of the current, D2H of
+the previous: a serving pipeline).
 """
 from __future__ import annotations
 
@@ -38,8 +40,8 @@ class DistributedBlur:
     def __init__(self, width: int, height: int, channels: str = "grey", filter="gaussian",
                  reps: Optional[int] = None, *, rank: Optional[int] = None, world: Optional[int] = None,
                  device: Optional[int] = None, halo: Optional[int] = None, fuse: Optional[int] = None,
-                 overlap: bool = True, preload_halo: bool = False, comm=None, graph: bool = False,
-                 variant: str = "auto"):
+                 overlap: bool = True, preload_halo: bool = False, comm=None, slots: int = 2,
+                 variant: str = "auto", graph: bool = False, transport: str = "rccl"):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -51,9 +53,10 @@ class DistributedBlur:
             fuse = DEFAULT_FUSE if n.supports_fusion(nf, variant) else 1
         if halo is None:
             halo = auto_halo(self.height, self.world, reps, fuse)
-        self.engine = n.BandEngine(self.width, self.height, channels, nf, self.rank, self.world, self.device,
-                                   halo=int(halo), fuse=int(fuse), overlap=bool(overlap),
-                                   graph=bool(graph) and self.world == 1, variant=variant)
+        self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
+                                   halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant,
+                                   slots=int(slots))
+        self.engine = self.pipe.slot(0)
         self.band = self.engine.band
         self.row_bytes = self.engine.row_bytes
         d = self.engine.halo
@@ -62,38 +65,72 @@ class DistributedBlur:
         self.above = min(d, b.y0) if self.preload_halo else 0
         self.below = min(d, self.height - (b.y0 + b.rows)) if self.preload_halo else 0
         in_rows = b.rows + self.above + self.below
-        self._in = n.PinnedBuffer(in_rows * self.row_bytes)
-        self._out = n.PinnedBuffer(b.rows * self.row_bytes)
-        self.input = np.asarray(self._in).reshape(in_rows, self.row_bytes)
-        self.output = np.asarray(self._out).reshape(b.rows, self.row_bytes)
+        self.slots = int(slots)
+        # one pinned input/output buffer per slot (in-flight images never share)
+        self._in = [n.PinnedBuffer(in_rows * self.row_bytes) for _ in range(self.slots)]
+        self._out = [n.PinnedBuffer(b.rows * self.row_bytes) for _ in range(self.slots)]
+        self.inputs = [np.asarray(x).reshape(in_rows, self.row_bytes) for x in self._in]
+        self.outputs = [np.asarray(x).reshape(b.rows, self.row_bytes) for x in self._out]
+        self.input, self.output = self.inputs[0], self.outputs[0]
+        self._next = 0
         self.comm = None
+        self.transport = None
         if self.world > 1:
-            self.comm = comm if comm is not None else make_rccl_comm(self.device)
-            self.engine.attach_rccl(self.comm)
+            if transport == "rccl":
+                self.comm = comm if comm is not None else make_rccl_comm(self.device)
+                self.pipe.attach_rccl(self.comm)
+            elif transport == "gloo-host":
+                from .transports import GlooHostTransport
+
+                self.transport = GlooHostTransport()
+                self.pipe.attach_transport(self.transport)
+            else:
+                raise ValueError(f"unknown transport {transport!r} (rccl|gloo-host)")
 
     # ------------------------------------------------------------ inputs
     @property
     def input_rows(self):
-        """Global rows [first, last) held by the pinned input buffer."""
+        """Global rows [first, last) held by the pinned input buffers."""
         return self.band.y0 - self.above, self.band.y0 + self.band.rows + self.below
 
-    def load_image(self, image: np.ndarray) -> None:
+    def load_image(self, image: np.ndarray, slot: Optional[int] = None) -> None:
         a, b = self.input_rows
-        self.input[:] = np.ascontiguousarray(image, dtype=np.uint8).reshape(self.height, self.row_bytes)[a:b]
+        rows = np.ascontiguousarray(image, dtype=np.uint8).reshape(self.height, self.row_bytes)[a:b]
+        for i in ([slot] if slot is not None else range(self.slots)):
+            self.inputs[i][:] = rows
 
     def load_file(self, path: str) -> None:
         a, b = self.input_rows
-        require_native().read_raw_rows(path, self.input.reshape(-1), self.width, self.height, self.channels, a, b - a)
+        require_native().read_raw_rows(path, self.inputs[0].reshape(-1), self.width, self.height, self.channels, a,
+                                       b - a)
+        for i in range(1, self.slots):
+            self.inputs[i][:] = self.inputs[0]
 
     def load_synthetic(self, seed: int = 0) -> None:
         a, b = self.input_rows
-        require_native().synth_rows(self.input.reshape(-1), self.width, self.height, self.channels, int(seed), a,
-                                    b - a)
+        require_native().synth_rows(self.inputs[0].reshape(-1), self.width, self.height, self.channels, int(seed),
+                                    a, b - a)
+        for i in range(1, self.slots):
+            self.inputs[i][:] = self.inputs[0]
 
     # ------------------------------------------------------------ compute
-    def step(self, reps: int) -> None:
-        """H2D of the input rows, `reps` repetitions, D2H of the owned rows."""
-        self.engine.process(self._in.ptr, -self.above, self.band.rows + self.below, self._out.ptr, int(reps))
+    def submit(self, reps: int) -> int:
+        """Enqueue one image (slot round-robin); returns the slot whose output
+        buffer will hold the result after drain()."""
+        k = self._next
+        self.pipe.submit(self._in[k].ptr, -self.above, self.band.rows + self.below, self._out[k].ptr, int(reps))
+        self._next = (k + 1) % self.slots
+        return k
+
+    def drain(self) -> None:
+        self.pipe.drain()
+
+    def step(self, reps: int) -> np.ndarray:
+        """Synchronous: one image through H2D + reps + D2H; returns its rows."""
+        k = self.submit(reps)
+        self.drain()
+        self.output = self.outputs[k]
+        return self.output
 
     @property
     def stats(self):
@@ -102,7 +139,7 @@ class DistributedBlur:
     def plan(self, reps: int):
         return self.engine.plan(reps)
 
-    def write_band(self, path: str) -> None:
+    def write_band(self, path: str, slot: int = 0) -> None:
         """pwrite the owned rows into an existing, pre-sized output file."""
-        require_native().write_raw_rows(path, self.output.reshape(-1), self.width, self.height, self.channels,
-                                        self.band.y0, self.band.rows)
+        require_native().write_raw_rows(path, self.outputs[slot].reshape(-1), self.width, self.height,
+                                        self.channels, self.band.y0, self.band.rows)

@@ -94,4 +94,71 @@ def test_shape_guard_rejects_out_of_frame(native):
     base = lay["pitch"] + 16
     with pytest.raises(RuntimeError, match="exceed frame"):
         native.launch_stencil("gaussian", "grey", src.data_ptr() + GUARD + base, dst.data_ptr() + GUARD + base,
-                              lay["pitch"], 64, -1, 8, -1, 9, 1, 0, 1 << 40, 0, "auto")
+                              lay["pitch"], 64, -1, 8, -1, 9, 1, 100, 1 << 40, 0, "auto")
+
+
+def _run_fused(native, img, steps, r0, r1, halo, g_row0, height, variant="auto"):
+    """Run one fused launch on a band frame whose row 0 is global row g_row0;
+    returns (gpu_rows, cpu_rows) of the whole frame's data columns."""
+    import torch
+
+    h = img.shape[0]  # frame owned rows
+    row_bytes = img.size // h
+    ch = {1: "grey", 3: "rgb", 4: "rgba"}[img.size // (h * img.shape[1])]
+    lay, src = _frame(native, torch, row_bytes, h, halo)
+    _, dst = _frame(native, torch, row_bytes, h, halo)
+    full = np.zeros((h + 2 * halo, lay["pitch"]), np.uint8)
+    # fill ghost + owned rows that lie inside the image with random data
+    rng = np.random.default_rng(steps * 1000 + r0)
+    for fr in range(-halo, h + halo):
+        if 0 <= g_row0 + fr < height:
+            full[halo + fr, 16 : 16 + row_bytes] = rng.integers(0, 256, row_bytes, dtype=np.uint8)
+    src[GUARD : GUARD + lay["bytes"]] = torch.from_numpy(full.reshape(-1)).cuda()
+    base = lay["pitch"] * halo + 16
+    native.launch_stencil("gaussian", ch, src.data_ptr() + GUARD + base, dst.data_ptr() + GUARD + base,
+                          lay["pitch"], row_bytes, r0, r1, -halo, h + halo, steps, g_row0, height,
+                          torch.cuda.current_stream().cuda_stream, variant)
+    torch.cuda.synchronize()
+    d = dst.cpu().numpy()
+    assert (d[:GUARD] == CANARY).all() and (d[-GUARD:] == CANARY).all(), "write outside the frame"
+    gpu = d[GUARD:-GUARD].reshape(h + 2 * halo, lay["pitch"])
+    cpu = np.zeros(lay["bytes"], np.uint8)
+    native.cpu_fused_launch("gaussian", ch, row_bytes, h, halo, full.reshape(-1), cpu, r0, r1, steps, g_row0, height)
+    return gpu, cpu.reshape(h + 2 * halo, lay["pitch"])
+
+
+@pytest.mark.parametrize("channels", ["grey", "rgb", "rgba"])
+@pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 8, 11, 16])
+def test_temporal_matches_fused_reference(native, rng, channels, steps):
+    c = CH[channels]
+    for (h, w) in [(1, 3), (7, 5), (40, 33), (97, 130), (150, 700)]:
+        img = rng.integers(0, 256, size=(h, w, c) if c > 1 else (h, w), dtype=np.uint8)
+        gpu, cpu = _run_fused(native, img, steps, 0, h, steps, 0, h, variant="temporal")
+        assert np.array_equal(gpu, cpu), (h, w, steps)
+
+
+@pytest.mark.parametrize("steps", [2, 4, 8, 16])
+def test_temporal_band_regions(native, rng, steps):
+    """Bands in the middle / at the edges of a taller image, regions reaching
+    into ghost rows (what the distributed schedule asks for)."""
+    H = 300
+    h = 60
+    img = np.zeros((h, 45, 3), np.uint8)
+    halo = 16
+    for g_row0 in (0, 100, H - h):
+        for (r0, r1) in [(0, h), (-(halo - steps), h + (halo - steps)), (steps, h - steps), (-3, 5), (h - 2, h + 1)]:
+            if r0 - steps < -halo or r1 + steps > h + halo or r0 >= r1:
+                continue
+            gpu, cpu = _run_fused(native, img, steps, r0, r1, halo, g_row0, H)
+            fr0, fr1 = halo + r0, halo + r1
+            assert np.array_equal(gpu[fr0:fr1], cpu[fr0:fr1]), (g_row0, r0, r1, steps)
+            # nothing written outside [r0, r1)
+            assert (gpu[:fr0] == 0).all() and (gpu[fr1:] == 0).all()
+
+
+def test_temporal_equals_repeated_single_steps(pconv_mod, rng):
+    """A fused launch of T steps == T single-step launches (whole image)."""
+    img = rng.integers(0, 256, size=(123, 211, 3), dtype=np.uint8)
+    for t in (2, 6, 13):
+        got = _run_kernel(pconv_mod.native, img, "gaussian", "temporal", steps=t)
+        assert np.array_equal(got, pconv_mod.numpy_convolve(img, t)), t
