@@ -49,6 +49,11 @@ struct EngineOptions {
   bool overlap = true;     // interior || halo
   bool use_graph = false;  // capture the rep loop into a hipGraph (no transport)
   KernelVariant variant = KernelVariant::Auto;
+  // Borrowed streams (nullptr: the engine creates its own).  A process has
+  // few hardware queues (GPU_MAX_HW_QUEUES, 4 by default); pipeline slots
+  // share streams so that unrelated streams never alias one queue.
+  hipStream_t compute_stream = nullptr;
+  hipStream_t comm_stream = nullptr;
 };
 
 struct RunStats {
@@ -68,11 +73,8 @@ class BandEngine {
   const Filter& filter() const { return filter_; }
   const FrameLayout& layout() const { return lay_; }
   const EngineOptions& options() const { return opt_; }
-  hipStream_t compute_stream() const { return cs_.get(); }
-  hipStream_t comm_stream() const { return comm_override_ ? comm_override_ : ms_.get(); }
-  // Share one communication stream between engines (pipeline slots): keeps
-  // every RCCL call of a rank on one stream, in issue order.
-  void set_comm_stream(hipStream_t s) { comm_override_ = s; }
+  hipStream_t compute_stream() const { return cs_; }
+  hipStream_t comm_stream() const { return ms_; }
 
   void set_transport(std::shared_ptr<HaloTransport> t) { transport_ = std::move(t); }
 
@@ -100,6 +102,12 @@ class BandEngine {
   void wait_stream(hipStream_t s);
   void signal_stream(hipStream_t s);
 
+  // Fill all `halo` ghost rows now (transport on `stream`, default: the comm
+  // stream) and mark them valid: lets a pipeline exchange image k+1's halos
+  // while image k still computes.
+  void exchange_now(hipStream_t stream = nullptr);
+  bool has_transport() const { return transport_ != nullptr; }
+
   // Enqueue `reps` repetitions (async).  stats filled after synchronize().
   void run(int reps);
   // Phase-by-phase execution for multi-band emulation on one device.
@@ -125,8 +133,9 @@ class BandEngine {
   DeviceBuffer frame_[2];
   int cur_ = 0;
   bool halo_valid_ = false;
-  Stream cs_, ms_;
-  hipStream_t comm_override_ = nullptr;
+  int pre_exchanges_ = 0;  // exchange_now() calls since the last run()
+  Stream own_cs_, own_ms_;
+  hipStream_t cs_ = nullptr, ms_ = nullptr;
   Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_;
   std::shared_ptr<HaloTransport> transport_;
   RunStats stats_;
@@ -156,9 +165,9 @@ class BandPipeline {
   int64_t submitted() const { return count_; }
 
  private:
+  Stream compute_, h2d_, d2h_, comm_;
   std::vector<std::unique_ptr<BandEngine>> slots_;
-  Stream h2d_, d2h_, comm_;
-  std::vector<Event> ev_up_, ev_done_, ev_free_;
+  std::vector<Event> ev_up_, ev_done_, ev_free_, ev_halo_;
   std::vector<bool> used_;
   int64_t count_ = 0;
 };
@@ -180,6 +189,15 @@ class LocalCluster {
  private:
   ImageGeom geom_;
   std::vector<std::unique_ptr<BandEngine>> engines_;
+};
+
+// Timing-only transport: moves nothing.  Measures a band's compute schedule
+// (launches, shrinking ghost regions) on one GPU without its peers.  Results
+// of bands with neighbours are NOT correct under it.
+class NullTransport : public HaloTransport {
+ public:
+  void exchange(BandEngine&, int64_t, hipStream_t) override {}
+  const char* name() const override { return "null (timing only)"; }
 };
 
 // Transport used by LocalCluster (neighbour engines live on the same device).

@@ -43,9 +43,10 @@ struct StencilLaunch {
 enum class KernelVariant : int {
   Auto = 0,      // pick by filter / steps
   Binomial = 1,  // packed-u16 gaussian, 1 step per launch
-  Temporal = 2,  // packed-u16 gaussian, `steps` fused in registers
+  Temporal = 2,  // SWAR-32 gaussian, `steps` fused in registers (production)
   Int9 = 3,      // generic int-exact 9-tap
   Float9 = 4,    // generic float32 9-tap (reference rounding)
+  TemporalPk = 5,  // packed-u16 (VOP3P) fused gaussian, kept for A/B measurements
 };
 
 const char* kernel_variant_name(KernelVariant v);

@@ -94,6 +94,7 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       if (v == "auto") c.variant = KernelVariant::Auto;
       else if (v == "binomial") c.variant = KernelVariant::Binomial;
       else if (v == "temporal") c.variant = KernelVariant::Temporal;
+      else if (v == "temporal_pk") c.variant = KernelVariant::TemporalPk;
       else if (v == "int9") c.variant = KernelVariant::Int9;
       else if (v == "float9") c.variant = KernelVariant::Float9;
       else PCONV_FAIL("invalid --kernel '" + v + "'");

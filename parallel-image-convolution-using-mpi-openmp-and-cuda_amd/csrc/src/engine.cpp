@@ -33,8 +33,21 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
     f = DeviceBuffer(static_cast<size_t>(lay_.bytes()));
     PCONV_HIP_CHECK(hipMemset(f.data(), 0, f.size()));
   }
-  cs_ = Stream::create(0);
-  ms_ = Stream::create(-1);  // communication gets the higher priority
+  if (opt_.compute_stream) {
+    cs_ = opt_.compute_stream;
+  } else {
+    own_cs_ = Stream::create(0);
+    cs_ = own_cs_.get();
+  }
+  // Communication stream only when the band has neighbours (or is borrowed).
+  if (opt_.comm_stream) {
+    ms_ = opt_.comm_stream;
+  } else if (band_.up >= 0 || band_.down >= 0) {
+    own_ms_ = Stream::create(-1);  // communication gets the higher priority
+    ms_ = own_ms_.get();
+  } else {
+    ms_ = cs_;
+  }
   ev_ready_ = Event::create();
   ev_halo_ = Event::create();
   ev_sync_ = Event::create();
@@ -45,8 +58,8 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
 
 BandEngine::~BandEngine() {
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
-  if (cs_.get()) (void)hipStreamSynchronize(cs_.get());
-  if (ms_.get()) (void)hipStreamSynchronize(ms_.get());
+  if (cs_) (void)hipStreamSynchronize(cs_);
+  if (ms_) (void)hipStreamSynchronize(ms_);
 }
 
 void BandEngine::clear() {
@@ -64,7 +77,7 @@ void BandEngine::upload_rows(const uint8_t* host, int64_t host_pitch, int64_t r_
   PCONV_CHECK(band_.y0 + r_begin >= 0 && band_.y0 + r_end <= geom_.height, "upload_rows: rows outside image");
   if (r_end == r_begin) return;
   PCONV_HIP_CHECK(hipMemcpy2DAsync(src_frame() + r_begin * lay_.pitch, lay_.pitch, host, host_pitch, lay_.row_bytes,
-                                   r_end - r_begin, hipMemcpyHostToDevice, stream ? stream : cs_.get()));
+                                   r_end - r_begin, hipMemcpyHostToDevice, stream ? stream : cs_));
 }
 
 void BandEngine::upload_rows_device(const uint8_t* dev, int64_t dev_pitch, int64_t r_begin, int64_t r_end) {
@@ -73,7 +86,7 @@ void BandEngine::upload_rows_device(const uint8_t* dev, int64_t dev_pitch, int64
   PCONV_CHECK(band_.y0 + r_begin >= 0 && band_.y0 + r_end <= geom_.height, "upload_rows_device: rows outside image");
   if (r_end == r_begin) return;
   PCONV_HIP_CHECK(hipMemcpy2DAsync(src_frame() + r_begin * lay_.pitch, lay_.pitch, dev, dev_pitch, lay_.row_bytes,
-                                   r_end - r_begin, hipMemcpyDeviceToDevice, cs_.get()));
+                                   r_end - r_begin, hipMemcpyDeviceToDevice, cs_));
 }
 
 void BandEngine::download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end,
@@ -81,23 +94,23 @@ void BandEngine::download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begi
   PCONV_CHECK(r_begin >= 0 && r_end <= lay_.rows && r_begin <= r_end, "download_rows: rows outside band");
   if (r_end == r_begin) return;
   PCONV_HIP_CHECK(hipMemcpy2DAsync(host, host_pitch, src_frame() + r_begin * lay_.pitch, lay_.pitch, lay_.row_bytes,
-                                   r_end - r_begin, hipMemcpyDeviceToHost, stream ? stream : cs_.get()));
+                                   r_end - r_begin, hipMemcpyDeviceToHost, stream ? stream : cs_));
 }
 
 void BandEngine::download_rows_device(uint8_t* dev, int64_t dev_pitch, int64_t r_begin, int64_t r_end) {
   PCONV_CHECK(r_begin >= 0 && r_end <= lay_.rows && r_begin <= r_end, "download_rows_device: rows outside band");
   if (r_end == r_begin) return;
   PCONV_HIP_CHECK(hipMemcpy2DAsync(dev, dev_pitch, src_frame() + r_begin * lay_.pitch, lay_.pitch, lay_.row_bytes,
-                                   r_end - r_begin, hipMemcpyDeviceToDevice, cs_.get()));
+                                   r_end - r_begin, hipMemcpyDeviceToDevice, cs_));
 }
 
 void BandEngine::wait_stream(hipStream_t s) {
   ev_sync_.record(s);
-  ev_sync_.wait_on(cs_.get());
+  ev_sync_.wait_on(cs_);
 }
 
 void BandEngine::signal_stream(hipStream_t s) {
-  ev_sync_.record(cs_.get());
+  ev_sync_.record(cs_);
   ev_sync_.wait_on(s);
 }
 
@@ -128,28 +141,41 @@ void BandEngine::enqueue_phase(const Phase& p) {
   if (p.exchange_depth > 0) {
     PCONV_CHECK(transport_ != nullptr, "band has neighbours but no halo transport is attached");
     hipStream_t ms = comm_stream();
-    ev_ready_.record(cs_.get());
+    ev_ready_.record(cs_);
     ev_ready_.wait_on(ms);
     transport_->exchange(*this, p.exchange_depth, ms);
     ev_halo_.record(ms);
     for (const auto& l : p.launches)
-      if (!l.after_halo) launch(l, cs_.get());
-    ev_halo_.wait_on(cs_.get());
+      if (!l.after_halo) launch(l, cs_);
+    ev_halo_.wait_on(cs_);
     for (const auto& l : p.launches)
-      if (l.after_halo) launch(l, cs_.get());
+      if (l.after_halo) launch(l, cs_);
     ++stats_.exchanges;
   } else {
-    for (const auto& l : p.launches) launch(l, cs_.get());
+    for (const auto& l : p.launches) launch(l, cs_);
   }
   cur_ ^= 1;
+}
+
+void BandEngine::exchange_now(hipStream_t stream) {
+  if (band_.up < 0 && band_.down < 0) {
+    halo_valid_ = true;
+    return;
+  }
+  PCONV_CHECK(transport_ != nullptr, "band has neighbours but no halo transport is attached");
+  transport_->exchange(*this, lay_.halo, stream ? stream : ms_);
+  halo_valid_ = true;
+  ++pre_exchanges_;
 }
 
 void BandEngine::run(int reps) {
   PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
   const std::vector<Phase> ph = plan(reps);
   stats_ = RunStats{};
+  stats_.exchanges = pre_exchanges_;
+  pre_exchanges_ = 0;
   wall_t0_ = wall_seconds();
-  ev_t0_.record(cs_.get());
+  ev_t0_.record(cs_);
   const bool graph = opt_.use_graph && !transport_ && !ph.empty();
   if (graph) {
     const auto key = std::make_pair(reps, cur_);
@@ -157,9 +183,9 @@ void BandEngine::run(int reps) {
     const int start = cur_;
     if (it == graphs_.end()) {
       hipGraph_t g = nullptr;
-      PCONV_HIP_CHECK(hipStreamBeginCapture(cs_.get(), hipStreamCaptureModeThreadLocal));
+      PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeThreadLocal));
       for (const auto& p : ph) enqueue_phase(p);
-      PCONV_HIP_CHECK(hipStreamEndCapture(cs_.get(), &g));
+      PCONV_HIP_CHECK(hipStreamEndCapture(cs_, &g));
       hipGraphExec_t ex = nullptr;
       PCONV_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
       PCONV_HIP_CHECK(hipGraphDestroy(g));
@@ -171,11 +197,11 @@ void BandEngine::run(int reps) {
       }
     }
     (void)start;
-    PCONV_HIP_CHECK(hipGraphLaunch(it->second, cs_.get()));
+    PCONV_HIP_CHECK(hipGraphLaunch(it->second, cs_));
   } else {
     for (const auto& p : ph) enqueue_phase(p);
   }
-  ev_t1_.record(cs_.get());
+  ev_t1_.record(cs_);
   timing_pending_ = true;
   halo_valid_ = false;
 }
@@ -183,18 +209,18 @@ void BandEngine::run(int reps) {
 void BandEngine::exec_exchange(const Phase& p) {
   if (p.exchange_depth <= 0) return;
   PCONV_CHECK(transport_ != nullptr, "band has neighbours but no halo transport is attached");
-  transport_->exchange(*this, p.exchange_depth, cs_.get());
+  transport_->exchange(*this, p.exchange_depth, cs_);
   ++stats_.exchanges;
 }
 
 void BandEngine::exec_compute(const Phase& p) {
-  for (const auto& l : p.launches) launch(l, cs_.get());
+  for (const auto& l : p.launches) launch(l, cs_);
   cur_ ^= 1;
 }
 
 void BandEngine::synchronize() {
-  cs_.sync();
-  PCONV_HIP_CHECK(hipStreamSynchronize(comm_stream()));
+  PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
+  if (ms_ != cs_) PCONV_HIP_CHECK(hipStreamSynchronize(ms_));
   if (timing_pending_) {
     stats_.loop_ms = Event::elapsed_ms(ev_t0_, ev_t1_);
     stats_.wall_ms = (wall_seconds() - wall_t0_) * 1e3;
@@ -207,25 +233,35 @@ void BandEngine::synchronize() {
 BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt,
                            int slots) {
   PCONV_CHECK(slots >= 1 && slots <= 8, "pipeline slots must be in [1, 8]");
-  EngineOptions o = opt;
-  o.use_graph = false;  // copies/events interleave with the loop
-  for (int i = 0; i < slots; ++i) slots_.push_back(std::make_unique<BandEngine>(geom, band, filter, o));
+  set_device(opt.device);
+  // Four streams in all (= the default number of hardware queues): compute
+  // (shared by every slot: one GPU runs one image's reps at a time), H2D,
+  // D2H and — only with neighbours — communication.
+  compute_ = Stream::create(0);
   h2d_ = Stream::create(0);
   d2h_ = Stream::create(0);
-  comm_ = Stream::create(-1);
+  EngineOptions o = opt;
+  o.use_graph = false;  // copies/events interleave with the loop
+  o.compute_stream = compute_.get();
+  if (band.up >= 0 || band.down >= 0) {
+    comm_ = Stream::create(-1);
+    o.comm_stream = comm_.get();
+  }
   for (int i = 0; i < slots; ++i) {
+    slots_.push_back(std::make_unique<BandEngine>(geom, band, filter, o));
     ev_up_.push_back(Event::create());
     ev_done_.push_back(Event::create());
     ev_free_.push_back(Event::create());
-    slots_[i]->set_comm_stream(comm_.get());
+    ev_halo_.push_back(Event::create());
   }
   used_.assign(slots, false);
 }
 
 BandPipeline::~BandPipeline() {
   (void)hipStreamSynchronize(h2d_.get());
+  (void)hipStreamSynchronize(compute_.get());
   (void)hipStreamSynchronize(d2h_.get());
-  (void)hipStreamSynchronize(comm_.get());
+  if (comm_.get()) (void)hipStreamSynchronize(comm_.get());
 }
 
 void BandPipeline::set_transport(std::shared_ptr<HaloTransport> t) {
@@ -239,9 +275,19 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   if (used_[k]) ev_free_[k].wait_on(h2d_.get());
   e.upload_rows(host_in, e.layout().row_bytes, in_r0, in_r1, h2d_.get());
   ev_up_[k].record(h2d_.get());
-  // reps on the slot's compute stream (halo exchanges on the shared comm stream)
-  ev_up_[k].wait_on(e.compute_stream());
-  e.set_halo_valid(in_r0 < 0 || in_r1 > e.band().rows);
+  const bool preloaded = in_r0 < 0 || in_r1 > e.band().rows;
+  e.set_halo_valid(preloaded);
+  if (!preloaded && comm_.get() && e.has_transport() && reps > 0) {
+    // Exchange this image's ghost rows as soon as it is uploaded — on the
+    // comm stream, concurrently with the previous image's repetitions.
+    ev_up_[k].wait_on(comm_.get());
+    e.exchange_now(comm_.get());
+    ev_halo_[k].record(comm_.get());
+    ev_halo_[k].wait_on(e.compute_stream());
+  } else {
+    ev_up_[k].wait_on(e.compute_stream());
+  }
+  // reps on the shared compute stream (later exchanges on the comm stream)
   e.run(reps);
   ev_done_[k].record(e.compute_stream());
   // D2H of the owned rows

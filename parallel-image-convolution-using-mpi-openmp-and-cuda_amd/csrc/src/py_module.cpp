@@ -53,6 +53,7 @@ KernelVariant parse_variant(const std::string& s) {
   if (s == "auto") return KernelVariant::Auto;
   if (s == "binomial") return KernelVariant::Binomial;
   if (s == "temporal") return KernelVariant::Temporal;
+  if (s == "temporal_pk") return KernelVariant::TemporalPk;
   if (s == "int9") return KernelVariant::Int9;
   if (s == "float9") return KernelVariant::Float9;
   PCONV_FAIL("unknown kernel variant '" + s + "'");
@@ -418,7 +419,9 @@ PYBIND11_MODULE(_pconv_native, m) {
              e.set_transport(std::make_shared<RcclTransport>(std::move(c)));
            })
       .def("attach_transport", [](BandEngine& e, std::shared_ptr<HaloTransport> t) { e.set_transport(std::move(t)); },
-           py::keep_alive<1, 2>());
+           py::keep_alive<1, 2>())
+      .def("attach_null_transport",
+           [](BandEngine& e) { e.set_transport(std::make_shared<NullTransport>()); });
 
   py::class_<BandPipeline>(m, "BandPipeline")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,

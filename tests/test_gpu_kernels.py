@@ -127,18 +127,24 @@ def _run_fused(native, img, steps, r0, r1, halo, g_row0, height, variant="auto")
     return gpu, cpu.reshape(h + 2 * halo, lay["pitch"])
 
 
+@pytest.mark.parametrize("variant", ["temporal", "temporal_pk"])
 @pytest.mark.parametrize("channels", ["grey", "rgb", "rgba"])
 @pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 8, 11, 16])
-def test_temporal_matches_fused_reference(native, rng, channels, steps):
+def test_temporal_matches_fused_reference(native, rng, channels, steps, variant):
     c = CH[channels]
-    for (h, w) in [(1, 3), (7, 5), (40, 33), (97, 130), (150, 700)]:
+    for (h, w) in [(1, 3), (7, 5), (40, 33), (97, 130), (150, 700), (33, 1500)]:
         img = rng.integers(0, 256, size=(h, w, c) if c > 1 else (h, w), dtype=np.uint8)
-        gpu, cpu = _run_fused(native, img, steps, 0, h, steps, 0, h, variant="temporal")
+        gpu, cpu = _run_fused(native, img, steps, 0, h, steps, 0, h, variant=variant)
         assert np.array_equal(gpu, cpu), (h, w, steps)
 
 
 @pytest.mark.parametrize("steps", [2, 4, 8, 16])
 def test_temporal_band_regions(native, rng, steps):
+    _band_regions(native, steps, "temporal")
+    _band_regions(native, steps, "temporal_pk")
+
+
+def _band_regions(native, steps, variant):
     """Bands in the middle / at the edges of a taller image, regions reaching
     into ghost rows (what the distributed schedule asks for)."""
     H = 300
@@ -149,9 +155,9 @@ def test_temporal_band_regions(native, rng, steps):
         for (r0, r1) in [(0, h), (-(halo - steps), h + (halo - steps)), (steps, h - steps), (-3, 5), (h - 2, h + 1)]:
             if r0 - steps < -halo or r1 + steps > h + halo or r0 >= r1:
                 continue
-            gpu, cpu = _run_fused(native, img, steps, r0, r1, halo, g_row0, H)
+            gpu, cpu = _run_fused(native, img, steps, r0, r1, halo, g_row0, H, variant=variant)
             fr0, fr1 = halo + r0, halo + r1
-            assert np.array_equal(gpu[fr0:fr1], cpu[fr0:fr1]), (g_row0, r0, r1, steps)
+            assert np.array_equal(gpu[fr0:fr1], cpu[fr0:fr1]), (variant, g_row0, r0, r1, steps)
             # nothing written outside [r0, r1)
             assert (gpu[:fr0] == 0).all() and (gpu[fr1:] == 0).all()
 

@@ -1,0 +1,107 @@
+// PCIe copy bandwidth for the serving pipeline's shapes (pinned host memory):
+// contiguous vs pitched (hipMemcpy2DAsync into a padded frame), H2D, D2H and
+// both directions at once on two streams.
+// build: hipcc --offload-arch=gfx950 -O3 tools/ubench/copy_bw.hip -o tools/ubench/copy_bw
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#define CHECK(x)                                                        \
+  do {                                                                  \
+    hipError_t e = (x);                                                 \
+    if (e != hipSuccess) {                                              \
+      printf("HIP error %s at line %d\n", hipGetErrorString(e), __LINE__); \
+      return 1;                                                         \
+    }                                                                   \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const size_t W = 5760, H = 2520, P = 5888;  // 1920x2520 RGB row bytes, frame pitch
+  const size_t bytes = W * H;
+  void *h_in, *h_out, *d_a, *d_b;
+  CHECK(hipHostMalloc(&h_in, bytes, 0));
+  CHECK(hipHostMalloc(&h_out, bytes, 0));
+  CHECK(hipMalloc(&d_a, P * (H + 16)));
+  CHECK(hipMalloc(&d_b, P * (H + 16)));
+  hipStream_t s1, s2;
+  CHECK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+  CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  const int iters = 20;
+  auto report = [&](const char* name, float ms, double gb) {
+    printf("%-34s %8.3f ms/iter  %6.1f GB/s\n", name, ms / iters, gb * iters / (ms * 1e-3));
+  };
+  for (int round = 0; round < 2; ++round) {
+    float ms;
+    // H2D contiguous
+    CHECK(hipEventRecord(e0, s1));
+    for (int i = 0; i < iters; ++i) CHECK(hipMemcpyAsync(d_a, h_in, bytes, hipMemcpyHostToDevice, s1));
+    CHECK(hipEventRecord(e1, s1));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    report("H2D contiguous", ms, bytes / 1e9);
+    // H2D pitched
+    CHECK(hipEventRecord(e0, s1));
+    for (int i = 0; i < iters; ++i)
+      CHECK(hipMemcpy2DAsync((char*)d_a + 16, P, h_in, W, W, H, hipMemcpyHostToDevice, s1));
+    CHECK(hipEventRecord(e1, s1));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    report("H2D pitched (2D)", ms, bytes / 1e9);
+    // D2H contiguous
+    CHECK(hipEventRecord(e0, s1));
+    for (int i = 0; i < iters; ++i) CHECK(hipMemcpyAsync(h_out, d_b, bytes, hipMemcpyDeviceToHost, s1));
+    CHECK(hipEventRecord(e1, s1));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    report("D2H contiguous", ms, bytes / 1e9);
+    // D2H pitched
+    CHECK(hipEventRecord(e0, s1));
+    for (int i = 0; i < iters; ++i)
+      CHECK(hipMemcpy2DAsync(h_out, W, (char*)d_b + 16, P, W, H, hipMemcpyDeviceToHost, s1));
+    CHECK(hipEventRecord(e1, s1));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    report("D2H pitched (2D)", ms, bytes / 1e9);
+    // both directions concurrently (pitched), two streams; wall by host events
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(e0, 0));
+    CHECK(hipStreamWaitEvent(s1, e0, 0));
+    CHECK(hipStreamWaitEvent(s2, e0, 0));
+    for (int i = 0; i < iters; ++i) {
+      CHECK(hipMemcpy2DAsync((char*)d_a + 16, P, h_in, W, W, H, hipMemcpyHostToDevice, s1));
+      CHECK(hipMemcpy2DAsync(h_out, W, (char*)d_b + 16, P, W, H, hipMemcpyDeviceToHost, s2));
+    }
+    hipEvent_t ea, eb;
+    CHECK(hipEventCreate(&ea));
+    CHECK(hipEventCreate(&eb));
+    CHECK(hipEventRecord(ea, s1));
+    CHECK(hipEventRecord(eb, s2));
+    CHECK(hipStreamWaitEvent(0, ea, 0));
+    CHECK(hipStreamWaitEvent(0, eb, 0));
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    report("H2D+D2H concurrent (per pair)", ms, 2 * bytes / 1e9);
+    // concurrent contiguous
+    CHECK(hipEventRecord(e0, 0));
+    CHECK(hipStreamWaitEvent(s1, e0, 0));
+    CHECK(hipStreamWaitEvent(s2, e0, 0));
+    for (int i = 0; i < iters; ++i) {
+      CHECK(hipMemcpyAsync(d_a, h_in, bytes, hipMemcpyHostToDevice, s1));
+      CHECK(hipMemcpyAsync(h_out, d_b, bytes, hipMemcpyDeviceToHost, s2));
+    }
+    CHECK(hipEventRecord(ea, s1));
+    CHECK(hipEventRecord(eb, s2));
+    CHECK(hipStreamWaitEvent(0, ea, 0));
+    CHECK(hipStreamWaitEvent(0, eb, 0));
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    report("H2D+D2H concurrent contiguous", ms, 2 * bytes / 1e9);
+  }
+  return 0;
+}
