@@ -51,11 +51,19 @@ def parse():
     p.add_argument("--variant", default="auto")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--slots", type=int, default=3, help="images in flight (H2D/compute/D2H overlap)")
+    p.add_argument("--concurrent", choices=["auto", "on", "off"], default="off",
+                   help="one compute stream per image in flight (default: one shared compute stream)")
     return p.parse_args()
 
 
 def main():
     a = parse()
+    # One hardware queue per stream of the serving pipeline (H2D, D2H, comm and
+    # one compute stream per image in flight) so independent streams never
+    # alias a queue; must be set before the HIP runtime initialises.
+    want = max(8, a.slots + 3)
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < want:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want)
     import torch
 
     import pconv
@@ -70,7 +78,8 @@ def main():
 
     blur = DistributedBlur(a.width, a.height, a.channels, a.filter, a.reps, rank=ctx.rank, world=world,
                            device=ctx.local_rank, halo=a.halo, fuse=a.fuse, overlap=not a.no_overlap,
-                           preload_halo=a.preload_halo, slots=a.slots, variant=a.variant)
+                           preload_halo=a.preload_halo, slots=a.slots, variant=a.variant,
+                           concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent])
     blur.load_synthetic(a.seed)
 
     for _ in range(a.warmup):
@@ -131,6 +140,7 @@ def main():
                 "parallelism": f"rowband{world}",
                 "step": "H2D + reps + D2H per image (reference GPU_convolution scope)",
                 "images_in_flight": a.slots,
+                "concurrent_images": bool(blur.pipe.concurrent),
                 "halo_depth": int(blur.engine.halo),
                 "fuse": int(blur.engine.fuse),
                 "preload_halo": bool(blur.preload_halo),

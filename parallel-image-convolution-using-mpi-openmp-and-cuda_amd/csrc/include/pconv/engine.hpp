@@ -54,6 +54,9 @@ struct EngineOptions {
   // share streams so that unrelated streams never alias one queue.
   hipStream_t compute_stream = nullptr;
   hipStream_t comm_stream = nullptr;
+  // hipEvent loop timing around every run() (two event records, ~3 us of
+  // host time each on ROCm 7: the serving pipeline turns it off).
+  bool timing = true;
 };
 
 struct RunStats {
@@ -152,7 +155,10 @@ class BandEngine {
 // events; all slots of a rank share one communication stream.
 class BandPipeline {
  public:
-  BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt, int slots);
+  // concurrent: -1 = when the hardware-queue budget allows, 0 = one shared
+  // compute stream, 1 = one compute stream per slot.
+  BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt, int slots,
+               int concurrent = -1);
   ~BandPipeline();
   int slots() const { return static_cast<int>(slots_.size()); }
   BandEngine& slot(int i) { return *slots_.at(i); }
@@ -163,9 +169,13 @@ class BandPipeline {
   void submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps);
   void drain();
   int64_t submitted() const { return count_; }
+  // True when slots run their repetitions on separate compute streams.
+  bool concurrent() const { return concurrent_; }
 
  private:
-  Stream compute_, h2d_, d2h_, comm_;
+  Stream h2d_, d2h_, comm_;
+  std::vector<Stream> computes_;
+  bool concurrent_ = false;
   std::vector<std::unique_ptr<BandEngine>> slots_;
   std::vector<Event> ev_up_, ev_done_, ev_free_, ev_halo_;
   std::vector<bool> used_;

@@ -21,6 +21,7 @@
 
 #include "pconv/kernels.hpp"
 #include "pconv/device.hpp"
+#include "swar.hpp"
 
 namespace pconv {
 namespace {
@@ -416,184 +417,6 @@ TemporalShape pick_temporal_shape(int steps) {
   return {16, 4};                   // 64-row tile, >= 32 valid
 }
 
-// ---------------------------------------------------------------------------
-// Temporal-blocked gaussian, SWAR-32 form (the production fused kernel).
-//
-// Measured on gfx950 (tools/ubench/isa_rates.hip): packed 16-bit VOP3P ops
-// (v_pk_add_u16, v_pk_mad_u16, v_pk_lshrrev_b16) and v_perm_b32 issue at
-// HALF the rate of plain 32-bit VALU ops, while v_add_u32 / v_lshl_add_u32 /
-// v_alignbit_b32 run at full rate.  Two 16-bit fields in a u32 never carry
-// into each other here (every sum stays < 4080 < 2^16), so plain 32-bit adds
-// do the packed work at twice the throughput.
-//
-// Layout: a lane holds, per row, eight u32 "pairs" P_k = (A_k, B_k): A_k is
-// byte k of the lane's 8-byte chunk in column strip A, B_k the same byte of
-// strip B (a second 512-byte strip of the row).  The horizontal neighbour of
-// P_k at distance CH is P_{k±CH}, or — across the lane boundary — the
-// neighbouring lane's whole register, which the hardware delivers with a DPP
-// wave_shr/wave_shl folded into the add (v_add_u32_dpp): no byte shuffles in
-// the stepping loop at all.  Per pair per step: 2 ops horizontal
-// (v_add_u32[_dpp], v_lshl_add_u32), 2 vertical (v_add_u32 x2 on a rolling
-// sum), 2 truncation (v_lshrrev_b32, v_and_b32) — all full rate.
-// Tiles, halos, LDS boundary exchange and zero-padding masks as in
-// k_temporal above.
-// ---------------------------------------------------------------------------
-template <int CH>
-__device__ __forceinline__ void horiz_swar(const u32 (&X)[8], u32 (&H)[8]) {
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int l = k - CH, r = k + CH;
-    const u32 lv = l >= 0 ? X[l] : __builtin_amdgcn_mov_dpp(X[8 + l], 0x138, 0xf, 0xf, true);  // wave_shr:1
-    const u32 rv = r < 8 ? X[r] : __builtin_amdgcn_mov_dpp(X[r - 8], 0x130, 0xf, 0xf, true);   // wave_shl:1
-    H[k] = (X[k] << 1) + (lv + rv);
-  }
-}
-
-template <int CH, int M, int NW>
-__global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                  int64_t pitch, int row_bytes, int r0, int r1, int steps, int g_row0,
-                                                  int height, int nstrips, int pair_stride) {
-  __shared__ uint4 lds[2][NW][2][2][64];  // [parity][wave][top/bottom][half][lane]
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int hl = (steps * CH + 7) >> 3;    // halo lanes per side (8 bytes per lane)
-  const int vbytes = (64 - 2 * hl) * 8;    // valid output bytes per strip
-  const int sA = blockIdx.x, sB = blockIdx.x + pair_stride;
-  const bool hasB = sB < nstrips;
-  const int baseA = sA * vbytes - hl * 8, baseB = sB * vbytes - hl * 8;  // strip starts (bytes)
-  const int xA = baseA + lane * 8, xB = baseB + lane * 8;
-  const int validA = (xA >= 0) ? min(max(row_bytes - xA, 0), 8) : 0;
-  const int validB = (hasB && xB >= 0) ? min(max(row_bytes - xB, 0), 8) : 0;
-  const bool needs_mask = baseA < 0 || baseA + 512 > row_bytes || !hasB || baseB + 512 > row_bytes;
-  u32 cm[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) cm[k] = (k < validA ? 0xffffu : 0u) | (k < validB ? 0xffff0000u : 0u);
-
-  const int vrows = NW * M - 2 * steps;
-  const int tile_r0 = r0 + static_cast<int>(blockIdx.y) * vrows;
-  const int row_base = tile_r0 - steps + w * M;
-  const int lo_ok = max(r0 - steps, -g_row0), hi_ok = min(r1 + steps, height - g_row0);
-
-  u32 D[M][8];
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    const int fr = row_base + i;
-    const bool rok = fr >= lo_ok && fr < hi_ok;
-    uint2 a = make_uint2(0, 0), b = make_uint2(0, 0);
-    const uint8_t* rowp = src + static_cast<int64_t>(fr) * pitch;
-    if (rok && validA > 0) a = *reinterpret_cast<const uint2*>(rowp + xA);
-    if (rok && validB > 0) b = *reinterpret_cast<const uint2*>(rowp + xB);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      D[i][k] = perm(b.x, a.x, pair_sel(k));
-      D[i][4 + k] = perm(b.y, a.y, pair_sel(k));
-    }
-  }
-  const int out_top = min(max(-g_row0 - row_base, 0), M);
-  const int out_bot = min(max(height - g_row0 - row_base, 0), M);
-
-  for (int s = 0; s < steps; ++s) {
-    const int par = s & 1;
-    lds[par][w][0][0][lane] = make_uint4(D[0][0], D[0][1], D[0][2], D[0][3]);
-    lds[par][w][0][1][lane] = make_uint4(D[0][4], D[0][5], D[0][6], D[0][7]);
-    lds[par][w][1][0][lane] = make_uint4(D[M - 1][0], D[M - 1][1], D[M - 1][2], D[M - 1][3]);
-    lds[par][w][1][1][lane] = make_uint4(D[M - 1][4], D[M - 1][5], D[M - 1][6], D[M - 1][7]);
-    __syncthreads();
-    u32 A[8], B[8];
-    {
-      const int wa = w > 0 ? w - 1 : 0;
-      const int wb = w < NW - 1 ? w + 1 : w;
-      const uint4 a0 = lds[par][wa][1][0][lane], a1 = lds[par][wa][1][1][lane];
-      const uint4 b0 = lds[par][wb][0][0][lane], b1 = lds[par][wb][0][1][lane];
-      A[0] = a0.x; A[1] = a0.y; A[2] = a0.z; A[3] = a0.w; A[4] = a1.x; A[5] = a1.y; A[6] = a1.z; A[7] = a1.w;
-      B[0] = b0.x; B[1] = b0.y; B[2] = b0.z; B[3] = b0.w; B[4] = b1.x; B[5] = b1.y; B[6] = b1.z; B[7] = b1.w;
-    }
-    u32 Hc[8], Sc[8];
-    {
-      u32 Ha[8];
-      horiz_swar<CH>(A, Ha);
-      horiz_swar<CH>(D[0], Hc);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) Sc[k] = Ha[k] + Hc[k];
-    }
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      u32 Hn[8];
-      if (i + 1 < M)
-        horiz_swar<CH>(D[i + 1], Hn);
-      else
-        horiz_swar<CH>(B, Hn);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const u32 Sn = Hc[k] + Hn[k];
-        D[i][k] = ((Sc[k] + Sn) >> 4) & 0x00ff00ffu;
-        Sc[k] = Sn;
-        Hc[k] = Hn[k];
-      }
-    }
-    if (needs_mask) {
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) D[i][k] &= cm[k];
-    }
-    if (out_top > 0 || out_bot < M) {
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-        if (i < out_top || i >= out_bot)
-#pragma unroll
-          for (int k = 0; k < 8; ++k) D[i][k] = 0;
-    }
-  }
-
-  const bool lane_in = lane >= hl && lane < 64 - hl;
-  const bool stA = lane_in && validA > 0, stB = lane_in && validB > 0;
-  const int st_lo = max(tile_r0, r0), st_hi = min(min(tile_r0 + vrows, r1), height - g_row0);
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    const int fr = row_base + i;
-    if (fr >= st_lo && fr < st_hi) {
-      const u32 t0 = perm(D[i][1], D[i][0], 0x06020400u);  // A0 A1 B0 B1
-      const u32 t1 = perm(D[i][3], D[i][2], 0x06020400u);  // A2 A3 B2 B3
-      const u32 t2 = perm(D[i][5], D[i][4], 0x06020400u);
-      const u32 t3 = perm(D[i][7], D[i][6], 0x06020400u);
-      uint8_t* rowq = dst + static_cast<int64_t>(fr) * pitch;
-      if (stA) *reinterpret_cast<uint2*>(rowq + xA) = make_uint2(perm(t1, t0, 0x05040100u), perm(t3, t2, 0x05040100u));
-      if (stB) *reinterpret_cast<uint2*>(rowq + xB) = make_uint2(perm(t1, t0, 0x07060302u), perm(t3, t2, 0x07060302u));
-    }
-  }
-}
-
-template <int CH>
-void launch_swar(const StencilLaunch& a, hipStream_t s, TemporalShape sh) {
-  const int steps = a.steps;
-  const int hl = (steps * CH + 7) / 8;
-  const int vbytes = (64 - 2 * hl) * 8;
-  const int vrows = sh.m * sh.nw - 2 * steps;
-  PCONV_CHECK(vbytes > 0 && vrows > 0, "swar temporal kernel: steps too large for the tile");
-  const int nstrips = static_cast<int>(ceil_div<int64_t>(a.row_bytes, vbytes));
-  const int pair_stride = (nstrips + 1) / 2;
-  const dim3 grid(pair_stride, ceil_div(static_cast<int>(a.r1 - a.r0), vrows));
-  const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
-#define PCONV_SWAR(M_, NW_)                                                                                       \
-  if (sh.m == M_ && sh.nw == NW_) {                                                                               \
-    k_swar<CH, M_, NW_><<<grid, dim3(64 * NW_), 0, s>>>(a.src, a.dst, a.pitch, static_cast<int>(a.row_bytes),      \
-                                                        static_cast<int>(a.r0), static_cast<int>(a.r1), steps,     \
-                                                        static_cast<int>(a.g_row0), static_cast<int>(hmax), nstrips, \
-                                                        pair_stride);                                              \
-    return;                                                                                                       \
-  }
-  PCONV_SWAR(8, 4)
-  PCONV_SWAR(8, 8)
-  PCONV_SWAR(16, 4)
-  PCONV_SWAR(4, 8)
-  PCONV_SWAR(4, 16)
-  PCONV_SWAR(2, 16)
-  PCONV_SWAR(4, 4)
-#undef PCONV_SWAR
-  PCONV_FAIL("swar temporal kernel: unsupported tile shape");
-}
-
 constexpr int kRowsPerLane = 4;
 
 template <int CH>
@@ -641,53 +464,6 @@ bool supports_fusion(const Filter& f, KernelVariant v) {
          (v == KernelVariant::Auto || v == KernelVariant::Temporal || v == KernelVariant::TemporalPk);
 }
 
-namespace {
-// Tile shape for the SWAR temporal kernel, from a latency model of one launch
-// on 256 CUs x 4 SIMDs.  Inputs measured on gfx950: a SIMD retires one VALU
-// wave-instruction per ~5.8 cycles with one resident wave, ~2.9 with two,
-// ~2.8 with three or more (tools/ubench/isa_rates.hip); workgroups per CU are
-// bounded by LDS (NW x 8 KiB of boundary-row buffers) and VGPRs (by M).  Big
-// images pick the least redundant tile; small bands (the 8-GPU split of a
-// small image) pick smaller tiles that spread over more CUs.
-double swar_launch_cycles(TemporalShape c, int steps, int ch, int64_t rows, int64_t row_bytes) {
-  const int hl = (steps * ch + 7) / 8;
-  const int64_t vbytes = (64 - 2 * hl) * 8;
-  const int64_t pairs = (ceil_div<int64_t>(row_bytes, vbytes) + 1) / 2;
-  const int vrows = c.m * c.nw - 2 * steps;
-  if (vrows <= 0 || vbytes <= 0) return 1e300;
-  const double g = static_cast<double>(pairs * ceil_div<int64_t>(rows, vrows));
-  const double instr = steps * ((c.m + 2) * (18.0 + 2 * ch) + c.m * 32.0) + 80.0;  // per wave
-  const int vgpr_waves = c.m <= 2 ? 8 : c.m <= 4 ? 6 : c.m <= 8 ? 4 : 2;             // per SIMD
-  const int lds_wgs = (160 * 1024) / (c.nw * 8 * 1024);
-  const int L = std::max(1, std::min({lds_wgs, vgpr_waves * 4 / c.nw, 8}));
-  const double per_cu = std::ceil(g / 256.0);
-  const double rounds = std::ceil(per_cu / L);
-  const double conc = std::min<double>(per_cu, L);
-  const double wps = conc * c.nw / 4.0;
-  const double rate = wps >= 3 ? 2.8 : wps >= 2 ? 2.9 : 5.8;
-  return rounds * (conc * c.nw * instr / 4.0 * rate + 4000.0 + steps * 400.0);
-}
-
-TemporalShape pick_swar_shape(int steps, int ch, int64_t rows, int64_t row_bytes) {
-  const TemporalShape cands[] = {{8, 8}, {16, 4}, {8, 4}, {4, 8}, {4, 16}, {2, 16}, {4, 4}};
-  // Tuning override (tools/kernel_sweep.py): PCONV_SWAR_SHAPE="M,NW".
-  if (const char* env = std::getenv("PCONV_SWAR_SHAPE")) {
-    int m = 0, nw = 0;
-    if (std::sscanf(env, "%d,%d", &m, &nw) == 2 && m * nw > 2 * steps) return {m, nw};
-  }
-  TemporalShape best{0, 0};
-  double best_cost = 1e300;
-  for (const auto& c : cands) {
-    const double cost = swar_launch_cycles(c, steps, ch, rows, row_bytes);
-    if (cost < best_cost) {
-      best_cost = cost;
-      best = c;
-    }
-  }
-  PCONV_CHECK(best.m > 0, "swar temporal kernel: steps too large for every tile shape");
-  return best;
-}
-}  // namespace
 
 void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hipStream_t stream, KernelVariant v) {
   // Rows outside the global image stay zero: clip the output region to it.
@@ -716,12 +492,7 @@ void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hip
     PCONV_CHECK(a.steps <= kMaxFusedSteps, "temporal kernel: too many fused steps");
     PCONV_CHECK(a.height < (int64_t(1) << 30) && a.g_row0 < (int64_t(1) << 30), "temporal kernel: rows exceed 2^30");
     if (v == KernelVariant::Temporal) {
-      const TemporalShape sh = pick_swar_shape(a.steps, channel_count(ch), a.r1 - a.r0, a.row_bytes);
-      switch (ch) {
-        case Channels::Grey: launch_swar<1>(a, stream, sh); break;
-        case Channels::Rgb: launch_swar<3>(a, stream, sh); break;
-        case Channels::Rgba: launch_swar<4>(a, stream, sh); break;
-      }
+      launch_swar(a, ch, stream);
     } else {
       const TemporalShape sh = pick_temporal_shape(a.steps);
       switch (ch) {

@@ -1,0 +1,376 @@
+// Temporal-blocked gaussian, SWAR-32 form — the production fused kernel.
+//
+// What it replaces: the reference launches one kernel per repetition with one
+// thread per pixel, lanes walking down rows (uncoalesced), FP64 math
+// (cuda/cuda_convolution.cu:9-47, 66-87).  Here one launch advances `steps`
+// repetitions of a whole tile held in registers.
+//
+// Why SWAR-32: measured on gfx950 (tools/ubench/isa_rates.hip), packed
+// 16-bit VOP3P ops (v_pk_add_u16, v_pk_mad_u16, v_pk_lshrrev_b16) and
+// v_perm_b32 issue at HALF the rate of plain 32-bit VALU ops, while
+// v_add_u32 / v_add3_u32 / v_lshlrev_b32 / v_and_b32 run at full rate.  Two
+// 16-bit fields in a u32 never carry into each other here (every sum stays
+// below 4080 < 2^16), so plain 32-bit adds do the packed work at twice the
+// throughput.
+//
+// Layout: per row a lane holds LW u32 "pairs" P_k = (A_k, B_k): A_k is byte k
+// of the lane's LW-byte chunk in column strip A, B_k the same byte of strip
+// B (two strips of 64*LW bytes per wave).  The horizontal neighbour of P_k at
+// distance CH is P_{k±CH}, or — across the lane boundary — the neighbouring
+// lane's register via DPP wave_shr/wave_shl.  Per pair per step: 2 ops
+// horizontal (v_lshlrev + v_add3), 2 vertical (rolling sum), 2 truncation
+// (v_lshrrev, v_and), all full rate; the byte shuffles (v_perm) happen only
+// when a tile is loaded and stored.
+//
+// Tile: NW waves stacked vertically, wave w keeps rows [w*M, (w+1)*M); each
+// step the waves swap their boundary rows through LDS (double-buffered by step
+// parity: one s_barrier per step).  Garbage enters the tile from outside at
+// one row / CH bytes per step and is absorbed by a `steps`-row / ceil(steps*
+// CH/LW)-lane halo; rows and columns outside the image are forced to zero
+// after every step (zero-padding semantics of mpi/mpi_convolution.c:111-118).
+// Tile shape (LW, M, NW) comes from a latency model of one launch (see
+// swar_launch_cycles) — big images get the least redundant tile, small bands
+// (the 8-GPU split of a small image) get small tiles spread over all CUs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <mutex>
+
+#include "pconv/device.hpp"
+#include "swar.hpp"
+
+namespace pconv {
+namespace {
+
+using u32 = uint32_t;
+
+__device__ __forceinline__ u32 perm(u32 hi, u32 lo, u32 sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
+
+// Selector building the pair (lo.byte j, hi.byte j) zero-extended to u16x2.
+__device__ __forceinline__ constexpr u32 pair_sel(int j) {
+  return 0x0c000c00u | ((4u + static_cast<u32>(j)) << 16) | static_cast<u32>(j);
+}
+
+// Horizontal [1,2,1] at tap distance CH over NP pairs; lane-crossing taps via DPP.
+template <int CH, int NP>
+__device__ __forceinline__ void horiz(const u32 (&X)[NP], u32 (&H)[NP]) {
+  static_assert(CH <= NP, "tap distance must not exceed the pairs per lane");
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int l = k - CH, r = k + CH;
+    const u32 lv = l >= 0 ? X[l] : __builtin_amdgcn_mov_dpp(X[NP + l], 0x138, 0xf, 0xf, true);  // wave_shr:1
+    const u32 rv = r < NP ? X[r] : __builtin_amdgcn_mov_dpp(X[r - NP], 0x130, 0xf, 0xf, true);   // wave_shl:1
+    H[k] = (X[k] << 1) + (lv + rv);
+  }
+}
+
+template <int NP>
+struct Chunk;  // raw bytes of one lane's chunk in one strip
+template <>
+struct Chunk<8> {
+  using T = uint2;
+  __device__ static T zero() { return make_uint2(0, 0); }
+};
+template <>
+struct Chunk<4> {
+  using T = u32;
+  __device__ static T zero() { return 0u; }
+};
+
+template <int NP>
+__device__ __forceinline__ void unpack(const typename Chunk<NP>::T& a, const typename Chunk<NP>::T& b, u32 (&D)[NP]) {
+  if constexpr (NP == 8) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      D[k] = perm(b.x, a.x, pair_sel(k));
+      D[4 + k] = perm(b.y, a.y, pair_sel(k));
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) D[k] = perm(b, a, pair_sel(k));
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void pack(const u32 (&D)[NP], typename Chunk<NP>::T& a, typename Chunk<NP>::T& b) {
+  if constexpr (NP == 8) {
+    const u32 t0 = perm(D[1], D[0], 0x06020400u);  // A0 A1 B0 B1
+    const u32 t1 = perm(D[3], D[2], 0x06020400u);  // A2 A3 B2 B3
+    const u32 t2 = perm(D[5], D[4], 0x06020400u);
+    const u32 t3 = perm(D[7], D[6], 0x06020400u);
+    a = make_uint2(perm(t1, t0, 0x05040100u), perm(t3, t2, 0x05040100u));
+    b = make_uint2(perm(t1, t0, 0x07060302u), perm(t3, t2, 0x07060302u));
+  } else {
+    const u32 t0 = perm(D[1], D[0], 0x06020400u);
+    const u32 t1 = perm(D[3], D[2], 0x06020400u);
+    a = perm(t1, t0, 0x05040100u);
+    b = perm(t1, t0, 0x07060302u);
+  }
+}
+
+template <int CH, int LW, int M, int NW>
+__global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                  int64_t pitch, int row_bytes, int r0, int r1, int steps, int g_row0,
+                                                  int height, int nstrips, int pair_stride) {
+  constexpr int NP = LW;       // pairs per row per lane
+  constexpr int NQ = NP / 4;   // uint4 per row per lane
+  using CT = typename Chunk<NP>::T;
+  __shared__ uint4 lds[2][NW][2][NQ][64];  // [parity][wave][top/bottom][quad][lane]
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hl = (steps * CH + LW - 1) / LW;  // halo lanes per side
+  const int vbytes = (64 - 2 * hl) * LW;      // valid output bytes per strip
+  const int sA = blockIdx.x, sB = blockIdx.x + pair_stride;
+  const bool hasB = sB < nstrips;
+  const int baseA = sA * vbytes - hl * LW, baseB = sB * vbytes - hl * LW;
+  const int xA = baseA + lane * LW, xB = baseB + lane * LW;
+  const int validA = (xA >= 0) ? min(max(row_bytes - xA, 0), LW) : 0;
+  const int validB = (hasB && xB >= 0) ? min(max(row_bytes - xB, 0), LW) : 0;
+  const bool needs_mask = baseA < 0 || baseA + 64 * LW > row_bytes || !hasB || baseB + 64 * LW > row_bytes;
+  u32 cm[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) cm[k] = (k < validA ? 0xffffu : 0u) | (k < validB ? 0xffff0000u : 0u);
+
+  const int vrows = NW * M - 2 * steps;
+  const int tile_r0 = r0 + static_cast<int>(blockIdx.y) * vrows;
+  const int row_base = tile_r0 - steps + w * M;
+  const int lo_ok = max(r0 - steps, -g_row0), hi_ok = min(r1 + steps, height - g_row0);
+
+  u32 D[M][NP];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const int fr = row_base + i;
+    const bool rok = fr >= lo_ok && fr < hi_ok;
+    CT a = Chunk<NP>::zero(), b = Chunk<NP>::zero();
+    const uint8_t* rowp = src + static_cast<int64_t>(fr) * pitch;
+    if (rok && validA > 0) a = *reinterpret_cast<const CT*>(rowp + xA);
+    if (rok && validB > 0) b = *reinterpret_cast<const CT*>(rowp + xB);
+    unpack<NP>(a, b, D[i]);
+  }
+  const int out_top = min(max(-g_row0 - row_base, 0), M);
+  const int out_bot = min(max(height - g_row0 - row_base, 0), M);
+
+  for (int s = 0; s < steps; ++s) {
+    const int par = s & 1;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      lds[par][w][0][q][lane] = make_uint4(D[0][4 * q], D[0][4 * q + 1], D[0][4 * q + 2], D[0][4 * q + 3]);
+      lds[par][w][1][q][lane] =
+          make_uint4(D[M - 1][4 * q], D[M - 1][4 * q + 1], D[M - 1][4 * q + 2], D[M - 1][4 * q + 3]);
+    }
+    __syncthreads();
+    u32 A[NP], B[NP];
+    {
+      const int wa = w > 0 ? w - 1 : 0;        // wave 0: tile top halo, value irrelevant
+      const int wb = w < NW - 1 ? w + 1 : w;   // last wave: tile bottom halo
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const uint4 av = lds[par][wa][1][q][lane], bv = lds[par][wb][0][q][lane];
+        A[4 * q] = av.x; A[4 * q + 1] = av.y; A[4 * q + 2] = av.z; A[4 * q + 3] = av.w;
+        B[4 * q] = bv.x; B[4 * q + 1] = bv.y; B[4 * q + 2] = bv.z; B[4 * q + 3] = bv.w;
+      }
+    }
+    u32 Hc[NP], Sc[NP];
+    {
+      u32 Ha[NP];
+      horiz<CH, NP>(A, Ha);
+      horiz<CH, NP>(D[0], Hc);
+#pragma unroll
+      for (int k = 0; k < NP; ++k) Sc[k] = Ha[k] + Hc[k];
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      u32 Hn[NP];
+      if (i + 1 < M)
+        horiz<CH, NP>(D[i + 1], Hn);
+      else
+        horiz<CH, NP>(B, Hn);
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const u32 Sn = Hc[k] + Hn[k];
+        D[i][k] = ((Sc[k] + Sn) >> 4) & 0x00ff00ffu;  // floor(sum/16) in both 16-bit fields
+        Sc[k] = Sn;
+        Hc[k] = Hn[k];
+      }
+    }
+    if (needs_mask) {
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int k = 0; k < NP; ++k) D[i][k] &= cm[k];
+    }
+    if (out_top > 0 || out_bot < M) {
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+        if (i < out_top || i >= out_bot)
+#pragma unroll
+          for (int k = 0; k < NP; ++k) D[i][k] = 0;
+    }
+  }
+
+  const bool lane_in = lane >= hl && lane < 64 - hl;
+  const bool stA = lane_in && validA > 0, stB = lane_in && validB > 0;
+  const int st_lo = max(tile_r0, r0), st_hi = min(min(tile_r0 + vrows, r1), height - g_row0);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const int fr = row_base + i;
+    if (fr >= st_lo && fr < st_hi) {
+      CT a, b;
+      pack<NP>(D[i], a, b);
+      uint8_t* rowq = dst + static_cast<int64_t>(fr) * pitch;
+      if (stA) *reinterpret_cast<CT*>(rowq + xA) = a;
+      if (stB) *reinterpret_cast<CT*>(rowq + xB) = b;
+    }
+  }
+}
+
+// Instantiated tile shapes (LW, M, NW).
+constexpr SwarShape kShapes[] = {
+    {8, 8, 8}, {8, 8, 4}, {8, 16, 4}, {8, 4, 8},              // 8-byte lanes: large images
+    {4, 8, 8}, {4, 6, 8}, {4, 5, 8}, {4, 4, 8}, {4, 3, 8}, {4, 4, 16},  // 4-byte lanes: small bands
+};
+
+template <int CH, int LW, int M, int NW>
+void launch_one(const StencilLaunch& a, hipStream_t s) {
+  const int steps = a.steps;
+  const int hl = (steps * CH + LW - 1) / LW;
+  const int vbytes = (64 - 2 * hl) * LW;
+  const int vrows = M * NW - 2 * steps;
+  PCONV_CHECK(vbytes > 0 && vrows > 0, "swar temporal kernel: steps too large for the tile");
+  const int nstrips = static_cast<int>(ceil_div<int64_t>(a.row_bytes, vbytes));
+  const int pair_stride = (nstrips + 1) / 2;
+  const dim3 grid(pair_stride, ceil_div(static_cast<int>(a.r1 - a.r0), vrows));
+  const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
+  k_swar<CH, LW, M, NW><<<grid, dim3(64 * NW), 0, s>>>(a.src, a.dst, a.pitch, static_cast<int>(a.row_bytes),
+                                                       static_cast<int>(a.r0), static_cast<int>(a.r1), steps,
+                                                       static_cast<int>(a.g_row0), static_cast<int>(hmax), nstrips,
+                                                       pair_stride);
+}
+
+template <int CH>
+void launch_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh) {
+#define PCONV_SWAR(LW_, M_, NW_)                            \
+  if (sh.lw == LW_ && sh.m == M_ && sh.nw == NW_) {         \
+    launch_one<CH, LW_, M_, NW_>(a, s);                     \
+    return;                                                 \
+  }
+  PCONV_SWAR(8, 8, 8)
+  PCONV_SWAR(8, 8, 4)
+  PCONV_SWAR(8, 16, 4)
+  PCONV_SWAR(8, 4, 8)
+  PCONV_SWAR(4, 8, 8)
+  PCONV_SWAR(4, 6, 8)
+  PCONV_SWAR(4, 5, 8)
+  PCONV_SWAR(4, 4, 8)
+  PCONV_SWAR(4, 3, 8)
+  PCONV_SWAR(4, 4, 16)
+#undef PCONV_SWAR
+  PCONV_FAIL("swar temporal kernel: unsupported tile shape");
+}
+
+bool known_shape(const SwarShape& s) {
+  for (const auto& k : kShapes)
+    if (k.lw == s.lw && k.m == s.m && k.nw == s.nw) return true;
+  return false;
+}
+
+// Shape override (tuning / tests): set_swar_shape(), initialised once from
+// PCONV_SWAR_SHAPE="lw,m,nw".
+std::mutex g_shape_mu;
+bool g_shape_init = false;
+bool g_have_shape = false;
+SwarShape g_shape;
+
+bool override_shape(SwarShape& out) {
+  std::lock_guard<std::mutex> lk(g_shape_mu);
+  if (!g_shape_init) {
+    g_shape_init = true;
+    if (const char* e = std::getenv("PCONV_SWAR_SHAPE")) {
+      SwarShape s;
+      if (std::sscanf(e, "%d,%d,%d", &s.lw, &s.m, &s.nw) == 3 && known_shape(s)) {
+        g_shape = s;
+        g_have_shape = true;
+      }
+    }
+  }
+  if (g_have_shape) out = g_shape;
+  return g_have_shape;
+}
+
+}  // namespace
+
+void set_swar_shape(int lw, int m, int nw) {
+  std::lock_guard<std::mutex> lk(g_shape_mu);
+  g_shape_init = true;
+  if (lw == 0) {
+    g_have_shape = false;
+    return;
+  }
+  const SwarShape s{lw, m, nw};
+  PCONV_CHECK(known_shape(s), "set_swar_shape: shape not instantiated");
+  g_shape = s;
+  g_have_shape = true;
+}
+
+std::vector<SwarShape> swar_shapes() { return std::vector<SwarShape>(std::begin(kShapes), std::end(kShapes)); }
+
+// Latency model of one launch on 256 CUs x 4 SIMDs (cycles).  Inputs measured
+// on gfx950: a SIMD retires one VALU wave-instruction per ~5.8 cycles with
+// one resident wave, ~2.9 with two, ~2.8 with three or more
+// (tools/ubench/isa_rates.hip); workgroups per CU are bounded by LDS (NW x
+// LW KiB of boundary-row buffers), VGPRs (by M and LW) and 32 waves per CU;
+// the CU that receives the most workgroups sets the launch time; ~5.5k cycles
+// of load / store latency per tile.
+double swar_launch_cycles(SwarShape s, int steps, int ch, int64_t rows, int64_t row_bytes) {
+  const int np = s.lw;
+  const int hl = (steps * ch + s.lw - 1) / s.lw;
+  if (2 * hl >= 64) return 1e300;
+  const int64_t vbytes = (64 - 2 * hl) * s.lw;
+  const int64_t pairs = (ceil_div<int64_t>(row_bytes, vbytes) + 1) / 2;
+  const int vrows = s.m * s.nw - 2 * steps;
+  if (vrows <= 0 || np < ch) return 1e300;
+  const double g = static_cast<double>(pairs * ceil_div<int64_t>(rows, vrows));
+  const double stage = (s.m + 2) * (2.0 * np + 2.0 * ch) + s.m * 4.0 * np + 24.0;
+  const double wave_instr = steps * stage + 40.0 + 3.0 * s.m * np;
+  const int vgpr = round_up(s.m * np + 3 * np + 40, 8);
+  const int vgpr_waves = std::min(8, 512 / vgpr);
+  const int lds_wgs = (160 * 1024) / (s.nw * np * 1024);
+  const int L = std::max(1, std::min({lds_wgs, vgpr_waves * 4 / s.nw, 32 / s.nw}));
+  const double per_cu = std::ceil(g / 256.0);
+  const double rounds = std::ceil(per_cu / L);
+  const double conc = std::min<double>(per_cu, L);
+  const double wps = conc * s.nw / 4.0;
+  const double rate = wps >= 3 ? 2.8 : wps >= 2 ? 2.9 : 5.8;
+  return rounds * (std::max(1.0, std::ceil(wps)) * wave_instr * rate + 5500.0);
+}
+
+SwarShape pick_swar_shape(int steps, int ch, int64_t rows, int64_t row_bytes) {
+  SwarShape best{0, 0, 0};
+  if (override_shape(best) && best.m * best.nw > 2 * steps && best.lw >= ch &&
+      2 * ((steps * ch + best.lw - 1) / best.lw) < 64)
+    return best;
+  double best_cost = 1e300;
+  for (const auto& c : kShapes) {
+    const double cost = swar_launch_cycles(c, steps, ch, rows, row_bytes);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  PCONV_CHECK(best.m > 0, "swar temporal kernel: steps too large for every tile shape");
+  return best;
+}
+
+void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream) {
+  const SwarShape sh = pick_swar_shape(a.steps, channel_count(ch), a.r1 - a.r0, a.row_bytes);
+  switch (ch) {
+    case Channels::Grey: launch_ch<1>(a, stream, sh); break;
+    case Channels::Rgb: launch_ch<3>(a, stream, sh); break;
+    case Channels::Rgba: launch_ch<4>(a, stream, sh); break;
+  }
+}
+
+}  // namespace pconv

@@ -1,0 +1,30 @@
+// Internal interface of the SWAR-32 temporal kernel (kernels/stencil_swar.hip).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <vector>
+
+#include "pconv/kernels.hpp"
+
+namespace pconv {
+
+// Tile of the SWAR kernel: lw bytes per lane per strip (4 or 8), m rows per
+// wave, nw waves stacked vertically per workgroup.
+struct SwarShape {
+  int lw = 8, m = 8, nw = 8;
+};
+
+// Latency model of one launch (cycles) and the shape it picks.
+double swar_launch_cycles(SwarShape s, int steps, int ch, int64_t rows, int64_t row_bytes);
+SwarShape pick_swar_shape(int steps, int ch, int64_t rows, int64_t row_bytes);
+
+// Enqueue the fused gaussian for `a.steps` repetitions (shape from the model
+// or from PCONV_SWAR_SHAPE="lw,m,nw").
+void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
+
+// Force a tile shape (lw = 0 restores the model) and list the instantiated ones.
+void set_swar_shape(int lw, int m, int nw);
+std::vector<SwarShape> swar_shapes();
+
+}  // namespace pconv

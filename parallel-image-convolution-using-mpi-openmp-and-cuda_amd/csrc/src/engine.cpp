@@ -2,6 +2,7 @@
 #include "pconv/engine.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <thread>
 
 namespace pconv {
@@ -175,7 +176,7 @@ void BandEngine::run(int reps) {
   stats_.exchanges = pre_exchanges_;
   pre_exchanges_ = 0;
   wall_t0_ = wall_seconds();
-  ev_t0_.record(cs_);
+  if (opt_.timing) ev_t0_.record(cs_);
   const bool graph = opt_.use_graph && !transport_ && !ph.empty();
   if (graph) {
     const auto key = std::make_pair(reps, cur_);
@@ -201,8 +202,10 @@ void BandEngine::run(int reps) {
   } else {
     for (const auto& p : ph) enqueue_phase(p);
   }
-  ev_t1_.record(cs_);
-  timing_pending_ = true;
+  if (opt_.timing) {
+    ev_t1_.record(cs_);
+    timing_pending_ = true;
+  }
   halo_valid_ = false;
 }
 
@@ -231,23 +234,33 @@ void BandEngine::synchronize() {
 // --------------------------------------------------------------- BandPipeline
 
 BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt,
-                           int slots) {
+                           int slots, int concurrent) {
   PCONV_CHECK(slots >= 1 && slots <= 8, "pipeline slots must be in [1, 8]");
   set_device(opt.device);
-  // Four streams in all (= the default number of hardware queues): compute
-  // (shared by every slot: one GPU runs one image's reps at a time), H2D,
-  // D2H and — only with neighbours — communication.
-  compute_ = Stream::create(0);
+  // Streams: H2D, D2H, communication (only with neighbours) and compute.
+  // HIP maps streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by
+  // default); two busy streams on one queue serialise falsely.  When the
+  // queue budget allows, every slot gets its own compute stream so that
+  // consecutive images run their repetitions CONCURRENTLY — a small band (the
+  // 8-GPU split of a small image) fills only part of the chip per launch, two
+  // images in flight fill it.  Otherwise all slots share one compute stream.
+  const bool nb = band.up >= 0 || band.down >= 0;
+  int hw_queues = 4;
+  if (const char* q = std::getenv("GPU_MAX_HW_QUEUES")) hw_queues = std::max(1, std::atoi(q));
+  const int fixed = 2 + (nb ? 1 : 0);
+  concurrent_ = concurrent < 0 ? (slots > 1 && hw_queues >= fixed + slots) : (concurrent > 0 && slots > 1);
   h2d_ = Stream::create(0);
   d2h_ = Stream::create(0);
   EngineOptions o = opt;
   o.use_graph = false;  // copies/events interleave with the loop
-  o.compute_stream = compute_.get();
-  if (band.up >= 0 || band.down >= 0) {
+  o.timing = false;     // host time per image matters here (see tools/ubench/api_cost.hip)
+  if (nb) {
     comm_ = Stream::create(-1);
     o.comm_stream = comm_.get();
   }
+  for (int i = 0; i < (concurrent_ ? slots : 1); ++i) computes_.push_back(Stream::create(0));
   for (int i = 0; i < slots; ++i) {
+    o.compute_stream = computes_[concurrent_ ? i : 0].get();
     slots_.push_back(std::make_unique<BandEngine>(geom, band, filter, o));
     ev_up_.push_back(Event::create());
     ev_done_.push_back(Event::create());
@@ -259,7 +272,7 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
 
 BandPipeline::~BandPipeline() {
   (void)hipStreamSynchronize(h2d_.get());
-  (void)hipStreamSynchronize(compute_.get());
+  for (auto& c : computes_) (void)hipStreamSynchronize(c.get());
   (void)hipStreamSynchronize(d2h_.get());
   if (comm_.get()) (void)hipStreamSynchronize(comm_.get());
 }

@@ -17,6 +17,7 @@
 #include "pconv/raw_io.hpp"
 #include "pconv/rccl_comm.hpp"
 #include "pconv/schedule.hpp"
+#include "../kernels/swar.hpp"
 
 namespace py = pybind11;
 using namespace pconv;
@@ -303,6 +304,21 @@ PYBIND11_MODULE(_pconv_native, m) {
       py::arg("r0"), py::arg("r1"), py::arg("frame_lo"), py::arg("frame_hi"), py::arg("steps") = 1,
       py::arg("g_row0") = 0, py::arg("height") = (int64_t(1) << 40), py::arg("stream") = 0,
       py::arg("variant") = "auto");
+  m.def("set_swar_shape", &set_swar_shape, py::arg("lw") = 0, py::arg("m") = 0, py::arg("nw") = 0,
+        "Force the SWAR temporal tile shape (lw=0: back to the latency model).");
+  m.def("swar_shapes", []() {
+    py::list out;
+    for (const auto& s : swar_shapes()) out.append(py::make_tuple(s.lw, s.m, s.nw));
+    return out;
+  });
+  m.def(
+      "swar_model",
+      [](int steps, const std::string& ch, int64_t rows, int64_t row_bytes) {
+        const SwarShape s = pick_swar_shape(steps, channel_count(parse_channels(ch)), rows, row_bytes);
+        return py::make_tuple(py::make_tuple(s.lw, s.m, s.nw),
+                              swar_launch_cycles(s, steps, channel_count(parse_channels(ch)), rows, row_bytes));
+      },
+      py::arg("steps"), py::arg("channels"), py::arg("rows"), py::arg("row_bytes"));
   m.def("supports_fusion",
         [](py::object filter, const std::string& v) { return supports_fusion(make_filter(filter), parse_variant(v)); },
         py::arg("filter"), py::arg("variant") = "auto");
@@ -425,7 +441,8 @@ PYBIND11_MODULE(_pconv_native, m) {
 
   py::class_<BandPipeline>(m, "BandPipeline")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
-                       int device, int halo, int fuse, bool overlap, const std::string& variant, int slots) {
+                       int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
+                       int concurrent) {
              EngineOptions o;
              o.device = device;
              o.halo_depth = halo;
@@ -433,11 +450,12 @@ PYBIND11_MODULE(_pconv_native, m) {
              o.overlap = overlap;
              o.variant = parse_variant(variant);
              const ImageGeom g = make_geom(w, h, ch);
-             return std::make_unique<BandPipeline>(g, row_band(h, world, rank), make_filter(filter), o, slots);
+             return std::make_unique<BandPipeline>(g, row_band(h, world, rank), make_filter(filter), o, slots,
+                                                   concurrent);
            }),
            py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
            py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
-           py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2)
+           py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -454,7 +472,8 @@ PYBIND11_MODULE(_pconv_native, m) {
           },
           py::arg("in_ptr"), py::arg("in_r0"), py::arg("in_r1"), py::arg("out_ptr"), py::arg("reps"))
       .def("drain", &BandPipeline::drain, py::call_guard<py::gil_scoped_release>())
-      .def_property_readonly("submitted", &BandPipeline::submitted);
+      .def_property_readonly("submitted", &BandPipeline::submitted)
+      .def_property_readonly("concurrent", &BandPipeline::concurrent);
 
   py::class_<LocalCluster>(m, "LocalCluster")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int bands, int device, int halo,

@@ -41,7 +41,7 @@ class DistributedBlur:
                  reps: Optional[int] = None, *, rank: Optional[int] = None, world: Optional[int] = None,
                  device: Optional[int] = None, halo: Optional[int] = None, fuse: Optional[int] = None,
                  overlap: bool = True, preload_halo: bool = False, comm=None, slots: int = 2,
-                 variant: str = "auto", graph: bool = False, transport: str = "rccl"):
+                 variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -55,7 +55,7 @@ class DistributedBlur:
             halo = auto_halo(self.height, self.world, reps, fuse)
         self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
                                    halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant,
-                                   slots=int(slots))
+                                   slots=int(slots), concurrent=int(concurrent))
         self.engine = self.pipe.slot(0)
         self.band = self.engine.band
         self.row_bytes = self.engine.row_bytes

@@ -168,3 +168,22 @@ def test_temporal_equals_repeated_single_steps(pconv_mod, rng):
     for t in (2, 6, 13):
         got = _run_kernel(pconv_mod.native, img, "gaussian", "temporal", steps=t)
         assert np.array_equal(got, pconv_mod.numpy_convolve(img, t)), t
+
+
+def test_every_swar_shape_bit_exact(native, rng):
+    """Force each instantiated SWAR tile shape (lane width, rows/wave, waves)
+    and compare a fused launch with the CPU fused-launch reference."""
+    try:
+        for (lw, m, nw) in native.swar_shapes():
+            native.set_swar_shape(lw, m, nw)
+            for channels, steps in (("grey", 3), ("rgb", 4), ("rgba", 2), ("rgb", 8)):
+                if m * nw <= 2 * steps or lw < CH[channels]:
+                    continue
+                c = CH[channels]
+                img = rng.integers(0, 256, size=(71, 301, c) if c > 1 else (71, 301), dtype=np.uint8)
+                gpu, cpu = _run_fused(native, img, steps, 0, 71, steps, 0, 71, variant="temporal")
+                assert np.array_equal(gpu, cpu), (lw, m, nw, channels, steps)
+                gpu, cpu = _run_fused(native, img[:40], steps, -5, 45, 16, 30, 200, variant="temporal")
+                assert np.array_equal(gpu[11:61], cpu[11:61]), (lw, m, nw, channels, steps, "band")
+    finally:
+        native.set_swar_shape(0, 0, 0)

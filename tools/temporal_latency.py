@@ -26,13 +26,13 @@ def main():
     dst = torch.zeros_like(src)
     base = lay["pitch"] * halo + 16
     s = torch.cuda.current_stream()
-    shapes = sys.argv[1].split(";") if len(sys.argv) > 1 else ["4,8", "8,8", "2,16", "8,4"]
+    shapes = sys.argv[1].split(";") if len(sys.argv) > 1 else ["4,5,8", "4,4,8", "8,8,8", "4,8,8"]
     for shape in shapes:
-        os.environ["PCONV_SWAR_SHAPE"] = shape
-        for rows in (16, 400, 2520):
+        n.set_swar_shape(*map(int, shape.split(",")))
+        for rows in (16, 100, 400, 2520):
             res = []
             for steps in (1, 2, 4, 8, 16):
-                m, nw = map(int, shape.split(","))
+                _, m, nw = map(int, shape.split(","))
                 if m * nw <= 2 * steps:
                     continue
                 times = []
