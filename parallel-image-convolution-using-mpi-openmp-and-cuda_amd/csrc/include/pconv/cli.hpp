@@ -45,6 +45,8 @@ struct CliConfig {
   bool explain = false;
   double timeout_s = 600.0;
   bool quiet = false;
+  std::string transport = "rccl";  // multi-GPU halo transport: rccl | shm (host-staged, shared memory)
+  bool preload_halo = true;        // ranks read their ghost rows from the input (no exchange at start)
 };
 
 // Parse argv.  Throws pconv::Error with the message to print on bad input.

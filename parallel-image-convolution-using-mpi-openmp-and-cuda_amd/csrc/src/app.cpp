@@ -176,13 +176,54 @@ void shm_barrier(SharedState* s, int world, double timeout_s) {
   }
 }
 
-void run_rank(const CliConfig& c, SharedState* sh, int rank) {
+// Host-staged halo transport through the launcher's shared memory (the
+// shared-memory path of an MPI library): each rank stages its boundary rows
+// into its own slots, all ranks meet at a barrier, each copies its
+// neighbours' slots into its ghost rows, and a second barrier frees the slots.
+// Synchronous; needs no RCCL, so several ranks may share one GPU.
+class ShmTransport : public HaloTransport {
+ public:
+  ShmTransport(SharedState* sh, uint8_t* slots, int64_t slot_bytes, int rank, int world, double timeout_s)
+      : sh_(sh), slots_(slots), slot_bytes_(slot_bytes), rank_(rank), world_(world), timeout_s_(timeout_s) {}
+
+  void exchange(BandEngine& e, int64_t depth, hipStream_t stream) override {
+    const Band& b = e.band();
+    const int64_t pitch = e.layout().pitch;
+    const int64_t n = depth * pitch;
+    PCONV_CHECK(n <= slot_bytes_, "shm halo: slot too small");
+    uint8_t* row0 = e.src_frame() - kPadLeft;
+    if (b.up >= 0) PCONV_HIP_CHECK(hipMemcpyAsync(slot(rank_, 0), row0, n, hipMemcpyDeviceToHost, stream));
+    if (b.down >= 0)
+      PCONV_HIP_CHECK(hipMemcpyAsync(slot(rank_, 1), row0 + (b.rows - depth) * pitch, n, hipMemcpyDeviceToHost, stream));
+    PCONV_HIP_CHECK(hipStreamSynchronize(stream));
+    shm_barrier(sh_, world_, timeout_s_);
+    if (b.up >= 0) PCONV_HIP_CHECK(hipMemcpyAsync(row0 - n, slot(b.up, 1), n, hipMemcpyHostToDevice, stream));
+    if (b.down >= 0)
+      PCONV_HIP_CHECK(hipMemcpyAsync(row0 + b.rows * pitch, slot(b.down, 0), n, hipMemcpyHostToDevice, stream));
+    PCONV_HIP_CHECK(hipStreamSynchronize(stream));
+    shm_barrier(sh_, world_, timeout_s_);
+  }
+  const char* name() const override { return "shm"; }
+
+ private:
+  uint8_t* slot(int r, int which) const { return slots_ + (static_cast<int64_t>(r) * 2 + which) * slot_bytes_; }
+  SharedState* sh_;
+  uint8_t* slots_;
+  int64_t slot_bytes_;
+  int rank_, world_;
+  double timeout_s_;
+};
+
+void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t slot_bytes, int rank) {
   set_error_rank(rank);
   const ImageGeom g = geom_of(c);
   const int world = c.gpus;
   const int ndev = device_count();
-  PCONV_CHECK(ndev >= world, "need " + std::to_string(world) + " GPUs, " + std::to_string(ndev) + " visible");
-  const int device = rank;
+  const bool shm = c.transport == "shm";
+  // RCCL needs one GPU per rank; the shared-memory transport may oversubscribe.
+  PCONV_CHECK(shm || ndev >= world,
+              "need " + std::to_string(world) + " GPUs, " + std::to_string(ndev) + " visible (try --transport shm)");
+  const int device = rank % ndev;
   set_device(device);
   const Filter f = Filter::by_name(c.filter);
   const Band b = row_band(g.height, world, rank);
@@ -190,37 +231,45 @@ void run_rank(const CliConfig& c, SharedState* sh, int rank) {
   BandEngine eng(g, b, f, o);
   if (c.explain && rank == 0) std::fprintf(stderr, "%s", describe_plan(eng.plan(c.reps)).c_str());
   const int64_t d = eng.layout().halo;
-  // Ghost rows come straight from the file (free here): first phase needs no exchange.
-  const int64_t above = std::min<int64_t>(d, b.y0);
-  const int64_t below = std::min<int64_t>(d, g.height - (b.y0 + b.rows));
+  // Ghost rows straight from the file (free here) unless --exchange-halo:
+  // then the first phase exchanges them like every later one.
+  const int64_t above = c.preload_halo ? std::min<int64_t>(d, b.y0) : 0;
+  const int64_t below = c.preload_halo ? std::min<int64_t>(d, g.height - (b.y0 + b.rows)) : 0;
   const int64_t rb = g.row_bytes();
   PinnedBuffer host(static_cast<size_t>((b.rows + above + below) * rb));
   load_rows(c, g, b.y0 - above, b.rows + above + below, host.data(), rb);
 
-  if (rank == 0) {
-    const auto id = rccl_unique_id();
-    std::memcpy(sh->id, id.data(), kUniqueIdBytes);
-    sh->id_ready.store(1);
+  std::shared_ptr<RcclComm> comm;
+  if (shm) {
+    eng.set_transport(std::make_shared<ShmTransport>(sh, halo_slots, slot_bytes, rank, world, c.timeout_s));
   } else {
-    const double t0 = wall_seconds();
-    while (!sh->id_ready.load()) {
-      if (sh->failed.load()) PCONV_FAIL("peer rank failed");
-      if (wall_seconds() - t0 > c.timeout_s) PCONV_FAIL("timed out waiting for the RCCL unique id");
-      std::this_thread::yield();
+    if (rank == 0) {
+      const auto id = rccl_unique_id();
+      std::memcpy(sh->id, id.data(), kUniqueIdBytes);
+      sh->id_ready.store(1);
+    } else {
+      const double t0 = wall_seconds();
+      while (!sh->id_ready.load()) {
+        if (sh->failed.load()) PCONV_FAIL("peer rank failed");
+        if (wall_seconds() - t0 > c.timeout_s) PCONV_FAIL("timed out waiting for the RCCL unique id");
+        std::this_thread::yield();
+      }
     }
+    std::vector<uint8_t> id(sh->id, sh->id + kUniqueIdBytes);
+    comm = std::make_shared<RcclComm>(id, rank, world, device);
+    eng.set_transport(std::make_shared<RcclTransport>(comm));
   }
-  std::vector<uint8_t> id(sh->id, sh->id + kUniqueIdBytes);
-  auto comm = std::make_shared<RcclComm>(id, rank, world, device);
-  eng.set_transport(std::make_shared<RcclTransport>(comm));
 
   eng.upload_rows(host.data(), rb, -above, b.rows + below);
-  eng.set_halo_valid(true);
+  eng.set_halo_valid(c.preload_halo);
   eng.synchronize();
   shm_barrier(sh, world, c.timeout_s);  // MPI_Barrier before the timer (mpi_convolution.c:151)
   const double l0 = wall_seconds();
   eng.run(c.reps);
-  comm->wait(eng.compute_stream(), c.timeout_s);
-  comm->wait(eng.comm_stream(), c.timeout_s);
+  if (comm) {
+    comm->wait(eng.compute_stream(), c.timeout_s);
+    comm->wait(eng.comm_stream(), c.timeout_s);
+  }
   eng.synchronize();
   sh->loop_s[rank] = wall_seconds() - l0;
   sh->launches[rank] = eng.last_stats().launches;
@@ -245,6 +294,17 @@ AppReport run_multi(const CliConfig& c) {
   sh->arrived = 0;
   sh->generation = 0;
   sh->failed = 0;
+  // Halo staging slots for --transport shm: [rank][top|bottom][depth * pitch].
+  uint8_t* slots = nullptr;
+  int64_t slot_bytes = 0, slots_total = 0;
+  if (c.transport == "shm") {
+    const EngineOptions o = engine_options(c, g, c.gpus, 0);
+    slot_bytes = static_cast<int64_t>(o.halo_depth) * FrameLayout::make(g.row_bytes(), 1, o.halo_depth).pitch;
+    slots_total = slot_bytes * 2 * c.gpus;
+    void* sm = mmap(nullptr, static_cast<size_t>(slots_total), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+    PCONV_CHECK(sm != MAP_FAILED, "mmap halo slots failed");
+    slots = static_cast<uint8_t*>(sm);
+  }
   std::fflush(stdout);
   std::fflush(stderr);
   std::vector<pid_t> kids;
@@ -254,7 +314,7 @@ AppReport run_multi(const CliConfig& c) {
     if (pid == 0) {
       int code = 0;
       try {
-        run_rank(c, sh, r);
+        run_rank(c, sh, slots, slot_bytes, r);
       } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());
         if (!sh->failed.exchange(1)) std::snprintf(sh->error, sizeof(sh->error), "%s", e.what());
@@ -272,6 +332,7 @@ AppReport run_multi(const CliConfig& c) {
     waitpid(p, &st, 0);
     ok = ok && WIFEXITED(st) && WEXITSTATUS(st) == 0;
   }
+  if (slots) munmap(slots, static_cast<size_t>(slots_total));
   AppReport r;
   r.gpus = c.gpus;
   r.output = out_path(c);

@@ -48,6 +48,9 @@ std::string help_text(const std::string& prog) {
          "  --checkpoint-every K      write <out>.rep<N> every K repetitions\n"
          "  --explain                 print the halo/launch schedule\n"
          "  --timeout S               RCCL watchdog timeout in seconds (default 600)\n"
+         "  --transport {rccl,shm}    multi-GPU halo transport (shm: host-staged through shared memory;\n"
+         "                            lets several ranks share one GPU)\n"
+         "  --exchange-halo           ranks load only their own rows; ghost rows come from neighbours\n"
          "  --quiet                   suppress the timing lines\n";
 }
 
@@ -123,6 +126,12 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       c.timeout_s = static_cast<double>(parse_int(next("--timeout"), "--timeout", 1, 86400));
     } else if (a == "--quiet") {
       c.quiet = true;
+    } else if (a == "--transport") {
+      c.transport = next("--transport");
+      if (c.transport != "rccl" && c.transport != "shm")
+        PCONV_FAIL("invalid --transport '" + c.transport + "' (rccl|shm)");
+    } else if (a == "--exchange-halo") {
+      c.preload_halo = false;
     } else {
       PCONV_FAIL("unknown option '" + a + "'");
     }

@@ -92,3 +92,25 @@ def test_cli_hip(pconv_mod, tmp_path, rng):
         assert meta["mismatches"] == 0
         out = pconv_mod.read_raw(str(tmp_path / "blur_img.raw"), 61, 77, "rgb")
         assert np.array_equal(out, pconv_mod.numpy_convolve(img, 11))
+
+
+@pytest.mark.parametrize("extra", [
+    ["--gpus", "2"],
+    ["--gpus", "3", "--exchange-halo"],
+    ["--gpus", "4", "--halo", "2", "--fuse", "2"],
+    ["--gpus", "2", "--filter", "box"],
+    ["--gpus", "3", "--no-overlap", "--exchange-halo", "--filter", "edge"],
+])
+def test_cli_multi_rank_shm(pconv_mod, tmp_path, rng, extra):
+    """Native fork launcher, several ranks on one GPU, host-staged shm halos."""
+    img = rng.integers(0, 256, size=(77, 61, 3), dtype=np.uint8)
+    pconv_mod.write_raw(str(tmp_path / "img.raw"), img)
+    r = subprocess.run([CONV_BIN, "img.raw", "61", "77", "13", "rgb", "--transport", "shm", "--check", "--json"]
+                       + extra, cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    meta = json.loads(r.stdout.strip().splitlines()[-1])
+    assert meta["mismatches"] == 0
+    assert meta["gpus"] == int(extra[1])
+    filt = extra[extra.index("--filter") + 1] if "--filter" in extra else "gaussian"
+    out = pconv_mod.read_raw(str(tmp_path / "blur_img.raw"), 61, 77, "rgb")
+    assert np.array_equal(out, pconv_mod.numpy_convolve(img, 13, filt))
