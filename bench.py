@@ -53,7 +53,32 @@ def parse():
     p.add_argument("--slots", type=int, default=3, help="images in flight (H2D/compute/D2H overlap)")
     p.add_argument("--concurrent", choices=["auto", "on", "off"], default="off",
                    help="one compute stream per image in flight (default: one shared compute stream)")
+    p.add_argument("--transport", choices=["rccl", "gloo-host"], default="rccl",
+                   help="halo transport (gloo-host: host-staged, lets several ranks share one GPU for rehearsals)")
+    p.add_argument("--check", action="store_true",
+                   help="after timing, verify every rank's band against the CPU oracle (not timed)")
     return p.parse_args()
+
+
+def check_bands(blur, a) -> int:
+    """Compare the newest image of every rank with the native OpenMP oracle on
+    the whole synthetic image; returns the total mismatching bytes (all ranks)."""
+    import numpy as np
+
+    from pconv import native
+    from pconv.models.filters import get_filter
+    from pconv.parallel.bootstrap import sum_over_ranks
+
+    n = native()
+    full = np.empty(a.width * a.height * {"grey": 1, "rgb": 3, "rgba": 4}[a.channels], np.uint8)
+    n.synth_rows(full, a.width, a.height, a.channels, int(a.seed), 0, a.height)
+    ref = np.empty_like(full)
+    n.cpu_convolve(full, ref, a.width, a.height, a.channels, a.reps, get_filter(a.filter).to_native(), True, 0)
+    ref = ref.reshape(a.height, -1)
+    b = blur.band
+    out = blur.step(a.reps)
+    bad = int(np.count_nonzero(out != ref[b.y0:b.y0 + b.rows]))
+    return int(sum_over_ranks(bad))
 
 
 def main():
@@ -74,12 +99,13 @@ def main():
     world = ctx.world
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(ctx.local_rank)
+    device = ctx.local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
 
     blur = DistributedBlur(a.width, a.height, a.channels, a.filter, a.reps, rank=ctx.rank, world=world,
-                           device=ctx.local_rank, halo=a.halo, fuse=a.fuse, overlap=not a.no_overlap,
+                           device=device, halo=a.halo, fuse=a.fuse, overlap=not a.no_overlap,
                            preload_halo=a.preload_halo, slots=a.slots, variant=a.variant,
-                           concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent])
+                           transport=a.transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent])
     blur.load_synthetic(a.seed)
 
     for _ in range(a.warmup):
@@ -98,6 +124,7 @@ def main():
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
     stats = blur.stats
+    mismatches = check_bands(blur, a) if a.check else None
 
     # ---- extra: device-resident loop only (reps on the resident band)
     eng = blur.engine
@@ -152,9 +179,11 @@ def main():
                 "mpix_per_s": round(loop_value, 2) if loop_value else None,
                 "us_per_rep": round(loop_elapsed / ls / a.reps * 1e6, 3) if ls else None,
             },
-            "device": torch.cuda.get_device_name(ctx.local_rank),
+            "device": torch.cuda.get_device_name(device),
             "pconv": pconv.__version__,
         }
+        if mismatches is not None:
+            out["mismatches"] = mismatches
         print(json.dumps(out), flush=True)
     shutdown(ctx)
 

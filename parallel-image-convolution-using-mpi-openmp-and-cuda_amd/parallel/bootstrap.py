@@ -86,6 +86,15 @@ def max_over_ranks(value: float, group=None) -> float:
     return float(t.item())
 
 
+def sum_over_ranks(value: int, group=None) -> int:
+    """Integer sum over ranks (mismatch counts of distributed checks)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return int(value)
+    t = torch.tensor([int(value)], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return int(t.item())
+
+
 def barrier(group=None) -> None:
     if dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.barrier(group=group)

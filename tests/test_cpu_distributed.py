@@ -69,3 +69,47 @@ def test_gloo_bands_equal_serial(pconv_mod, world, halo, fuse, preload):
     out = np.concatenate([r[2] for r in res], axis=0).reshape(img.shape)
     assert np.array_equal(out, pconv_mod.numpy_convolve(img, reps))
     assert all(r[3] >= (0 if preload else 1) for r in res)
+
+
+def _torchrun(world, args, cwd, timeout=240):
+    import subprocess
+    import sys
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", "-m", "pconv.parallel.run"] + args
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    return subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("world,extra", [
+    (1, []),
+    (2, []),
+    (3, ["--exchange-halo"]),
+    (2, ["--filter", "box", "--halo", "2"]),
+    (3, ["--filter", "edge", "--no-overlap", "--exchange-halo", "--halo", "1"]),
+    (4, ["--backend", "cpu", "--fuse", "3", "--halo", "3"]),
+])
+def test_torchrun_per_rank_program(pconv_mod, tmp_path, world, extra):
+    """`torch.distributed.run -m pconv.parallel.run` (the mpiexec analog): each
+    rank reads its band (+ ghost rows), runs the schedule with gloo halos,
+    pwrites its band; the file equals the oracle."""
+    import json
+
+    img = np.random.default_rng(world).integers(0, 256, size=(37, 29, 3), dtype=np.uint8)
+    pconv_mod.write_raw(str(tmp_path / "pic.raw"), img)
+    r = _torchrun(world, ["pic.raw", "29", "37", "7", "rgb", "--backend", "omp", "--json", "--check"] + extra,
+                  tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.strip().splitlines()
+    float(lines[-2])  # reference "%f" line
+    meta = json.loads(lines[-1])
+    assert meta["mismatches"] == 0 and meta["ranks"] == world
+    filt = extra[extra.index("--filter") + 1] if "--filter" in extra else "gaussian"
+    out = pconv_mod.read_raw(str(tmp_path / "blur_pic.raw"), 29, 37, "rgb")
+    assert np.array_equal(out, pconv_mod.numpy_convolve(img, 7, filt))
+
+
+def test_torchrun_usage_error(tmp_path):
+    r = _torchrun(1, ["pic.raw", "29", "37", "7", "purple"], tmp_path)
+    assert r.returncode != 0
+    assert "Error Input!" in r.stderr

@@ -68,3 +68,48 @@ def test_multiprocess_bands_one_gpu(pconv_mod, world, halo, fuse, preload, slots
         out = np.concatenate([r[2][i] for r in res]).reshape(ref.shape)
         assert np.array_equal(out, ref), (world, halo, fuse, preload, i)
     assert all(r[3] >= 1 for r in res)
+
+
+@pytest.mark.parametrize("world,extra", [(2, []), (3, ["--preload-halo"]), (2, ["--slots", "1", "--no-overlap"])])
+def test_bench_torchrun_rehearsal(world, extra):
+    """bench.py under torch.distributed.run with `world` ranks sharing the one
+    GPU (gloo-host halos): the driver's N-GPU launch path, checked bit-exact."""
+    import json
+    import subprocess
+    import sys
+
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--steps", "3", "--warmup", "1", "--transport", "gloo-host", "--check"] + extra
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    meta = json.loads(lines[0])
+    assert meta["n_gpus"] == world and meta["mismatches"] == 0
+    assert meta["value"] > 0 and meta["config"]["parallelism"] == f"rowband{world}"
+
+
+@pytest.mark.parametrize("world,extra", [(2, []), (3, ["--exchange-halo", "--halo", "3", "--fuse", "3"]),
+                                         (2, ["--filter", "box"])])
+def test_torchrun_per_rank_program_hip(pconv_mod, tmp_path, world, extra):
+    """`torch.distributed.run -m pconv.parallel.run --backend hip`: ranks share
+    the GPU, halos via gloo-host; the written file equals the oracle."""
+    import json
+    import subprocess
+    import sys
+
+    img = np.random.default_rng(world).integers(0, 256, size=(61, 47, 3), dtype=np.uint8)
+    pconv_mod.write_raw(str(tmp_path / "pic.raw"), img)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", "-m", "pconv.parallel.run",
+           "pic.raw", "47", "61", "11", "rgb", "--transport", "gloo-host", "--json", "--check"] + extra
+    r = subprocess.run(cmd, cwd=tmp_path, env=dict(os.environ, PYTHONPATH=ROOT), capture_output=True, text=True,
+                       timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    meta = json.loads(r.stdout.strip().splitlines()[-1])
+    assert meta["mismatches"] == 0 and meta["backend"] == "hip"
+    filt = extra[extra.index("--filter") + 1] if "--filter" in extra else "gaussian"
+    out = pconv_mod.read_raw(str(tmp_path / "blur_pic.raw"), 47, 61, "rgb")
+    assert np.array_equal(out, pconv_mod.numpy_convolve(img, 11, filt))
