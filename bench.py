@@ -65,11 +65,11 @@ def check_bands(blur, a) -> int:
     the whole synthetic image; returns the total mismatching bytes (all ranks)."""
     import numpy as np
 
-    from pconv import native
+    from pconv._native import require_native
     from pconv.models.filters import get_filter
     from pconv.parallel.bootstrap import sum_over_ranks
 
-    n = native()
+    n = require_native()
     full = np.empty(a.width * a.height * {"grey": 1, "rgb": 3, "rgba": 4}[a.channels], np.uint8)
     n.synth_rows(full, a.width, a.height, a.channels, int(a.seed), 0, a.height)
     ref = np.empty_like(full)
