@@ -113,6 +113,16 @@ class BandEngine {
 
   // Enqueue `reps` repetitions (async).  stats filled after synchronize().
   void run(int reps);
+  // One whole serving step — H2D of host rows [in_r0, in_r1) (ghost rows
+  // allowed), `reps` repetitions, D2H of the owned rows — as ONE cached
+  // hipGraph launched on the compute stream: one host API call per image
+  // instead of ~12 (copies, launches, events; tools/ubench/api_cost.hip).
+  // The schedule must need no halo exchange (single band, or pre-loaded
+  // ghost rows deep enough for all `reps`).  Host buffers must be pinned and
+  // stay valid; the graph is keyed on them.
+  void process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps);
+  // True when `reps` repetitions with / without pre-loaded ghost rows need no exchange.
+  bool exchange_free(int reps, bool halo_preloaded) const;
   // Phase-by-phase execution for multi-band emulation on one device.
   std::vector<Phase> plan(int reps) const;
   void exec_exchange(const Phase& p);
@@ -146,6 +156,13 @@ class BandEngine {
   bool timing_pending_ = false;
   // hipGraph cache: (reps, start buffer) -> executable graph
   std::map<std::pair<int, int>, hipGraphExec_t> graphs_;
+  struct StepGraph {
+    hipGraphExec_t exec = nullptr;
+    int end_cur = 0;
+    int launches = 0;
+  };
+  // (reps, start buffer, in, in_r0, in_r1, out) -> whole-step graph
+  std::map<std::tuple<int, int, const uint8_t*, int64_t, int64_t, uint8_t*>, StepGraph> step_graphs_;
 };
 
 // Serving pipeline: S band engines ("slots") so that the H2D copy of image
@@ -157,8 +174,11 @@ class BandPipeline {
  public:
   // concurrent: -1 = when the hardware-queue budget allows, 0 = one shared
   // compute stream, 1 = one compute stream per slot.
+  // graphs: every image is one hipGraph (H2D + reps + D2H) on its slot's own
+  // stream — slots run concurrently, one host call per image; needs
+  // exchange-free images (see BandEngine::process_graph).
   BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt, int slots,
-               int concurrent = -1);
+               int concurrent = -1, bool graphs = false);
   ~BandPipeline();
   int slots() const { return static_cast<int>(slots_.size()); }
   BandEngine& slot(int i) { return *slots_.at(i); }
@@ -171,11 +191,13 @@ class BandPipeline {
   int64_t submitted() const { return count_; }
   // True when slots run their repetitions on separate compute streams.
   bool concurrent() const { return concurrent_; }
+  bool graphs() const { return graphs_; }
 
  private:
   Stream h2d_, d2h_, comm_;
   std::vector<Stream> computes_;
   bool concurrent_ = false;
+  bool graphs_ = false;
   std::vector<std::unique_ptr<BandEngine>> slots_;
   std::vector<Event> ev_up_, ev_done_, ev_free_, ev_halo_;
   std::vector<bool> used_;

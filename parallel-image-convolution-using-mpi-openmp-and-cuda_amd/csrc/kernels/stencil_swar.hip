@@ -231,6 +231,7 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
 constexpr SwarShape kShapes[] = {
     {8, 8, 8}, {8, 8, 4}, {8, 16, 4}, {8, 4, 8},              // 8-byte lanes: large images
     {4, 8, 8}, {4, 6, 8}, {4, 5, 8}, {4, 4, 8}, {4, 3, 8}, {4, 4, 16},  // 4-byte lanes: small bands
+    {4, 2, 16}, {4, 3, 16}, {8, 2, 16}, {8, 4, 16},                     // 16 waves: latency-bound bands
 };
 
 template <int CH, int LW, int M, int NW>
@@ -267,6 +268,10 @@ void launch_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh) {
   PCONV_SWAR(4, 4, 8)
   PCONV_SWAR(4, 3, 8)
   PCONV_SWAR(4, 4, 16)
+  PCONV_SWAR(4, 2, 16)
+  PCONV_SWAR(4, 3, 16)
+  PCONV_SWAR(8, 2, 16)
+  PCONV_SWAR(8, 4, 16)
 #undef PCONV_SWAR
   PCONV_FAIL("swar temporal kernel: unsupported tile shape");
 }

@@ -59,6 +59,7 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
 
 BandEngine::~BandEngine() {
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : step_graphs_) (void)hipGraphExecDestroy(kv.second.exec);
   if (cs_) (void)hipStreamSynchronize(cs_);
   if (ms_) (void)hipStreamSynchronize(ms_);
 }
@@ -177,7 +178,8 @@ void BandEngine::run(int reps) {
   pre_exchanges_ = 0;
   wall_t0_ = wall_seconds();
   if (opt_.timing) ev_t0_.record(cs_);
-  const bool graph = opt_.use_graph && !transport_ && !ph.empty();
+  bool graph = opt_.use_graph && !ph.empty();
+  for (const auto& p : ph) graph = graph && p.exchange_depth == 0;
   if (graph) {
     const auto key = std::make_pair(reps, cur_);
     auto it = graphs_.find(key);
@@ -209,6 +211,46 @@ void BandEngine::run(int reps) {
   halo_valid_ = false;
 }
 
+bool BandEngine::exchange_free(int reps, bool halo_preloaded) const {
+  PlanConfig c = engine_plan_config(geom_, band_, filter_, opt_);
+  c.halo_preloaded = halo_preloaded;
+  for (const auto& p : plan_band(band_, reps, c))
+    if (p.exchange_depth > 0) return false;
+  return true;
+}
+
+void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
+  PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
+  const bool preloaded = in_r0 < 0 || in_r1 > band_.rows;
+  halo_valid_ = preloaded;
+  const std::vector<Phase> ph = plan(reps);
+  for (const auto& p : ph)
+    PCONV_CHECK(p.exchange_depth == 0, "process_graph: this schedule needs halo exchanges (pre-load deeper ghost rows)");
+  const auto key = std::make_tuple(reps, cur_, host_in, in_r0, in_r1, host_out);
+  auto it = step_graphs_.find(key);
+  stats_ = RunStats{};
+  if (it == step_graphs_.end()) {
+    const int64_t rb = lay_.row_bytes;
+    hipGraph_t g = nullptr;
+    PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
+    upload_rows(host_in, rb, in_r0, in_r1, cs_);
+    for (const auto& p : ph) enqueue_phase(p);
+    download_rows(host_out, rb, 0, band_.rows, cs_);
+    PCONV_HIP_CHECK(hipStreamEndCapture(cs_, &g));
+    StepGraph sg;
+    PCONV_HIP_CHECK(hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0));
+    PCONV_HIP_CHECK(hipGraphDestroy(g));
+    sg.end_cur = cur_;
+    sg.launches = stats_.launches;
+    it = step_graphs_.emplace(key, sg).first;
+  } else {
+    cur_ = it->second.end_cur;
+    stats_.launches = it->second.launches;
+  }
+  PCONV_HIP_CHECK(hipGraphLaunch(it->second.exec, cs_));
+  halo_valid_ = false;
+}
+
 void BandEngine::exec_exchange(const Phase& p) {
   if (p.exchange_depth <= 0) return;
   PCONV_CHECK(transport_ != nullptr, "band has neighbours but no halo transport is attached");
@@ -234,9 +276,26 @@ void BandEngine::synchronize() {
 // --------------------------------------------------------------- BandPipeline
 
 BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt,
-                           int slots, int concurrent) {
+                           int slots, int concurrent, bool graphs) {
   PCONV_CHECK(slots >= 1 && slots <= 8, "pipeline slots must be in [1, 8]");
   set_device(opt.device);
+  if (graphs) {
+    // One stream per slot carries that slot's whole image (H2D, reps, D2H) as
+    // one graph: slots overlap each other without cross-stream events.
+    graphs_ = true;
+    concurrent_ = slots > 1;
+    EngineOptions o = opt;
+    o.use_graph = false;
+    o.timing = false;
+    for (int i = 0; i < slots; ++i) {
+      computes_.push_back(Stream::create(0));
+      o.compute_stream = computes_.back().get();
+      o.comm_stream = computes_.back().get();
+      slots_.push_back(std::make_unique<BandEngine>(geom, band, filter, o));
+    }
+    used_.assign(slots, false);
+    return;
+  }
   // Streams: H2D, D2H, communication (only with neighbours) and compute.
   // HIP maps streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by
   // default); two busy streams on one queue serialise falsely.  When the
@@ -271,9 +330,9 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
 }
 
 BandPipeline::~BandPipeline() {
-  (void)hipStreamSynchronize(h2d_.get());
+  if (h2d_.get()) (void)hipStreamSynchronize(h2d_.get());
   for (auto& c : computes_) (void)hipStreamSynchronize(c.get());
-  (void)hipStreamSynchronize(d2h_.get());
+  if (d2h_.get()) (void)hipStreamSynchronize(d2h_.get());
   if (comm_.get()) (void)hipStreamSynchronize(comm_.get());
 }
 
@@ -284,6 +343,12 @@ void BandPipeline::set_transport(std::shared_ptr<HaloTransport> t) {
 void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
   const int k = static_cast<int>(count_ % static_cast<int64_t>(slots_.size()));
   BandEngine& e = *slots_[k];
+  if (graphs_) {
+    e.process_graph(host_in, in_r0, in_r1, host_out, reps);
+    used_[k] = true;
+    ++count_;
+    return;
+  }
   // H2D into slot k once its previous image has been downloaded.
   if (used_[k]) ev_free_[k].wait_on(h2d_.get());
   e.upload_rows(host_in, e.layout().row_bytes, in_r0, in_r1, h2d_.get());
@@ -312,9 +377,9 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
 }
 
 void BandPipeline::drain() {
-  PCONV_HIP_CHECK(hipStreamSynchronize(h2d_.get()));
+  if (h2d_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(h2d_.get()));
   for (auto& s : slots_) s->synchronize();
-  PCONV_HIP_CHECK(hipStreamSynchronize(d2h_.get()));
+  if (d2h_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(d2h_.get()));
 }
 
 // --------------------------------------------------------------- LocalCluster

@@ -430,6 +430,15 @@ PYBIND11_MODULE(_pconv_native, m) {
             e.synchronize();
           },
           py::arg("in_ptr"), py::arg("in_r0"), py::arg("in_r1"), py::arg("out_ptr"), py::arg("reps"))
+      .def(
+          "process_graph",
+          [](BandEngine& e, uintptr_t in_ptr, int64_t in_r0, int64_t in_r1, uintptr_t out_ptr, int reps) {
+            py::gil_scoped_release nogil;
+            e.process_graph(reinterpret_cast<const uint8_t*>(in_ptr), in_r0, in_r1, reinterpret_cast<uint8_t*>(out_ptr),
+                            reps);
+          },
+          py::arg("in_ptr"), py::arg("in_r0"), py::arg("in_r1"), py::arg("out_ptr"), py::arg("reps"))
+      .def("exchange_free", &BandEngine::exchange_free, py::arg("reps"), py::arg("halo_preloaded"))
       .def("attach_rccl",
            [](BandEngine& e, std::shared_ptr<RcclComm> c) {
              e.set_transport(std::make_shared<RcclTransport>(std::move(c)));
@@ -442,7 +451,7 @@ PYBIND11_MODULE(_pconv_native, m) {
   py::class_<BandPipeline>(m, "BandPipeline")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
-                       int concurrent) {
+                       int concurrent, bool graphs) {
              EngineOptions o;
              o.device = device;
              o.halo_depth = halo;
@@ -451,11 +460,12 @@ PYBIND11_MODULE(_pconv_native, m) {
              o.variant = parse_variant(variant);
              const ImageGeom g = make_geom(w, h, ch);
              return std::make_unique<BandPipeline>(g, row_band(h, world, rank), make_filter(filter), o, slots,
-                                                   concurrent);
+                                                   concurrent, graphs);
            }),
            py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
            py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
-           py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1)
+           py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1,
+           py::arg("graphs") = false)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -473,7 +483,8 @@ PYBIND11_MODULE(_pconv_native, m) {
           py::arg("in_ptr"), py::arg("in_r0"), py::arg("in_r1"), py::arg("out_ptr"), py::arg("reps"))
       .def("drain", &BandPipeline::drain, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("submitted", &BandPipeline::submitted)
-      .def_property_readonly("concurrent", &BandPipeline::concurrent);
+      .def_property_readonly("concurrent", &BandPipeline::concurrent)
+      .def_property_readonly("graphs", &BandPipeline::graphs);
 
   py::class_<LocalCluster>(m, "LocalCluster")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int bands, int device, int halo,

@@ -41,7 +41,8 @@ class DistributedBlur:
                  reps: Optional[int] = None, *, rank: Optional[int] = None, world: Optional[int] = None,
                  device: Optional[int] = None, halo: Optional[int] = None, fuse: Optional[int] = None,
                  overlap: bool = True, preload_halo: bool = False, comm=None, slots: int = 2,
-                 variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1):
+                 variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
+                 step_graphs: Optional[bool] = None):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -53,15 +54,25 @@ class DistributedBlur:
             fuse = DEFAULT_FUSE if n.supports_fusion(nf, variant) else 1
         if halo is None:
             halo = auto_halo(self.height, self.world, reps, fuse)
-        self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
-                                   halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant,
-                                   slots=int(slots), concurrent=int(concurrent))
+        kw = dict(halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant, slots=int(slots),
+                  concurrent=int(concurrent))
+        self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device, **kw)
+        self.preload_halo = bool(preload_halo) and self.world > 1
+        # Whole-step graphs (one host call per image, slots on their own
+        # streams) whenever the images need no halo exchange: one band, or
+        # ghost rows pre-loaded deep enough for all `reps`.
+        free = reps is not None and self.pipe.slot(0).exchange_free(int(reps), self.preload_halo)
+        if step_graphs and not free:
+            raise ValueError("step_graphs needs exchange-free images (world 1, or preload_halo with halo >= reps)")
+        if (free if step_graphs is None else bool(step_graphs)):
+            del self.pipe
+            self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
+                                       graphs=True, **kw)
         self.engine = self.pipe.slot(0)
         self.band = self.engine.band
         self.row_bytes = self.engine.row_bytes
         d = self.engine.halo
         b = self.band
-        self.preload_halo = bool(preload_halo) and self.world > 1
         self.above = min(d, b.y0) if self.preload_halo else 0
         self.below = min(d, self.height - (b.y0 + b.rows)) if self.preload_halo else 0
         in_rows = b.rows + self.above + self.below
@@ -75,7 +86,7 @@ class DistributedBlur:
         self._next = 0
         self.comm = None
         self.transport = None
-        if self.world > 1:
+        if self.world > 1 and transport != "none":  # "none": exchange-free images only
             if transport == "rccl":
                 self.comm = comm if comm is not None else make_rccl_comm(self.device)
                 self.pipe.attach_rccl(self.comm)
@@ -85,7 +96,7 @@ class DistributedBlur:
                 self.transport = GlooHostTransport()
                 self.pipe.attach_transport(self.transport)
             else:
-                raise ValueError(f"unknown transport {transport!r} (rccl|gloo-host)")
+                raise ValueError(f"unknown transport {transport!r} (rccl|gloo-host|none)")
 
     # ------------------------------------------------------------ inputs
     @property

@@ -70,7 +70,8 @@ def test_multiprocess_bands_one_gpu(pconv_mod, world, halo, fuse, preload, slots
     assert all(r[3] >= 1 for r in res)
 
 
-@pytest.mark.parametrize("world,extra", [(2, []), (3, ["--preload-halo"]), (2, ["--slots", "1", "--no-overlap"])])
+@pytest.mark.parametrize("world,extra", [(2, []), (3, ["--halo-mode", "exchange"]), (4, []),
+                                         (2, ["--slots", "1", "--no-overlap", "--halo-mode", "exchange"])])
 def test_bench_torchrun_rehearsal(world, extra):
     """bench.py under torch.distributed.run with `world` ranks sharing the one
     GPU (gloo-host halos): the driver's N-GPU launch path, checked bit-exact."""

@@ -25,6 +25,7 @@ def main():
     p.add_argument("--fuse", default="4,8,12,16")
     p.add_argument("--iters", type=int, default=10)
     p.add_argument("--rounds", type=int, default=2)
+    p.add_argument("--shapes", default="all", help="all | auto | list of lw,m,nw separated by ';'")
     a = p.parse_args()
     import numpy as np
 
@@ -46,7 +47,9 @@ def main():
             e.upload(np.ascontiguousarray(rows).reshape(-1), 0, b.rows)
             e.synchronize()
             res = {}
-            for sh in [None] + shapes:
+            todo = [None] + shapes if a.shapes == "all" else [None] if a.shapes == "auto" else \
+                [tuple(int(v) for v in x.split(",")) for x in a.shapes.split(";")]
+            for sh in todo:
                 try:
                     n.set_swar_shape(*(sh or (0, 0, 0)))
                     e.run(a.reps)

@@ -16,6 +16,17 @@
     }                                                                   \
   } while (0)
 
+// Zero-copy: the CUs move the bytes over PCIe themselves (pinned host memory
+// is mapped into the GPU's address space).  One uint4 per lane, rows pitched.
+__global__ void k_copy_rows(const uint8_t* __restrict__ src, size_t sp, uint8_t* __restrict__ dst, size_t dp, int w16,
+                            int h) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  const int y = blockIdx.y;
+  if (x >= w16 || y >= h) return;
+  const uint4 v = reinterpret_cast<const uint4*>(src + y * sp)[x];
+  reinterpret_cast<uint4*>(dst + y * dp)[x] = v;
+}
+
 int main(int argc, char** argv) {
   const size_t W = 5760, H = 2520, P = 5888;  // 1920x2520 RGB row bytes, frame pitch
   const size_t bytes = W * H;
@@ -102,6 +113,55 @@ int main(int argc, char** argv) {
     CHECK(hipEventSynchronize(e1));
     CHECK(hipEventElapsedTime(&ms, e0, e1));
     report("H2D+D2H concurrent contiguous", ms, 2 * bytes / 1e9);
+    // zero-copy kernels (pitched device frame, contiguous host rows)
+    const int w16 = static_cast<int>(W / 16);
+    const dim3 blk(256), grd((w16 + 255) / 256, H);
+    CHECK(hipEventRecord(e0, s1));
+    for (int i = 0; i < iters; ++i)
+      k_copy_rows<<<grd, blk, 0, s1>>>((const uint8_t*)h_in, W, (uint8_t*)d_a + 16 + 0, P, w16, H);
+    CHECK(hipEventRecord(e1, s1));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    report("H2D zero-copy kernel", ms, bytes / 1e9);
+    CHECK(hipEventRecord(e0, s1));
+    for (int i = 0; i < iters; ++i)
+      k_copy_rows<<<grd, blk, 0, s1>>>((const uint8_t*)d_b + 16, P, (uint8_t*)h_out, W, w16, H);
+    CHECK(hipEventRecord(e1, s1));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    report("D2H zero-copy kernel", ms, bytes / 1e9);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(e0, 0));
+    CHECK(hipStreamWaitEvent(s1, e0, 0));
+    CHECK(hipStreamWaitEvent(s2, e0, 0));
+    for (int i = 0; i < iters; ++i) {
+      k_copy_rows<<<grd, blk, 0, s1>>>((const uint8_t*)h_in, W, (uint8_t*)d_a + 16, P, w16, H);
+      k_copy_rows<<<grd, blk, 0, s2>>>((const uint8_t*)d_b + 16, P, (uint8_t*)h_out, W, w16, H);
+    }
+    CHECK(hipEventRecord(ea, s1));
+    CHECK(hipEventRecord(eb, s2));
+    CHECK(hipStreamWaitEvent(0, ea, 0));
+    CHECK(hipStreamWaitEvent(0, eb, 0));
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    report("H2D+D2H zero-copy concurrent", ms, 2 * bytes / 1e9);
+    // mixed: SDMA H2D + zero-copy D2H kernel
+    CHECK(hipEventRecord(e0, 0));
+    CHECK(hipStreamWaitEvent(s1, e0, 0));
+    CHECK(hipStreamWaitEvent(s2, e0, 0));
+    for (int i = 0; i < iters; ++i) {
+      CHECK(hipMemcpy2DAsync((char*)d_a + 16, P, h_in, W, W, H, hipMemcpyHostToDevice, s1));
+      k_copy_rows<<<grd, blk, 0, s2>>>((const uint8_t*)d_b + 16, P, (uint8_t*)h_out, W, w16, H);
+    }
+    CHECK(hipEventRecord(ea, s1));
+    CHECK(hipEventRecord(eb, s2));
+    CHECK(hipStreamWaitEvent(0, ea, 0));
+    CHECK(hipStreamWaitEvent(0, eb, 0));
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    report("SDMA H2D + zero-copy D2H", ms, 2 * bytes / 1e9);
   }
   return 0;
 }
