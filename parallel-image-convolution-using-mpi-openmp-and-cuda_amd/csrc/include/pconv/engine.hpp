@@ -57,6 +57,10 @@ struct EngineOptions {
   // hipEvent loop timing around every run() (two event records, ~3 us of
   // host time each on ROCm 7: the serving pipeline turns it off).
   bool timing = true;
+  // process_graph(): the image's last launch stores its rows straight into
+  // the pinned host output (zero-copy D2H fused into the producing kernel)
+  // instead of a separate D2H copy — when the filter / row size allow it.
+  bool zero_copy_out = false;
 };
 
 struct RunStats {
@@ -136,7 +140,7 @@ class BandEngine {
 
  private:
   void enqueue_phase(const Phase& p);
-  void launch(const LaunchSpec& l, hipStream_t s);
+  void launch(const LaunchSpec& l, hipStream_t s, uint8_t* dst = nullptr, int64_t dst_pitch = 0);
 
   ImageGeom geom_;
   Band band_;
@@ -160,6 +164,7 @@ class BandEngine {
     hipGraphExec_t exec = nullptr;
     int end_cur = 0;
     int launches = 0;
+    bool zero_copy = false;
   };
   // (reps, start buffer, in, in_r0, in_r1, out) -> whole-step graph
   std::map<std::tuple<int, int, const uint8_t*, int64_t, int64_t, uint8_t*>, StepGraph> step_graphs_;

@@ -111,10 +111,23 @@ __device__ __forceinline__ void pack(const u32 (&D)[NP], typename Chunk<NP>::T& 
   }
 }
 
+template <int NP>
+__device__ __forceinline__ void store_bytes(uint8_t* p, const typename Chunk<NP>::T& v, int n) {
+  u32 w[2];
+  if constexpr (NP == 8) {
+    w[0] = v.x;
+    w[1] = v.y;
+  } else {
+    w[0] = v;
+    w[1] = 0;
+  }
+  for (int k = 0; k < n; ++k) p[k] = static_cast<uint8_t>(w[k >> 2] >> (8 * (k & 3)));
+}
+
 template <int CH, int LW, int M, int NW>
 __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                  int64_t pitch, int row_bytes, int r0, int r1, int steps, int g_row0,
-                                                  int height, int nstrips, int pair_stride) {
+                                                  int64_t pitch, int64_t dst_pitch, int row_bytes, int r0, int r1,
+                                                  int steps, int g_row0, int height, int nstrips, int pair_stride) {
   constexpr int NP = LW;       // pairs per row per lane
   constexpr int NQ = NP / 4;   // uint4 per row per lane
   using CT = typename Chunk<NP>::T;
@@ -220,9 +233,21 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
     if (fr >= st_lo && fr < st_hi) {
       CT a, b;
       pack<NP>(D[i], a, b);
-      uint8_t* rowq = dst + static_cast<int64_t>(fr) * pitch;
-      if (stA) *reinterpret_cast<CT*>(rowq + xA) = a;
-      if (stB) *reinterpret_cast<CT*>(rowq + xB) = b;
+      uint8_t* rowq = dst + static_cast<int64_t>(fr) * dst_pitch;
+      // Whole chunks as one store; the row's last partial chunk byte by byte
+      // (dst may be a packed host buffer with no pad after the row).
+      if (stA) {
+        if (validA == LW)
+          *reinterpret_cast<CT*>(rowq + xA) = a;
+        else
+          store_bytes<NP>(rowq + xA, a, validA);
+      }
+      if (stB) {
+        if (validB == LW)
+          *reinterpret_cast<CT*>(rowq + xB) = b;
+        else
+          store_bytes<NP>(rowq + xB, b, validB);
+      }
     }
   }
 }
@@ -245,7 +270,8 @@ void launch_one(const StencilLaunch& a, hipStream_t s) {
   const int pair_stride = (nstrips + 1) / 2;
   const dim3 grid(pair_stride, ceil_div(static_cast<int>(a.r1 - a.r0), vrows));
   const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
-  k_swar<CH, LW, M, NW><<<grid, dim3(64 * NW), 0, s>>>(a.src, a.dst, a.pitch, static_cast<int>(a.row_bytes),
+  k_swar<CH, LW, M, NW><<<grid, dim3(64 * NW), 0, s>>>(a.src, a.dst, a.pitch, a.dst_pitch ? a.dst_pitch : a.pitch,
+                                                       static_cast<int>(a.row_bytes),
                                                        static_cast<int>(a.r0), static_cast<int>(a.r1), steps,
                                                        static_cast<int>(a.g_row0), static_cast<int>(hmax), nstrips,
                                                        pair_stride);

@@ -122,10 +122,11 @@ std::vector<Phase> BandEngine::plan(int reps) const {
   return plan_band(band_, reps, c);
 }
 
-void BandEngine::launch(const LaunchSpec& l, hipStream_t s) {
+void BandEngine::launch(const LaunchSpec& l, hipStream_t s, uint8_t* dst, int64_t dst_pitch) {
   StencilLaunch a;
   a.src = src_frame();
-  a.dst = dst_frame();
+  a.dst = dst ? dst : dst_frame();
+  a.dst_pitch = dst ? dst_pitch : 0;
   a.pitch = lay_.pitch;
   a.row_bytes = lay_.row_bytes;
   a.r0 = l.lo;
@@ -232,12 +233,24 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
   if (it == step_graphs_.end()) {
     const int64_t rb = lay_.row_bytes;
     hipGraph_t g = nullptr;
+    // Zero-copy output: the last launch must produce exactly the owned rows
+    // with the SWAR kernel (gaussian) into a 4-byte-aligned packed row pitch.
+    const bool zc = opt_.zero_copy_out && !ph.empty() && ph.back().launches.size() == 1 &&
+                    ph.back().launches[0].lo == 0 && ph.back().launches[0].hi == band_.rows && filter_.binomial121 &&
+                    (opt_.variant == KernelVariant::Auto || opt_.variant == KernelVariant::Temporal) && rb % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(host_out) % 16 == 0;
     PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
     upload_rows(host_in, rb, in_r0, in_r1, cs_);
-    for (const auto& p : ph) enqueue_phase(p);
-    download_rows(host_out, rb, 0, band_.rows, cs_);
+    for (size_t i = 0; i + (zc ? 1 : 0) < ph.size(); ++i) enqueue_phase(ph[i]);
+    if (zc) {
+      launch(ph.back().launches[0], cs_, host_out, rb);
+      cur_ ^= 1;  // frame state as after the phase (its rows now live on the host)
+    } else {
+      download_rows(host_out, rb, 0, band_.rows, cs_);
+    }
     PCONV_HIP_CHECK(hipStreamEndCapture(cs_, &g));
     StepGraph sg;
+    sg.zero_copy = zc;
     PCONV_HIP_CHECK(hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0));
     PCONV_HIP_CHECK(hipGraphDestroy(g));
     sg.end_cur = cur_;

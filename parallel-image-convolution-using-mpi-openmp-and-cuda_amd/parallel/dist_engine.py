@@ -42,7 +42,7 @@ class DistributedBlur:
                  device: Optional[int] = None, halo: Optional[int] = None, fuse: Optional[int] = None,
                  overlap: bool = True, preload_halo: bool = False, comm=None, slots: int = 2,
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
-                 step_graphs: Optional[bool] = None):
+                 step_graphs: Optional[bool] = None, zero_copy_out: bool = False):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -67,7 +67,7 @@ class DistributedBlur:
         if (free if step_graphs is None else bool(step_graphs)):
             del self.pipe
             self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
-                                       graphs=True, **kw)
+                                       graphs=True, zero_copy_out=bool(zero_copy_out), **kw)
         self.engine = self.pipe.slot(0)
         self.band = self.engine.band
         self.row_bytes = self.engine.row_bytes

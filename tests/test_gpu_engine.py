@@ -152,3 +152,26 @@ def test_pipeline_step_graphs_preloaded_band(pconv_mod, rng):
     out = blur.step(reps)
     b = blur.band
     assert np.array_equal(out, pconv_mod.numpy_convolve(img, reps)[b.y0:b.y0 + b.rows])
+
+
+@pytest.mark.parametrize("w,h,ch,reps,fuse", [(67, 45, "rgb", 9, 8), (64, 33, "grey", 13, 8), (40, 50, "rgba", 8, 4),
+                                              (61, 20, "rgb", 3, 8), (1920, 64, "rgb", 40, 8)])
+def test_pipeline_zero_copy_out(pconv_mod, rng, w, h, ch, reps, fuse):
+    """The last fused launch writes into pinned host memory (packed rows):
+    every byte rewritten (pre-filled with 0xAB) and exact — a partial last
+    chunk spilling into the next packed row would show as a mismatch."""
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    c = {"grey": 1, "rgb": 3, "rgba": 4}[ch]
+    blur = DistributedBlur(w, h, ch, "gaussian", reps, rank=0, world=1, device=0, fuse=fuse, slots=2,
+                           step_graphs=True, zero_copy_out=True)
+    for rnd in range(2):
+        img = rng.integers(0, 256, size=(h, w, c), dtype=np.uint8)
+        blur.load_image(img)
+        for k in range(2):
+            blur.outputs[k][:] = 0xAB
+        ks = [blur.submit(reps) for _ in range(2)]
+        blur.drain()
+        ref = pconv_mod.numpy_convolve(img if c > 1 else img[..., 0], reps).reshape(h, -1)
+        for k in ks:
+            assert np.array_equal(blur.outputs[k].reshape(h, -1), ref), (rnd, k)
