@@ -18,6 +18,7 @@
 #include "pconv/engine.hpp"
 #include "pconv/raw_io.hpp"
 #include "pconv/rccl_comm.hpp"
+#include "pconv/trace.hpp"
 
 namespace pconv {
 
@@ -187,6 +188,7 @@ class ShmTransport : public HaloTransport {
       : sh_(sh), slots_(slots), slot_bytes_(slot_bytes), rank_(rank), world_(world), timeout_s_(timeout_s) {}
 
   void exchange(BandEngine& e, int64_t depth, hipStream_t stream) override {
+    TraceRange tr("pconv.halo.shm");
     const Band& b = e.band();
     const int64_t pitch = e.layout().pitch;
     const int64_t n = depth * pitch;
@@ -237,7 +239,10 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
   const int64_t below = c.preload_halo ? std::min<int64_t>(d, g.height - (b.y0 + b.rows)) : 0;
   const int64_t rb = g.row_bytes();
   PinnedBuffer host(static_cast<size_t>((b.rows + above + below) * rb));
-  load_rows(c, g, b.y0 - above, b.rows + above + below, host.data(), rb);
+  {
+    TraceRange tr("pconv.io.read_band");
+    load_rows(c, g, b.y0 - above, b.rows + above + below, host.data(), rb);
+  }
 
   std::shared_ptr<RcclComm> comm;
   if (shm) {
@@ -276,7 +281,10 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
   sh->exchanges[rank] = eng.last_stats().exchanges;
   eng.download_rows(host.data(), rb, 0, b.rows);
   eng.synchronize();
-  write_rows(out_path(c), g, b.y0, b.rows, host.data(), rb);
+  {
+    TraceRange tr("pconv.io.write_band");
+    write_rows(out_path(c), g, b.y0, b.rows, host.data(), rb);
+  }
   shm_barrier(sh, world, c.timeout_s);
 }
 

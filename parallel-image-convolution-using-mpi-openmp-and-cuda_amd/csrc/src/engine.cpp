@@ -1,6 +1,8 @@
 // BandEngine / LocalCluster (see engine.hpp).
 #include "pconv/engine.hpp"
 
+#include "pconv/trace.hpp"
+
 #include <algorithm>
 #include <cstdlib>
 #include <thread>
@@ -141,6 +143,7 @@ void BandEngine::launch(const LaunchSpec& l, hipStream_t s, uint8_t* dst, int64_
 }
 
 void BandEngine::enqueue_phase(const Phase& p) {
+  TraceRange tr(p.exchange_depth > 0 ? "pconv.phase.exchange" : "pconv.phase.compute");
   if (p.exchange_depth > 0) {
     PCONV_CHECK(transport_ != nullptr, "band has neighbours but no halo transport is attached");
     hipStream_t ms = comm_stream();
@@ -172,6 +175,7 @@ void BandEngine::exchange_now(hipStream_t stream) {
 }
 
 void BandEngine::run(int reps) {
+  TraceRange tr("pconv.run");
   PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
   const std::vector<Phase> ph = plan(reps);
   stats_ = RunStats{};
@@ -221,6 +225,7 @@ bool BandEngine::exchange_free(int reps, bool halo_preloaded) const {
 }
 
 void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
+  TraceRange tr("pconv.step_graph");
   PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
   const bool preloaded = in_r0 < 0 || in_r1 > band_.rows;
   halo_valid_ = preloaded;
@@ -354,6 +359,7 @@ void BandPipeline::set_transport(std::shared_ptr<HaloTransport> t) {
 }
 
 void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
+  TraceRange tr("pconv.pipeline.submit");
   const int k = static_cast<int>(count_ % static_cast<int64_t>(slots_.size()));
   BandEngine& e = *slots_[k];
   if (graphs_) {

@@ -1,5 +1,6 @@
 // RCCL communicator and halo transport (see rccl_comm.hpp).
 #include "pconv/rccl_comm.hpp"
+#include "pconv/trace.hpp"
 
 #include <rccl/rccl.h>
 
@@ -89,6 +90,7 @@ double RcclComm::allreduce_sum(double v) { return allreduce(v, ncclSum); }
 void RcclComm::barrier() { (void)allreduce(0.0, ncclSum); }
 
 void RcclTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream) {
+  TraceRange tr("pconv.halo.rccl");
   const FrameLayout& L = e.layout();
   const Band& b = e.band();
   const int64_t pitch = L.pitch;
