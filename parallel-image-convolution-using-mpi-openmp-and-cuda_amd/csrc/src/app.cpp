@@ -118,6 +118,7 @@ AppReport run_gpu1(const CliConfig& c) {
   const EngineOptions o = engine_options(c, g, 1, 0);
   BandEngine eng(g, row_band(g.height, 1, 0), f, o);
   if (c.explain) std::fprintf(stderr, "%s", describe_plan(eng.plan(c.reps)).c_str());
+  for (int i = 0; i < c.warmup; ++i) eng.run(c.reps);  // zero frames stay zero
   eng.upload_rows(host.data(), g.row_bytes(), 0, g.height);
   eng.synchronize();
   AppReport r;
@@ -265,6 +266,11 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
     eng.set_transport(std::make_shared<RcclTransport>(comm));
   }
 
+  for (int i = 0; i < c.warmup; ++i) {  // zero frames stay zero; every rank runs the same phases
+    eng.run(c.reps);
+    if (comm) comm->wait(eng.comm_stream(), c.timeout_s);
+    eng.synchronize();
+  }
   eng.upload_rows(host.data(), rb, -above, b.rows + below);
   eng.set_halo_valid(c.preload_halo);
   eng.synchronize();

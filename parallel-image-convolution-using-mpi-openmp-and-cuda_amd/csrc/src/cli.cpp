@@ -51,6 +51,8 @@ std::string help_text(const std::string& prog) {
          "  --transport {rccl,shm}    multi-GPU halo transport (shm: host-staged through shared memory;\n"
          "                            lets several ranks share one GPU)\n"
          "  --exchange-halo           ranks load only their own rows; ghost rows come from neighbours\n"
+         "  --warmup N                untimed runs of the schedule before loading the image (default 1;\n"
+         "                            loads the kernels' code objects and sets up RCCL connections)\n"
          "  --quiet                   suppress the timing lines\n";
 }
 
@@ -132,6 +134,8 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
         PCONV_FAIL("invalid --transport '" + c.transport + "' (rccl|shm)");
     } else if (a == "--exchange-halo") {
       c.preload_halo = false;
+    } else if (a == "--warmup") {
+      c.warmup = static_cast<int>(parse_int(next("--warmup"), "--warmup", 0, 100));
     } else {
       PCONV_FAIL("unknown option '" + a + "'");
     }

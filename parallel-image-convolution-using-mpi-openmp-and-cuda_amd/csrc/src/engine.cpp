@@ -188,7 +188,6 @@ void BandEngine::run(int reps) {
   if (graph) {
     const auto key = std::make_pair(reps, cur_);
     auto it = graphs_.find(key);
-    const int start = cur_;
     if (it == graphs_.end()) {
       hipGraph_t g = nullptr;
       PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeThreadLocal));
@@ -204,7 +203,6 @@ void BandEngine::run(int reps) {
         cur_ ^= 1;
       }
     }
-    (void)start;
     PCONV_HIP_CHECK(hipGraphLaunch(it->second, cs_));
   } else {
     for (const auto& p : ph) enqueue_phase(p);

@@ -162,6 +162,35 @@ int main(int argc, char** argv) {
     CHECK(hipEventSynchronize(e1));
     CHECK(hipEventElapsedTime(&ms, e0, e1));
     report("SDMA H2D + zero-copy D2H", ms, 2 * bytes / 1e9);
+    // each direction split in halves on two streams (4 SDMA queues busy)
+    {
+      static hipStream_t s3 = nullptr, s4 = nullptr;
+      if (!s3) {
+        CHECK(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
+        CHECK(hipStreamCreateWithFlags(&s4, hipStreamNonBlocking));
+      }
+      const size_t H2 = H / 2;
+      hipEvent_t ec, ed;
+      CHECK(hipEventCreate(&ec));
+      CHECK(hipEventCreate(&ed));
+      CHECK(hipEventRecord(e0, 0));
+      for (hipStream_t q : {s1, s2, s3, s4}) CHECK(hipStreamWaitEvent(q, e0, 0));
+      for (int i = 0; i < iters; ++i) {
+        CHECK(hipMemcpy2DAsync((char*)d_a + 16, P, h_in, W, W, H2, hipMemcpyHostToDevice, s1));
+        CHECK(hipMemcpy2DAsync((char*)d_a + 16 + H2 * P, P, (char*)h_in + H2 * W, W, W, H - H2, hipMemcpyHostToDevice, s3));
+        CHECK(hipMemcpy2DAsync(h_out, W, (char*)d_b + 16, P, W, H2, hipMemcpyDeviceToHost, s2));
+        CHECK(hipMemcpy2DAsync((char*)h_out + H2 * W, W, (char*)d_b + 16 + H2 * P, P, W, H - H2, hipMemcpyDeviceToHost, s4));
+      }
+      CHECK(hipEventRecord(ea, s1));
+      CHECK(hipEventRecord(eb, s2));
+      CHECK(hipEventRecord(ec, s3));
+      CHECK(hipEventRecord(ed, s4));
+      for (hipEvent_t x : {ea, eb, ec, ed}) CHECK(hipStreamWaitEvent(0, x, 0));
+      CHECK(hipEventRecord(e1, 0));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      report("H2D+D2H halves on 4 streams", ms, 2 * bytes / 1e9);
+    }
   }
   return 0;
 }
