@@ -37,7 +37,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <mutex>
+#include <tuple>
 
 #include "pconv/device.hpp"
 #include "swar.hpp"
@@ -348,14 +350,80 @@ void set_swar_shape(int lw, int m, int nw) {
 
 std::vector<SwarShape> swar_shapes() { return std::vector<SwarShape>(std::begin(kShapes), std::end(kShapes)); }
 
-// Latency model of one launch on 256 CUs x 4 SIMDs (cycles).  Inputs measured
-// on gfx950: a SIMD retires one VALU wave-instruction per ~5.8 cycles with
-// one resident wave, ~2.9 with two, ~2.8 with three or more
-// (tools/ubench/isa_rates.hip); workgroups per CU are bounded by LDS (NW x
-// LW KiB of boundary-row buffers), VGPRs (by M and LW) and 32 waves per CU;
-// the CU that receives the most workgroups sets the launch time; ~5.5k cycles
-// of load / store latency per tile.
+namespace {
+
+// Resources of one instantiation (VGPRs per lane, LDS bytes per workgroup)
+// as the compiler built it, from the runtime (hipFuncGetAttributes), cached.
+struct KernelRes {
+  int vgpr = 0;
+  int lds = 0;
+  bool measured = false;
+};
+
+template <int CH>
+KernelRes query_res(SwarShape sh) {
+  hipFuncAttributes at{};
+  hipError_t e = hipErrorInvalidValue;
+#define PCONV_SWAR(LW_, M_, NW_)                                                                     \
+  if (sh.lw == LW_ && sh.m == M_ && sh.nw == NW_)                                                   \
+    e = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_swar<CH, LW_, M_, NW_>));
+  PCONV_SWAR(8, 8, 8)
+  PCONV_SWAR(8, 8, 4)
+  PCONV_SWAR(8, 16, 4)
+  PCONV_SWAR(8, 4, 8)
+  PCONV_SWAR(4, 8, 8)
+  PCONV_SWAR(4, 6, 8)
+  PCONV_SWAR(4, 5, 8)
+  PCONV_SWAR(4, 4, 8)
+  PCONV_SWAR(4, 3, 8)
+  PCONV_SWAR(4, 4, 16)
+  PCONV_SWAR(4, 2, 16)
+  PCONV_SWAR(4, 3, 16)
+  PCONV_SWAR(8, 2, 16)
+  PCONV_SWAR(8, 4, 16)
+#undef PCONV_SWAR
+  KernelRes r;
+  if (e == hipSuccess && at.numRegs > 0) {
+    r.vgpr = at.numRegs;
+    r.lds = static_cast<int>(at.sharedSizeBytes);
+    r.measured = true;
+  } else {  // no device yet: estimate (register tile + temporaries; LDS = boundary rows)
+    (void)hipGetLastError();
+    r.vgpr = round_up(sh.m * sh.lw + 3 * sh.lw + 40, 8);
+    r.lds = sh.nw * sh.lw * 1024;
+  }
+  return r;
+}
+
+KernelRes kernel_res(SwarShape sh, int ch) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, int>, KernelRes> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_tuple(ch, sh.lw, sh.m, sh.nw);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  const KernelRes r = ch == 1 ? query_res<1>(sh) : ch == 3 ? query_res<3>(sh) : query_res<4>(sh);
+  if (r.measured) cache.emplace(key, r);  // estimates (no device) are not cached
+  return r;
+}
+
+}  // namespace
+
+// Latency model of one launch on 256 CUs x 4 SIMDs, in gfx950 cycles.
+//   * VALU instructions per wave: steps x per-step row work + load/pack/store
+//     (matches SQ_INSTS_VALU within ~10 %, profiles/r01/pmc_sq_*).
+//   * A SIMD with k resident waves retires one wave-instruction per
+//     max(k x 2.88, 5.86) / k cycles: 5.86 with one wave (issue latency),
+//     2.88 once two or more overlap (tools/ubench/isa_rates.hip).
+//   * Per step ~550 cycles of LDS exchange + barrier latency, ~570 cycles of
+//     load latency per register row, ~17.8k cycles per launch (dispatch,
+//     first loads, drain).
+//   * Workgroups per CU limited by the kernel's real VGPRs and LDS
+//     (hipFuncGetAttributes) and 32 waves per CU; the busiest CU sets the time.
+// Constants fitted (median error 9 %) to 228 measured launches over 14 shapes,
+// 4 image sizes, grey/RGB and 1-8-way bands (profiles/r01/band_shape_sweep.txt).
 double swar_launch_cycles(SwarShape s, int steps, int ch, int64_t rows, int64_t row_bytes) {
+  constexpr double kCyclesMin = 2.88, kCyclesOneWave = 5.86, kStep = 549.0, kRowLoad = 568.0, kLaunch = 17813.0;
   const int np = s.lw;
   const int hl = (steps * ch + s.lw - 1) / s.lw;
   if (2 * hl >= 64) return 1e300;
@@ -364,18 +432,17 @@ double swar_launch_cycles(SwarShape s, int steps, int ch, int64_t rows, int64_t 
   const int vrows = s.m * s.nw - 2 * steps;
   if (vrows <= 0 || np < ch) return 1e300;
   const double g = static_cast<double>(pairs * ceil_div<int64_t>(rows, vrows));
-  const double stage = (s.m + 2) * (2.0 * np + 2.0 * ch) + s.m * 4.0 * np + 24.0;
-  const double wave_instr = steps * stage + 40.0 + 3.0 * s.m * np;
-  const int vgpr = round_up(s.m * np + 3 * np + 40, 8);
-  const int vgpr_waves = std::min(8, 512 / vgpr);
-  const int lds_wgs = (160 * 1024) / (s.nw * np * 1024);
+  const KernelRes res = kernel_res(s, ch);
+  const int vgpr_waves = std::max(1, std::min(8, 512 / round_up(std::max(res.vgpr, 1), 8)));
+  const int lds_wgs = res.lds > 0 ? (160 * 1024) / res.lds : 8;
   const int L = std::max(1, std::min({lds_wgs, vgpr_waves * 4 / s.nw, 32 / s.nw}));
   const double per_cu = std::ceil(g / 256.0);
   const double rounds = std::ceil(per_cu / L);
-  const double conc = std::min<double>(per_cu, L);
-  const double wps = conc * s.nw / 4.0;
-  const double rate = wps >= 3 ? 2.8 : wps >= 2 ? 2.9 : 5.8;
-  return rounds * (std::max(1.0, std::ceil(wps)) * wave_instr * rate + 5500.0);
+  const double k = std::min<double>(per_cu, L) * s.nw / 4.0;  // waves per SIMD
+  const double stage = (s.m + 2) * (2.0 * np + 2.0 * ch) + s.m * 4.0 * np + 24.0;
+  const double instr = steps * stage + 40.0 + 3.0 * s.m * np;
+  const double round_cycles = instr * std::max(k * kCyclesMin, kCyclesOneWave) + steps * kStep + kRowLoad * s.m;
+  return rounds * round_cycles + kLaunch;
 }
 
 SwarShape pick_swar_shape(int steps, int ch, int64_t rows, int64_t row_bytes) {
