@@ -129,7 +129,8 @@ __device__ __forceinline__ void store_bytes(uint8_t* p, const typename Chunk<NP>
 template <int CH, int LW, int M, int NW>
 __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                   int64_t pitch, int64_t dst_pitch, int row_bytes, int r0, int r1,
-                                                  int steps, int g_row0, int height, int nstrips, int pair_stride) {
+                                                  int steps, int g_row0, int height, int nstrips, int pair_stride,
+                                                  int row_tiles, int xcd_swizzle) {
   constexpr int NP = LW;       // pairs per row per lane
   constexpr int NQ = NP / 4;   // uint4 per row per lane
   using CT = typename Chunk<NP>::T;
@@ -138,7 +139,19 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hl = (steps * CH + LW - 1) / LW;  // halo lanes per side
   const int vbytes = (64 - 2 * hl) * LW;      // valid output bytes per strip
-  const int sA = blockIdx.x, sB = blockIdx.x + pair_stride;
+  // 1-D grid of pair_stride x row_tiles workgroups.  The dispatcher deals
+  // consecutive workgroup ids round-robin to the 8 XCDs; with xcd_swizzle the
+  // ids are remapped (bijectively) so that each XCD receives one contiguous
+  // run of tiles, walked down a column strip: vertically adjacent tiles,
+  // which read each other's halo rows, share an L2.
+  int tile = static_cast<int>(blockIdx.x);
+  if (xcd_swizzle) {
+    const int nwg = static_cast<int>(gridDim.x);
+    const int q = nwg >> 3, rem = nwg & 7, xcd = tile & 7, local = tile >> 3;
+    tile = xcd * q + min(xcd, rem) + local;
+  }
+  const int col = tile / row_tiles, rtile = tile - col * row_tiles;
+  const int sA = col, sB = col + pair_stride;
   const bool hasB = sB < nstrips;
   const int baseA = sA * vbytes - hl * LW, baseB = sB * vbytes - hl * LW;
   const int xA = baseA + lane * LW, xB = baseB + lane * LW;
@@ -150,7 +163,7 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
   for (int k = 0; k < NP; ++k) cm[k] = (k < validA ? 0xffffu : 0u) | (k < validB ? 0xffff0000u : 0u);
 
   const int vrows = NW * M - 2 * steps;
-  const int tile_r0 = r0 + static_cast<int>(blockIdx.y) * vrows;
+  const int tile_r0 = r0 + rtile * vrows;
   const int row_base = tile_r0 - steps + w * M;
   const int lo_ok = max(r0 - steps, -g_row0), hi_ok = min(r1 + steps, height - g_row0);
 
@@ -261,6 +274,14 @@ constexpr SwarShape kShapes[] = {
     {4, 2, 16}, {4, 3, 16}, {8, 2, 16}, {8, 4, 16},                     // 16 waves: latency-bound bands
 };
 
+bool xcd_swizzle_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PCONV_XCD_SWIZZLE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int CH, int LW, int M, int NW>
 void launch_one(const StencilLaunch& a, hipStream_t s) {
   const int steps = a.steps;
@@ -270,13 +291,14 @@ void launch_one(const StencilLaunch& a, hipStream_t s) {
   PCONV_CHECK(vbytes > 0 && vrows > 0, "swar temporal kernel: steps too large for the tile");
   const int nstrips = static_cast<int>(ceil_div<int64_t>(a.row_bytes, vbytes));
   const int pair_stride = (nstrips + 1) / 2;
-  const dim3 grid(pair_stride, ceil_div(static_cast<int>(a.r1 - a.r0), vrows));
+  const int row_tiles = ceil_div(static_cast<int>(a.r1 - a.r0), vrows);
+  const dim3 grid(pair_stride * row_tiles);
   const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
   k_swar<CH, LW, M, NW><<<grid, dim3(64 * NW), 0, s>>>(a.src, a.dst, a.pitch, a.dst_pitch ? a.dst_pitch : a.pitch,
                                                        static_cast<int>(a.row_bytes),
                                                        static_cast<int>(a.r0), static_cast<int>(a.r1), steps,
                                                        static_cast<int>(a.g_row0), static_cast<int>(hmax), nstrips,
-                                                       pair_stride);
+                                                       pair_stride, row_tiles, xcd_swizzle_enabled() ? 1 : 0);
 }
 
 template <int CH>
