@@ -17,10 +17,11 @@
 // of the lane's LW-byte chunk in column strip A, B_k the same byte of strip
 // B (two strips of 64*LW bytes per wave).  The horizontal neighbour of P_k at
 // distance CH is P_{k±CH}, or — across the lane boundary — the neighbouring
-// lane's register via DPP wave_shr/wave_shl.  Per pair per step: 2 ops
-// horizontal (v_lshlrev + v_add3), 2 vertical (rolling sum), 2 truncation
-// (v_lshrrev, v_and), all full rate; the byte shuffles (v_perm) happen only
-// when a tile is loaded and stored.
+// lane's register via DPP wave_shr/wave_shl (at 4-byte lanes folded into the
+// add as a DPP source operand).  Per pair per step: 2 ops horizontal
+// (v_lshl_add / v_add3 / v_add_u32_dpp), 2 vertical (rolling sum), 2
+// truncation (v_lshrrev, v_and), all full rate; the byte shuffles (v_perm)
+// happen only when a tile is loaded and stored.
 //
 // Tile: NW waves stacked vertically, wave w keeps rows [w*M, (w+1)*M); each
 // step the waves swap their boundary rows through LDS (double-buffered by step
@@ -56,16 +57,41 @@ __device__ __forceinline__ constexpr u32 pair_sel(int j) {
   return 0x0c000c00u | ((4u + static_cast<u32>(j)) << 16) | static_cast<u32>(j);
 }
 
-// Horizontal [1,2,1] at tap distance CH over NP pairs; lane-crossing taps via DPP.
+// Keeps `v` in a register as computed: stops instruction selection from
+// merging the next add into a 3-input v_add3 (VOP3 cannot take a DPP source
+// on gfx950), so the lane-crossing tap folds into v_add_u32_dpp.
+__device__ __forceinline__ u32 opaque(u32 v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// Horizontal [1,2,1] at tap distance CH over NP pairs; taps in the
+// neighbouring lane come through DPP (wave_shr:1 / wave_shl:1, bound_ctrl: 0
+// past the wave edge).
+//   NP = 4: most taps cross lanes (RGB: 6 of 8 per row), so each one is the
+//     DPP source of its add (v_add_u32_dpp) — 2 VALU ops per pair instead of
+//     up to 4 with separate v_mov_b32_dpp;
+//   NP = 8: few taps cross lanes and the register budget is tight (the big
+//     tiles sit at 2 waves/SIMD); the plain form keeps the compiler free to
+//     schedule (folding costs these tiles ~20 VGPRs = one wave per SIMD).
 template <int CH, int NP>
 __device__ __forceinline__ void horiz(const u32 (&X)[NP], u32 (&H)[NP]) {
   static_assert(CH <= NP, "tap distance must not exceed the pairs per lane");
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
     const int l = k - CH, r = k + CH;
-    const u32 lv = l >= 0 ? X[l] : __builtin_amdgcn_mov_dpp(X[NP + l], 0x138, 0xf, 0xf, true);  // wave_shr:1
-    const u32 rv = r < NP ? X[r] : __builtin_amdgcn_mov_dpp(X[r - NP], 0x130, 0xf, 0xf, true);   // wave_shl:1
-    H[k] = (X[k] << 1) + (lv + rv);
+    if constexpr (NP == 4) {
+      u32 t = X[k] << 1;
+      if (l >= 0) t += X[l];
+      if (r < NP) t += X[r];
+      if (l < 0) t = __builtin_amdgcn_mov_dpp(X[NP + l], 0x138, 0xf, 0xf, true) + opaque(t);
+      if (r >= NP) t = __builtin_amdgcn_mov_dpp(X[r - NP], 0x130, 0xf, 0xf, true) + opaque(t);
+      H[k] = t;
+    } else {
+      const u32 lv = l >= 0 ? X[l] : __builtin_amdgcn_mov_dpp(X[NP + l], 0x138, 0xf, 0xf, true);
+      const u32 rv = r < NP ? X[r] : __builtin_amdgcn_mov_dpp(X[r - NP], 0x130, 0xf, 0xf, true);
+      H[k] = (X[k] << 1) + (lv + rv);
+    }
   }
 }
 
@@ -126,6 +152,69 @@ __device__ __forceinline__ void store_bytes(uint8_t* p, const typename Chunk<NP>
   for (int k = 0; k < n; ++k) p[k] = static_cast<uint8_t>(w[k >> 2] >> (8 * (k & 3)));
 }
 
+// One repetition of a wave's M register rows: swap boundary rows with the
+// neighbouring waves through LDS (double-buffered by `par`, one barrier),
+// horizontal pass per row, rolling vertical sum, truncation, re-zeroing of
+// everything outside the image.
+template <int CH, int NP, int M, int NW>
+__device__ __forceinline__ void swar_step(u32 (&D)[M][NP], uint4 (&lds)[2][NW][2][NP / 4][64], int par, int w,
+                                          int lane, bool needs_mask, const u32 (&cm)[NP], int out_top, int out_bot) {
+  constexpr int NQ = NP / 4;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    lds[par][w][0][q][lane] = make_uint4(D[0][4 * q], D[0][4 * q + 1], D[0][4 * q + 2], D[0][4 * q + 3]);
+    lds[par][w][1][q][lane] = make_uint4(D[M - 1][4 * q], D[M - 1][4 * q + 1], D[M - 1][4 * q + 2], D[M - 1][4 * q + 3]);
+  }
+  __syncthreads();
+  u32 A[NP], B[NP];
+  {
+    const int wa = w > 0 ? w - 1 : 0;       // wave 0: tile top halo, value irrelevant
+    const int wb = w < NW - 1 ? w + 1 : w;  // last wave: tile bottom halo
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint4 av = lds[par][wa][1][q][lane], bv = lds[par][wb][0][q][lane];
+      A[4 * q] = av.x; A[4 * q + 1] = av.y; A[4 * q + 2] = av.z; A[4 * q + 3] = av.w;
+      B[4 * q] = bv.x; B[4 * q + 1] = bv.y; B[4 * q + 2] = bv.z; B[4 * q + 3] = bv.w;
+    }
+  }
+  u32 Hc[NP], Sc[NP];
+  {
+    u32 Ha[NP];
+    horiz<CH, NP>(A, Ha);
+    horiz<CH, NP>(D[0], Hc);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) Sc[k] = Ha[k] + Hc[k];
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    u32 Hn[NP];
+    if (i + 1 < M)
+      horiz<CH, NP>(D[i + 1], Hn);
+    else
+      horiz<CH, NP>(B, Hn);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const u32 Sn = Hc[k] + Hn[k];
+      D[i][k] = ((Sc[k] + Sn) >> 4) & 0x00ff00ffu;  // floor(sum of the 9 taps / 16), both fields
+      Sc[k] = Sn;
+      Hc[k] = Hn[k];
+    }
+  }
+  if (needs_mask) {
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int k = 0; k < NP; ++k) D[i][k] &= cm[k];
+  }
+  if (out_top > 0 || out_bot < M) {
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+      if (i < out_top || i >= out_bot)
+#pragma unroll
+        for (int k = 0; k < NP; ++k) D[i][k] = 0;
+  }
+}
+
 template <int CH, int LW, int M, int NW>
 __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                   int64_t pitch, int64_t dst_pitch, int row_bytes, int r0, int r1,
@@ -181,63 +270,10 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
   const int out_top = min(max(-g_row0 - row_base, 0), M);
   const int out_bot = min(max(height - g_row0 - row_base, 0), M);
 
-  for (int s = 0; s < steps; ++s) {
-    const int par = s & 1;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      lds[par][w][0][q][lane] = make_uint4(D[0][4 * q], D[0][4 * q + 1], D[0][4 * q + 2], D[0][4 * q + 3]);
-      lds[par][w][1][q][lane] =
-          make_uint4(D[M - 1][4 * q], D[M - 1][4 * q + 1], D[M - 1][4 * q + 2], D[M - 1][4 * q + 3]);
-    }
-    __syncthreads();
-    u32 A[NP], B[NP];
-    {
-      const int wa = w > 0 ? w - 1 : 0;        // wave 0: tile top halo, value irrelevant
-      const int wb = w < NW - 1 ? w + 1 : w;   // last wave: tile bottom halo
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const uint4 av = lds[par][wa][1][q][lane], bv = lds[par][wb][0][q][lane];
-        A[4 * q] = av.x; A[4 * q + 1] = av.y; A[4 * q + 2] = av.z; A[4 * q + 3] = av.w;
-        B[4 * q] = bv.x; B[4 * q + 1] = bv.y; B[4 * q + 2] = bv.z; B[4 * q + 3] = bv.w;
-      }
-    }
-    u32 Hc[NP], Sc[NP];
-    {
-      u32 Ha[NP];
-      horiz<CH, NP>(A, Ha);
-      horiz<CH, NP>(D[0], Hc);
-#pragma unroll
-      for (int k = 0; k < NP; ++k) Sc[k] = Ha[k] + Hc[k];
-    }
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      u32 Hn[NP];
-      if (i + 1 < M)
-        horiz<CH, NP>(D[i + 1], Hn);
-      else
-        horiz<CH, NP>(B, Hn);
-#pragma unroll
-      for (int k = 0; k < NP; ++k) {
-        const u32 Sn = Hc[k] + Hn[k];
-        D[i][k] = ((Sc[k] + Sn) >> 4) & 0x00ff00ffu;  // floor(sum/16) in both 16-bit fields
-        Sc[k] = Sn;
-        Hc[k] = Hn[k];
-      }
-    }
-    if (needs_mask) {
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-#pragma unroll
-        for (int k = 0; k < NP; ++k) D[i][k] &= cm[k];
-    }
-    if (out_top > 0 || out_bot < M) {
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-        if (i < out_top || i >= out_bot)
-#pragma unroll
-          for (int k = 0; k < NP; ++k) D[i][k] = 0;
-    }
-  }
+  // (Measured and rejected: steps in pairs keeping 16 x the truncated value
+  // in between — one AND instead of shift + AND every other step — the two
+  // step bodies per iteration cost up to +40 VGPRs and a wave per SIMD.)
+  for (int s = 0; s < steps; ++s) swar_step<CH, NP, M, NW>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
 
   const bool lane_in = lane >= hl && lane < 64 - hl;
   const bool stA = lane_in && validA > 0, stB = lane_in && validB > 0;
@@ -443,7 +479,14 @@ KernelRes kernel_res(SwarShape sh, int ch) {
 //   * Workgroups per CU limited by the kernel's real VGPRs and LDS
 //     (hipFuncGetAttributes) and 32 waves per CU; the busiest CU sets the time.
 // Constants fitted (median error 9 %) to 228 measured launches over 14 shapes,
-// 4 image sizes, grey/RGB and 1-8-way bands (profiles/r01/band_shape_sweep.txt).
+// 4 image sizes, grey/RGB and 1-8-way bands (profiles/r01/band_shape_sweep.txt;
+// tools/fit_swar_data.py + tools/fit_swar_model.py); they pick the measured
+// best shape in 6 of 6 configurations of the current kernel.
+SwarResources swar_resources(SwarShape s, int ch) {
+  const KernelRes r = kernel_res(s, ch);
+  return SwarResources{r.vgpr, r.lds, r.measured};
+}
+
 double swar_launch_cycles(SwarShape s, int steps, int ch, int64_t rows, int64_t row_bytes) {
   constexpr double kCyclesMin = 2.88, kCyclesOneWave = 5.86, kStep = 549.0, kRowLoad = 568.0, kLaunch = 17813.0;
   const int np = s.lw;
@@ -461,7 +504,10 @@ double swar_launch_cycles(SwarShape s, int steps, int ch, int64_t rows, int64_t 
   const double per_cu = std::ceil(g / 256.0);
   const double rounds = std::ceil(per_cu / L);
   const double k = std::min<double>(per_cu, L) * s.nw / 4.0;  // waves per SIMD
-  const double stage = (s.m + 2) * (2.0 * np + 2.0 * ch) + s.m * 4.0 * np + 24.0;
+  // lane-crossing taps per row: separate DPP moves at 8-byte lanes, folded
+  // into the adds at 4-byte lanes (only the pairs with both taps outside cost one)
+  const double cross = np == 4 ? (ch == 1 ? 0.0 : ch == 3 ? 2.0 : 4.0) : 2.0 * ch;
+  const double stage = (s.m + 2) * (2.0 * np + cross) + s.m * 4.0 * np + 24.0;
   const double instr = steps * stage + 40.0 + 3.0 * s.m * np;
   const double round_cycles = instr * std::max(k * kCyclesMin, kCyclesOneWave) + steps * kStep + kRowLoad * s.m;
   return rounds * round_cycles + kLaunch;

@@ -26,5 +26,13 @@ void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
 // Force a tile shape (lw = 0 restores the model) and list the instantiated ones.
 void set_swar_shape(int lw, int m, int nw);
 std::vector<SwarShape> swar_shapes();
+// VGPRs per lane and LDS bytes of one instantiation as the runtime reports
+// them (measured = false: no device, model estimate).
+struct SwarResources {
+  int vgpr = 0;
+  int lds = 0;
+  bool measured = false;
+};
+SwarResources swar_resources(SwarShape s, int ch);
 
 }  // namespace pconv

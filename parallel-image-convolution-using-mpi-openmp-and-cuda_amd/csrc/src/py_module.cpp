@@ -319,6 +319,20 @@ PYBIND11_MODULE(_pconv_native, m) {
                               swar_launch_cycles(s, steps, channel_count(parse_channels(ch)), rows, row_bytes));
       },
       py::arg("steps"), py::arg("channels"), py::arg("rows"), py::arg("row_bytes"));
+  m.def(
+      "swar_model_table",
+      [](int steps, const std::string& ch, int64_t rows, int64_t row_bytes) {
+        // every shape: (lw, m, nw, vgpr, lds, measured, predicted cycles)
+        const int c = channel_count(parse_channels(ch));
+        py::list out;
+        for (const auto& s : swar_shapes()) {
+          const SwarResources r = swar_resources(s, c);
+          out.append(py::make_tuple(s.lw, s.m, s.nw, r.vgpr, r.lds, r.measured,
+                                    swar_launch_cycles(s, steps, c, rows, row_bytes)));
+        }
+        return out;
+      },
+      py::arg("steps"), py::arg("channels"), py::arg("rows"), py::arg("row_bytes"));
   m.def("supports_fusion",
         [](py::object filter, const std::string& v) { return supports_fusion(make_filter(filter), parse_variant(v)); },
         py::arg("filter"), py::arg("variant") = "auto");

@@ -24,10 +24,10 @@ def load(fn,W,H,reps):
         if sh[1]*sh[2]-2*fuse<=0 or 2*((fuse*ch+sh[0]-1)//sh[0])>=64: continue
         out.append(dict(W=W,H=H,ch=ch,rb=W*ch,world=world,reps=reps,fuse=fuse,shape=sh,launches=launches,us=r['us_per_rep'],src=fn.split('/')[-1]))
     return out
+# usage: python tools/fit_swar_data.py W:H:REPS:log [...]   (band_sweep.py outputs)
 D=[]
-D+=load('gpurun_out/bs_rgb.log',1920,2520,40)
-D+=load('gpurun_out/bs_grey.log',1920,2520,40)
-D+=load('gpurun_out/bs_big_grey.log',32768,32768,16)
-D+=load('gpurun_out/bs_8k_rgb.log',8192,8192,16)
+for spec in sys.argv[1:]:
+    W, H, R, fn = spec.split(':', 3)
+    D += load(fn, int(W), int(H), int(R))
 json.dump(D,open('gpurun_out/fit_data.json','w'))
 print(len(D))

@@ -22,7 +22,8 @@ def launch_cycles(p, sh, ch, rb, R, s):
     rounds=math.ceil(per_cu/L)
     conc=min(per_cu,L)
     k=conc*nw/4.0
-    stage=(m+2)*(2*np_+2*ch)+m*4*np_+24
+    e = (0 if ch == 1 else 2 if ch == 3 else 4) if np_ == 4 else 2 * ch  # lane-crossing taps (folded at np 4)
+    stage=(m+2)*(2*np_+e)+m*4*np_+24
     I=s*stage+40+3*m*np_
     rt=I*max(k*c_min,c_lat)+s*b_step+b0+lat_ld*m
     return rounds*rt+fixed
