@@ -47,8 +47,8 @@ METRIC = "Mpixels/sec (and wall-time) for 1920x2520 RGB, 40 reps at 1/2/4/8 MI35
 def parse():
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=30)
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=2520)
     p.add_argument("--channels", default="rgb")
@@ -70,6 +70,8 @@ def parse():
                    help="halo transport (gloo-host: host-staged, lets several ranks share one GPU for rehearsals)")
     p.add_argument("--step-graphs", choices=["auto", "on", "off"], default="auto",
                    help="one hipGraph per image (H2D + reps + D2H) on per-slot streams (auto: when exchange-free)")
+    p.add_argument("--graph-capture", choices=["on", "off"], default="on",
+                   help="slot-stream pipeline: capture each image as a hipGraph (on) or issue directly (off)")
     p.add_argument("--zero-copy-out", choices=["on", "off"], default="off",
                    help="step graphs: the last fused launch stores the result straight into pinned host memory "
                         "(measured slower than the SDMA D2H copy: 0.41 vs 0.32 ms/step at N=1)")
@@ -136,7 +138,7 @@ def main():
                            preload_halo=a.preload_halo, slots=a.slots, variant=a.variant,
                            transport=transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
                            step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
-                           zero_copy_out=a.zero_copy_out == "on")
+                           zero_copy_out=a.zero_copy_out == "on", graph_capture=a.graph_capture == "on")
     blur.load_synthetic(a.seed)
 
     for _ in range(a.warmup):
@@ -207,7 +209,8 @@ def main():
                 "step": "H2D + reps + D2H per image (reference GPU_convolution scope)",
                 "images_in_flight": a.slots,
                 "concurrent_images": bool(blur.pipe.concurrent),
-                "step_graphs": bool(blur.pipe.graphs),
+                "slot_streams": bool(blur.pipe.graphs),
+                "step_graphs": bool(blur.pipe.step_graphs),
                 "zero_copy_out": bool(blur.pipe.graphs) and a.zero_copy_out == "on",
                 "halo_depth": int(blur.engine.halo),
                 "fuse": int(blur.engine.fuse),

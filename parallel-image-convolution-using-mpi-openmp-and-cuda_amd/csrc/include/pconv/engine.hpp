@@ -182,8 +182,12 @@ class BandPipeline {
   // graphs: every image is one hipGraph (H2D + reps + D2H) on its slot's own
   // stream — slots run concurrently, one host call per image; needs
   // exchange-free images (see BandEngine::process_graph).
+  // slot_streams: every image runs on its slot's own stream (H2D, reps, D2H
+  // stream-ordered, no cross-stream events) — slots overlap each other; needs
+  // exchange-free images.  step_graphs: each such image is one cached hipGraph
+  // (one host call), otherwise its copies and launches are issued directly.
   BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt, int slots,
-               int concurrent = -1, bool graphs = false);
+               int concurrent = -1, bool slot_streams = false, bool step_graphs = true);
   ~BandPipeline();
   int slots() const { return static_cast<int>(slots_.size()); }
   BandEngine& slot(int i) { return *slots_.at(i); }
@@ -197,12 +201,14 @@ class BandPipeline {
   // True when slots run their repetitions on separate compute streams.
   bool concurrent() const { return concurrent_; }
   bool graphs() const { return graphs_; }
+  bool step_graphs() const { return graphs_ && step_graphs_; }
 
  private:
   Stream h2d_, d2h_, comm_;
   std::vector<Stream> computes_;
   bool concurrent_ = false;
-  bool graphs_ = false;
+  bool graphs_ = false;  // slot-stream mode
+  bool step_graphs_ = true;
   std::vector<std::unique_ptr<BandEngine>> slots_;
   std::vector<Event> ev_up_, ev_done_, ev_free_, ev_halo_;
   std::vector<bool> used_;

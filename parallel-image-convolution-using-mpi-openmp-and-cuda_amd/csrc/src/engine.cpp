@@ -292,13 +292,14 @@ void BandEngine::synchronize() {
 // --------------------------------------------------------------- BandPipeline
 
 BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt,
-                           int slots, int concurrent, bool graphs) {
+                           int slots, int concurrent, bool graphs, bool step_graphs) {
   PCONV_CHECK(slots >= 1 && slots <= 8, "pipeline slots must be in [1, 8]");
   set_device(opt.device);
   if (graphs) {
     // One stream per slot carries that slot's whole image (H2D, reps, D2H) as
     // one graph: slots overlap each other without cross-stream events.
     graphs_ = true;
+    step_graphs_ = step_graphs;
     concurrent_ = slots > 1;
     EngineOptions o = opt;
     o.use_graph = false;
@@ -360,6 +361,17 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   TraceRange tr("pconv.pipeline.submit");
   const int k = static_cast<int>(count_ % static_cast<int64_t>(slots_.size()));
   BandEngine& e = *slots_[k];
+  if (graphs_ && !step_graphs_) {
+    const bool preloaded = in_r0 < 0 || in_r1 > e.band().rows;
+    PCONV_CHECK(e.exchange_free(reps, preloaded), "slot-stream pipeline: this image needs halo exchanges");
+    e.upload_rows(host_in, e.layout().row_bytes, in_r0, in_r1);
+    e.set_halo_valid(preloaded);
+    e.run(reps);
+    e.download_rows(host_out, e.layout().row_bytes, 0, e.band().rows);
+    used_[k] = true;
+    ++count_;
+    return;
+  }
   if (graphs_) {
     e.process_graph(host_in, in_r0, in_r1, host_out, reps);
     used_[k] = true;

@@ -465,7 +465,7 @@ PYBIND11_MODULE(_pconv_native, m) {
   py::class_<BandPipeline>(m, "BandPipeline")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
-                       int concurrent, bool graphs, bool zero_copy_out) {
+                       int concurrent, bool graphs, bool zero_copy_out, bool step_graphs) {
              EngineOptions o;
              o.zero_copy_out = zero_copy_out;
              o.device = device;
@@ -475,12 +475,12 @@ PYBIND11_MODULE(_pconv_native, m) {
              o.variant = parse_variant(variant);
              const ImageGeom g = make_geom(w, h, ch);
              return std::make_unique<BandPipeline>(g, row_band(h, world, rank), make_filter(filter), o, slots,
-                                                   concurrent, graphs);
+                                                   concurrent, graphs, step_graphs);
            }),
            py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
            py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
            py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1,
-           py::arg("graphs") = false, py::arg("zero_copy_out") = false)
+           py::arg("graphs") = false, py::arg("zero_copy_out") = false, py::arg("step_graphs") = true)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -499,7 +499,8 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def("drain", &BandPipeline::drain, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("submitted", &BandPipeline::submitted)
       .def_property_readonly("concurrent", &BandPipeline::concurrent)
-      .def_property_readonly("graphs", &BandPipeline::graphs);
+      .def_property_readonly("graphs", &BandPipeline::graphs)
+      .def_property_readonly("step_graphs", &BandPipeline::step_graphs);
 
   py::class_<LocalCluster>(m, "LocalCluster")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int bands, int device, int halo,

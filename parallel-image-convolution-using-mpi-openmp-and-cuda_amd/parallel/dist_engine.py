@@ -42,7 +42,7 @@ class DistributedBlur:
                  device: Optional[int] = None, halo: Optional[int] = None, fuse: Optional[int] = None,
                  overlap: bool = True, preload_halo: bool = False, comm=None, slots: int = 2,
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
-                 step_graphs: Optional[bool] = None, zero_copy_out: bool = False):
+                 step_graphs: Optional[bool] = None, zero_copy_out: bool = False, graph_capture: bool = True):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -67,7 +67,8 @@ class DistributedBlur:
         if (free if step_graphs is None else bool(step_graphs)):
             del self.pipe
             self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
-                                       graphs=True, zero_copy_out=bool(zero_copy_out), **kw)
+                                       graphs=True, zero_copy_out=bool(zero_copy_out),
+                                       step_graphs=bool(graph_capture), **kw)
         self.engine = self.pipe.slot(0)
         self.band = self.engine.band
         self.row_bytes = self.engine.row_bytes
