@@ -38,6 +38,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -310,12 +311,16 @@ constexpr SwarShape kShapes[] = {
     {4, 2, 16}, {4, 3, 16}, {8, 2, 16}, {8, 4, 16},                     // 16 waves: latency-bound bands
 };
 
+std::atomic<int> g_xcd_swizzle{-1};  // -1: from PCONV_XCD_SWIZZLE on first use (default on)
+
 bool xcd_swizzle_enabled() {
-  static const bool on = [] {
+  int v = g_xcd_swizzle.load(std::memory_order_relaxed);
+  if (v < 0) {
     const char* e = std::getenv("PCONV_XCD_SWIZZLE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+    v = (e && e[0] == '0') ? 0 : 1;
+    g_xcd_swizzle.store(v, std::memory_order_relaxed);
+  }
+  return v != 0;
 }
 
 template <int CH, int LW, int M, int NW>
@@ -482,6 +487,8 @@ KernelRes kernel_res(SwarShape sh, int ch) {
 // 4 image sizes, grey/RGB and 1-8-way bands (profiles/r01/band_shape_sweep.txt;
 // tools/fit_swar_data.py + tools/fit_swar_model.py); they pick the measured
 // best shape in 6 of 6 configurations of the current kernel.
+void set_xcd_swizzle(bool on) { g_xcd_swizzle.store(on ? 1 : 0, std::memory_order_relaxed); }
+
 SwarResources swar_resources(SwarShape s, int ch) {
   const KernelRes r = kernel_res(s, ch);
   return SwarResources{r.vgpr, r.lds, r.measured};

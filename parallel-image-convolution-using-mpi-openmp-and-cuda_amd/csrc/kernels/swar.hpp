@@ -34,5 +34,7 @@ struct SwarResources {
   bool measured = false;
 };
 SwarResources swar_resources(SwarShape s, int ch);
+// XCD-aware tile order of the SWAR kernel (default on; PCONV_XCD_SWIZZLE=0).
+void set_xcd_swizzle(bool on);
 
 }  // namespace pconv

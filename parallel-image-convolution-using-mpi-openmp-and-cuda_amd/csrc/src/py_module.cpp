@@ -319,6 +319,8 @@ PYBIND11_MODULE(_pconv_native, m) {
                               swar_launch_cycles(s, steps, channel_count(parse_channels(ch)), rows, row_bytes));
       },
       py::arg("steps"), py::arg("channels"), py::arg("rows"), py::arg("row_bytes"));
+  m.def("set_xcd_swizzle", &set_xcd_swizzle, py::arg("on"),
+        "XCD-aware (bijective, per-XCD contiguous) tile order of the SWAR kernel.");
   m.def(
       "swar_model_table",
       [](int steps, const std::string& ch, int64_t rows, int64_t row_bytes) {

@@ -175,3 +175,40 @@ def test_pipeline_zero_copy_out(pconv_mod, rng, w, h, ch, reps, fuse):
         ref = pconv_mod.numpy_convolve(img if c > 1 else img[..., 0], reps).reshape(h, -1)
         for k in ks:
             assert np.array_equal(blur.outputs[k].reshape(h, -1), ref), (rnd, k)
+
+
+@pytest.mark.parametrize("capture", [True, False])
+def test_pipeline_slot_streams_direct_and_graph(pconv_mod, rng, capture):
+    """Slot-stream pipeline with and without whole-step graph capture."""
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    w, h, reps = 71, 52, 10
+    blur = DistributedBlur(w, h, "rgb", "gaussian", reps, rank=0, world=1, device=0, slots=3, step_graphs=True,
+                           graph_capture=capture)
+    assert blur.pipe.graphs and blur.pipe.step_graphs == capture
+    imgs = [rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for _ in range(3)]
+    ks = []
+    for img in imgs:
+        blur.load_image(img, slot=blur._next)
+        ks.append(blur.submit(reps))
+    blur.drain()
+    for img, k in zip(imgs, ks):
+        assert np.array_equal(blur.outputs[k].reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps))
+
+
+def test_xcd_swizzle_off_and_model_table(pconv_mod, native, rng):
+    """Tile order without the XCD remap gives the same bytes; the shape model
+    sees the runtime's real VGPR / LDS numbers for every instantiation."""
+    img = rng.integers(0, 256, size=(300, 257, 3), dtype=np.uint8)
+    ref = pconv_mod.numpy_convolve(img, 9)
+    try:
+        native.set_xcd_swizzle(False)
+        out_off = pconv_mod.convolve(img, 9, backend="hip", fuse=8)
+    finally:
+        native.set_xcd_swizzle(True)
+    out_on = pconv_mod.convolve(img, 9, backend="hip", fuse=8)
+    assert np.array_equal(out_off, ref) and np.array_equal(out_on, ref)
+    table = native.swar_model_table(8, "rgb", 2520, 5760)
+    assert len(table) == len(native.swar_shapes())
+    for lw, m, nw, vgpr, lds, measured, cycles in table:
+        assert measured and 0 < vgpr <= 512 and lds >= 16384 and cycles > 0
