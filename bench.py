@@ -78,6 +78,11 @@ def parse():
     p.add_argument("--emulate", default=None, metavar="WORLD:RANK",
                    help="time ONE rank of a WORLD-way split on this GPU (pre-loaded halos, no peers): a "
                         "single-GPU proxy of the per-rank step; reported as emulated, never as the headline")
+    p.add_argument("--exchange-check", choices=["auto", "on", "off"], default="auto",
+                   help="N>1: after the headline timing, also time the RCCL halo-exchange pipeline (ghost rows "
+                        "moved GPU-to-GPU, one communicator per image slot) and compare its bytes with the "
+                        "headline result; reported under 'halo_exchange' (auto: on for N>1)")
+    p.add_argument("--exchange-timeout", type=float, default=60.0, help="seconds before the exchange check aborts")
     p.add_argument("--check", action="store_true",
                    help="after timing, verify every rank's band against the CPU oracle (not timed)")
     return p.parse_args()
@@ -102,6 +107,43 @@ def check_bands(blur, a) -> int:
     out = blur.step(a.reps)
     bad = int(np.count_nonzero(out != ref[b.y0:b.y0 + b.rows]))
     return int(sum_over_ranks(bad))
+
+
+def exchange_check(a, blur, world, rank, device, transport):
+    """Secondary measurement for N>1: the same images with halo rows exchanged
+    GPU-to-GPU (RCCL over xGMI, one communicator per slot) instead of
+    pre-loaded.  Bounded by timeouts; returns a dict for the JSON line."""
+    import numpy as np
+
+    from pconv.parallel.bootstrap import barrier, max_over_ranks, sum_over_ranks
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    res = {"transport": transport, "status": "ok"}
+    try:
+        xb = DistributedBlur(a.width, a.height, a.channels, a.filter, a.reps, rank=rank, world=world, device=device,
+                             halo=a.halo, fuse=a.fuse, preload_halo=False, slots=a.slots, variant=a.variant,
+                             transport=transport, slot_exchange=True)
+        xb.load_synthetic(a.seed)
+        for _ in range(min(a.warmup, 5) + a.slots):
+            xb.submit(a.reps)
+        xb.drain(timeout_s=a.exchange_timeout)
+        k2 = min(a.steps, 100)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(k2):
+            xb.submit(a.reps)
+        xb.drain(timeout_s=a.exchange_timeout)
+        elapsed = max_over_ranks(time.perf_counter() - t0)
+        got = xb.step(a.reps).copy()
+        ref = blur.step(a.reps)
+        bad = sum_over_ranks(int(np.count_nonzero(got != ref)))
+        px = a.width * a.height * a.reps
+        res.update(steps=k2, ms_per_step=round(elapsed / k2 * 1e3, 4), value=round(px * k2 / elapsed / 1e6, 2),
+                   mismatches_vs_headline=int(bad), exchanges_per_step=int(xb.stats.exchanges),
+                   halo_depth=int(xb.engine.halo))
+    except Exception as e:  # reported, never fatal for the headline line
+        res["status"] = f"error: {type(e).__name__}: {e}"[:400]
+    return res
 
 
 def main():
@@ -183,6 +225,10 @@ def main():
     barrier()
     loop_elapsed = max_over_ranks(time.perf_counter() - t1)
 
+    halo_exchange = None
+    if world > 1 and not a.emulate and (a.exchange_check == "on" or (a.exchange_check == "auto" and world > 1)):
+        halo_exchange = exchange_check(a, blur, world, rank, device, transport)
+
     px = a.width * a.height * a.reps
     value = px * a.steps / elapsed / 1e6
     loop_value = px * ls / loop_elapsed / 1e6 if ls else None
@@ -228,6 +274,8 @@ def main():
         }
         if mismatches is not None:
             out["mismatches"] = mismatches
+        if halo_exchange is not None:
+            out["halo_exchange"] = halo_exchange
         if a.emulate:
             out["emulated"] = f"rank {rank} of a {a.emulate.split(':')[0]}-way split on one GPU; value = this " \
                               "rank's step rate x full-image pixels (proxy, not a multi-GPU measurement)"

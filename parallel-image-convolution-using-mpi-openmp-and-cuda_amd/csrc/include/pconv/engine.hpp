@@ -192,6 +192,10 @@ class BandPipeline {
   int slots() const { return static_cast<int>(slots_.size()); }
   BandEngine& slot(int i) { return *slots_.at(i); }
   void set_transport(std::shared_ptr<HaloTransport> t);
+  // Slot-stream mode: slot k exchanges its halos through its own transport
+  // (e.g. one RCCL communicator per slot, so each communicator's operations
+  // stay in one stream's order on every rank).
+  void set_slot_transport(int k, std::shared_ptr<HaloTransport> t);
   // Enqueue one image: host_in holds frame rows [in_r0, in_r1) (ghost rows
   // allowed), host_out receives the owned rows.  Host buffers must be pinned
   // and must stay untouched until drain() (or until S later submits).

@@ -147,13 +147,16 @@ void BandEngine::enqueue_phase(const Phase& p) {
   if (p.exchange_depth > 0) {
     PCONV_CHECK(transport_ != nullptr, "band has neighbours but no halo transport is attached");
     hipStream_t ms = comm_stream();
-    ev_ready_.record(cs_);
-    ev_ready_.wait_on(ms);
+    const bool split = ms != cs_;  // one stream: stream order is the dependency
+    if (split) {
+      ev_ready_.record(cs_);
+      ev_ready_.wait_on(ms);
+    }
     transport_->exchange(*this, p.exchange_depth, ms);
-    ev_halo_.record(ms);
+    if (split) ev_halo_.record(ms);
     for (const auto& l : p.launches)
       if (!l.after_halo) launch(l, cs_);
-    ev_halo_.wait_on(cs_);
+    if (split) ev_halo_.wait_on(cs_);
     for (const auto& l : p.launches)
       if (l.after_halo) launch(l, cs_);
     ++stats_.exchanges;
@@ -304,6 +307,7 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
     EngineOptions o = opt;
     o.use_graph = false;
     o.timing = false;
+    o.overlap = false;  // an image's exchange and launches share its stream: no split launches
     for (int i = 0; i < slots; ++i) {
       computes_.push_back(Stream::create(0));
       o.compute_stream = computes_.back().get();
@@ -353,6 +357,11 @@ BandPipeline::~BandPipeline() {
   if (comm_.get()) (void)hipStreamSynchronize(comm_.get());
 }
 
+void BandPipeline::set_slot_transport(int k, std::shared_ptr<HaloTransport> t) {
+  PCONV_CHECK(graphs_, "per-slot transports need the slot-stream pipeline");
+  slots_.at(k)->set_transport(std::move(t));
+}
+
 void BandPipeline::set_transport(std::shared_ptr<HaloTransport> t) {
   for (auto& s : slots_) s->set_transport(t);
 }
@@ -362,8 +371,10 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   const int k = static_cast<int>(count_ % static_cast<int64_t>(slots_.size()));
   BandEngine& e = *slots_[k];
   if (graphs_ && !step_graphs_) {
+    // Everything of this image on the slot's stream; halo exchanges (if the
+    // ghost rows are not pre-loaded) through this slot's own transport, in
+    // stream order between the upload and the launches.
     const bool preloaded = in_r0 < 0 || in_r1 > e.band().rows;
-    PCONV_CHECK(e.exchange_free(reps, preloaded), "slot-stream pipeline: this image needs halo exchanges");
     e.upload_rows(host_in, e.layout().row_bytes, in_r0, in_r1);
     e.set_halo_valid(preloaded);
     e.run(reps);

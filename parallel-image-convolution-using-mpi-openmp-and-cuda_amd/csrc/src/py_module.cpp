@@ -491,6 +491,13 @@ PYBIND11_MODULE(_pconv_native, m) {
            })
       .def("attach_transport", [](BandPipeline& p, std::shared_ptr<HaloTransport> t) { p.set_transport(std::move(t)); },
            py::keep_alive<1, 2>())
+      .def("attach_slot_rccl",
+           [](BandPipeline& p, int k, std::shared_ptr<RcclComm> c) {
+             p.set_slot_transport(k, std::make_shared<RcclTransport>(std::move(c)));
+           })
+      .def("attach_slot_transport",
+           [](BandPipeline& p, int k, std::shared_ptr<HaloTransport> t) { p.set_slot_transport(k, std::move(t)); },
+           py::keep_alive<1, 3>())
       .def(
           "submit",
           [](BandPipeline& p, uintptr_t in_ptr, int64_t in_r0, int64_t in_r1, uintptr_t out_ptr, int reps) {
@@ -545,7 +552,12 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_property_readonly("world", &RcclComm::world)
       .def("allreduce_max", &RcclComm::allreduce_max, py::call_guard<py::gil_scoped_release>())
       .def("allreduce_sum", &RcclComm::allreduce_sum, py::call_guard<py::gil_scoped_release>())
-      .def("barrier", &RcclComm::barrier, py::call_guard<py::gil_scoped_release>());
+      .def("barrier", &RcclComm::barrier, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "wait",
+          [](RcclComm& c, uintptr_t stream, double timeout_s) { c.wait(reinterpret_cast<hipStream_t>(stream), timeout_s); },
+          py::arg("stream"), py::arg("timeout_s"), py::call_guard<py::gil_scoped_release>(),
+          "Wait for a stream while polling RCCL async errors; aborts the communicator and raises on timeout.");
 
   m.def("set_error_rank", &set_error_rank);
 }

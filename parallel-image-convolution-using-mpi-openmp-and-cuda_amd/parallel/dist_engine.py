@@ -42,7 +42,8 @@ class DistributedBlur:
                  device: Optional[int] = None, halo: Optional[int] = None, fuse: Optional[int] = None,
                  overlap: bool = True, preload_halo: bool = False, comm=None, slots: int = 2,
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
-                 step_graphs: Optional[bool] = None, zero_copy_out: bool = False, graph_capture: bool = True):
+                 step_graphs: Optional[bool] = None, zero_copy_out: bool = False, graph_capture: bool = True,
+                 slot_exchange: bool = False):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -62,9 +63,16 @@ class DistributedBlur:
         # streams) whenever the images need no halo exchange: one band, or
         # ghost rows pre-loaded deep enough for all `reps`.
         free = reps is not None and self.pipe.slot(0).exchange_free(int(reps), self.preload_halo)
-        if step_graphs and not free:
+        if step_graphs and not free and not slot_exchange:
             raise ValueError("step_graphs needs exchange-free images (world 1, or preload_halo with halo >= reps)")
-        if (free if step_graphs is None else bool(step_graphs)):
+        # slot_exchange: images that DO exchange halos, each on its slot's own
+        # stream with its own transport (one RCCL communicator per slot), the
+        # exchange in stream order between upload and launches — slots overlap
+        # each other instead of the exchange overlapping its own image.
+        self.slot_exchange = bool(slot_exchange) and self.world > 1
+        if self.slot_exchange:
+            graph_capture = False
+        if self.slot_exchange or (free if step_graphs is None else bool(step_graphs)):
             del self.pipe
             self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
                                        graphs=True, zero_copy_out=bool(zero_copy_out),
@@ -87,7 +95,24 @@ class DistributedBlur:
         self._next = 0
         self.comm = None
         self.transport = None
-        if self.world > 1 and transport != "none":  # "none": exchange-free images only
+        self.slot_comms = []
+        self.slot_transports = []
+        if self.slot_exchange:
+            for k in range(self.slots):
+                if transport == "rccl":
+                    c = make_rccl_comm(self.device)
+                    self.slot_comms.append(c)
+                    self.pipe.attach_slot_rccl(k, c)
+                elif transport == "gloo-host":
+                    from .transports import GlooHostTransport
+
+                    t = GlooHostTransport()
+                    self.slot_transports.append(t)
+                    self.pipe.attach_slot_transport(k, t)
+                else:
+                    raise ValueError(f"slot_exchange needs transport rccl or gloo-host, not {transport!r}")
+            self.comm = self.slot_comms[0] if self.slot_comms else None
+        elif self.world > 1 and transport != "none":  # "none": exchange-free images only
             if transport == "rccl":
                 self.comm = comm if comm is not None else make_rccl_comm(self.device)
                 self.pipe.attach_rccl(self.comm)
@@ -134,7 +159,13 @@ class DistributedBlur:
         self._next = (k + 1) % self.slots
         return k
 
-    def drain(self) -> None:
+    def drain(self, timeout_s: Optional[float] = None) -> None:
+        """Wait for every submitted image.  With per-slot RCCL communicators
+        and a timeout, each slot's stream is polled for RCCL asynchronous
+        errors and the communicator aborted (raising) if it does not finish."""
+        if timeout_s is not None and self.slot_comms:
+            for k, c in enumerate(self.slot_comms):
+                c.wait(self.pipe.slot(k).compute_stream, float(timeout_s))
         self.pipe.drain()
 
     def step(self, reps: int) -> np.ndarray:

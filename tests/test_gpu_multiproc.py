@@ -90,6 +90,9 @@ def test_bench_torchrun_rehearsal(world, extra):
     meta = json.loads(lines[0])
     assert meta["n_gpus"] == world and meta["mismatches"] == 0
     assert meta["value"] > 0 and meta["config"]["parallelism"] == f"rowband{world}"
+    hx = meta["halo_exchange"]  # secondary run: ghost rows exchanged, one transport per slot
+    assert hx["status"] == "ok", hx
+    assert hx["mismatches_vs_headline"] == 0 and hx["exchanges_per_step"] >= 1
 
 
 @pytest.mark.parametrize("world,extra", [(2, []), (3, ["--exchange-halo", "--halo", "3", "--fuse", "3"]),
@@ -114,3 +117,48 @@ def test_torchrun_per_rank_program_hip(pconv_mod, tmp_path, world, extra):
     filt = extra[extra.index("--filter") + 1] if "--filter" in extra else "gaussian"
     out = pconv_mod.read_raw(str(tmp_path / "blur_pic.raw"), 47, 61, "rgb")
     assert np.array_equal(out, pconv_mod.numpy_convolve(img, 11, filt))
+
+
+def _slot_exchange_worker(rank, world, port, w, h, reps, halo, fuse, slots, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    from pconv.parallel.bootstrap import init_distributed, shutdown
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    ctx = init_distributed("gloo")
+    try:
+        blur = DistributedBlur(w, h, "rgb", "gaussian", reps, rank=rank, world=world, device=0, halo=halo, fuse=fuse,
+                               slots=slots, transport="gloo-host", slot_exchange=True)
+        assert blur.pipe.graphs and not blur.pipe.step_graphs
+        blur.load_synthetic(5)
+        ks = [blur.submit(reps) for _ in range(slots + 2)]
+        blur.drain()
+        q.put((rank, blur.band.y0, [blur.outputs[k].copy() for k in ks[-slots:]]))
+    finally:
+        shutdown(ctx)
+
+
+@pytest.mark.parametrize("world,halo,fuse,reps,slots", [(2, 4, 4, 13, 2), (3, 6, 3, 19, 3), (4, 8, 8, 8, 2)])
+def test_slot_exchange_pipeline_one_gpu(pconv_mod, world, halo, fuse, reps, slots):
+    """Slot-stream pipeline that exchanges halos (one transport per slot, the
+    exchange in stream order): every image of every band bit-exact."""
+    w, h = 59, 83
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slot_exchange_worker, args=(r, world, port, w, h, reps, halo, fuse, slots, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    img = pconv_mod.synthetic_image(w, h, "rgb", seed=5)
+    ref = pconv_mod.numpy_convolve(img, reps).reshape(h, -1)
+    for rank, y0, outs in res:
+        for o in outs:
+            assert np.array_equal(o, ref[y0:y0 + o.shape[0]]), rank
