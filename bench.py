@@ -19,6 +19,11 @@ each rank uploads only its band and downloads only its band.  Ghost rows:
   --halo-mode exchange: ghost rows move GPU-to-GPU with RCCL ncclSend/Recv
       over xGMI on a communication stream, overlapped with interior compute
       (event-ordered streams; the reference's MPI_Isend/Irecv loop).
+For N>1 the JSON line also carries "halo_exchange": the same images re-run
+with ghost rows exchanged GPU-to-GPU (RCCL, one communicator per image slot,
+each image's exchange in its slot stream's order), its ms/step and its byte
+comparison with the headline result — measured after the headline's timed
+region, bounded by --exchange-timeout, never fatal for the headline line.
 Measured on one GPU (tools: --emulate), preload is the faster per-rank step:
 the 40-row ghost zone costs ~25% more H2D at N=8, the exchange path costs
 more host API calls and RCCL latency per image.  The RCCL communicator is
