@@ -62,6 +62,10 @@ constexpr int kMaxFusedSteps = 16;
 // frame before launching (no out-of-frame access is possible).
 void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream,
                     KernelVariant v = KernelVariant::Auto);
+// Settle per-launch choices (SWAR tile-shape tuning) for a launch that will be
+// enqueued later — e.g. inside a graph capture, where nothing may be timed.
+void prepare_stencil(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream,
+                     KernelVariant v = KernelVariant::Auto);
 
 // Whether `v` (or Auto) can fuse `steps` > 1 for this filter.
 bool supports_fusion(const Filter& f, KernelVariant v);

@@ -465,6 +465,16 @@ bool supports_fusion(const Filter& f, KernelVariant v) {
 }
 
 
+void prepare_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hipStream_t stream, KernelVariant v) {
+  StencilLaunch a = a_in;
+  a.r0 = std::max(a.r0, -a.g_row0);
+  a.r1 = std::min(a.r1, a.height - a.g_row0);
+  if (a.r1 <= a.r0) return;
+  const bool own_dst_pitch = a.dst_pitch != 0 && a.dst_pitch != a.pitch;
+  if (v == KernelVariant::Auto && f.binomial121 && (a.steps > 1 || own_dst_pitch)) v = KernelVariant::Temporal;
+  if (v == KernelVariant::Temporal && f.binomial121 && a.steps <= kMaxFusedSteps) prepare_swar(a, ch, stream);
+}
+
 void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hipStream_t stream, KernelVariant v) {
   // Rows outside the global image stay zero: clip the output region to it.
   StencilLaunch a = a_in;

@@ -216,7 +216,83 @@ __device__ __forceinline__ void swar_step(u32 (&D)[M][NP], uint4 (&lds)[2][NW][2
   }
 }
 
-template <int CH, int LW, int M, int NW>
+// Interior-first variant: the wave publishes its boundary rows, computes its
+// interior rows 1..M-2 (they need only its own registers) while the other
+// waves catch up, and only then meets them at the barrier to finish rows 0
+// and M-1 with the neighbours' rows — the LDS round trip and the barrier wait
+// hide behind M-2 rows of arithmetic.
+template <int CH, int NP, int M, int NW>
+__device__ __forceinline__ void swar_step_if(u32 (&D)[M][NP], uint4 (&lds)[2][NW][2][NP / 4][64], int par, int w,
+                                             int lane, bool needs_mask, const u32 (&cm)[NP], int out_top,
+                                             int out_bot) {
+  static_assert(M >= 2, "interior-first step needs two register rows per wave");
+  constexpr int NQ = NP / 4;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    lds[par][w][0][q][lane] = make_uint4(D[0][4 * q], D[0][4 * q + 1], D[0][4 * q + 2], D[0][4 * q + 3]);
+    lds[par][w][1][q][lane] = make_uint4(D[M - 1][4 * q], D[M - 1][4 * q + 1], D[M - 1][4 * q + 2], D[M - 1][4 * q + 3]);
+  }
+  u32 H0[NP], H1[NP], Hp[NP], Hc[NP];
+  horiz<CH, NP>(D[0], H0);
+  horiz<CH, NP>(D[1], H1);
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    Hp[k] = H0[k];
+    Hc[k] = H1[k];
+  }
+  u32 Sc[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) Sc[k] = Hp[k] + Hc[k];
+#pragma unroll
+  for (int i = 1; i + 1 < M; ++i) {
+    u32 Hn[NP];
+    horiz<CH, NP>(D[i + 1], Hn);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const u32 Sn = Hc[k] + Hn[k];
+      D[i][k] = ((Sc[k] + Sn) >> 4) & 0x00ff00ffu;
+      Sc[k] = Sn;
+      Hp[k] = Hc[k];
+      Hc[k] = Hn[k];
+    }
+  }
+  // Hp = H[M-2], Hc = H[M-1] (old rows); H0, H1 = H[0], H[1].
+  __syncthreads();
+  {
+    const int wa = w > 0 ? w - 1 : 0;       // wave 0: tile top halo, value irrelevant
+    const int wb = w < NW - 1 ? w + 1 : w;  // last wave: tile bottom halo
+    u32 A[NP], B[NP];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint4 av = lds[par][wa][1][q][lane], bv = lds[par][wb][0][q][lane];
+      A[4 * q] = av.x; A[4 * q + 1] = av.y; A[4 * q + 2] = av.z; A[4 * q + 3] = av.w;
+      B[4 * q] = bv.x; B[4 * q + 1] = bv.y; B[4 * q + 2] = bv.z; B[4 * q + 3] = bv.w;
+    }
+    u32 Ha[NP], Hb[NP];
+    horiz<CH, NP>(A, Ha);
+    horiz<CH, NP>(B, Hb);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      D[0][k] = (((Ha[k] + H0[k]) + (H0[k] + H1[k])) >> 4) & 0x00ff00ffu;
+      D[M - 1][k] = (((Hp[k] + Hc[k]) + (Hc[k] + Hb[k])) >> 4) & 0x00ff00ffu;
+    }
+  }
+  if (needs_mask) {
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int k = 0; k < NP; ++k) D[i][k] &= cm[k];
+  }
+  if (out_top > 0 || out_bot < M) {
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+      if (i < out_top || i >= out_bot)
+#pragma unroll
+        for (int k = 0; k < NP; ++k) D[i][k] = 0;
+  }
+}
+
+template <int CH, int LW, int M, int NW, bool IF>
 __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                   int64_t pitch, int64_t dst_pitch, int row_bytes, int r0, int r1,
                                                   int steps, int g_row0, int height, int nstrips, int pair_stride,
@@ -274,7 +350,12 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
   // (Measured and rejected: steps in pairs keeping 16 x the truncated value
   // in between — one AND instead of shift + AND every other step — the two
   // step bodies per iteration cost up to +40 VGPRs and a wave per SIMD.)
-  for (int s = 0; s < steps; ++s) swar_step<CH, NP, M, NW>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
+  for (int s = 0; s < steps; ++s) {
+    if constexpr (IF)
+      swar_step_if<CH, NP, M, NW>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
+    else
+      swar_step<CH, NP, M, NW>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
+  }
 
   const bool lane_in = lane >= hl && lane < 64 - hl;
   const bool stA = lane_in && validA > 0, stB = lane_in && validB > 0;
@@ -323,6 +404,18 @@ bool xcd_swizzle_enabled() {
   return v != 0;
 }
 
+std::atomic<int> g_interior_first{-1};  // -1: PCONV_INTERIOR_FIRST on first use (default on)
+
+bool interior_first_enabled() {
+  int v = g_interior_first.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = std::getenv("PCONV_INTERIOR_FIRST");
+    v = (e && e[0] == '0') ? 0 : 1;
+    g_interior_first.store(v, std::memory_order_relaxed);
+  }
+  return v != 0;
+}
+
 template <int CH, int LW, int M, int NW>
 void launch_one(const StencilLaunch& a, hipStream_t s) {
   const int steps = a.steps;
@@ -335,7 +428,14 @@ void launch_one(const StencilLaunch& a, hipStream_t s) {
   const int row_tiles = ceil_div(static_cast<int>(a.r1 - a.r0), vrows);
   const dim3 grid(pair_stride * row_tiles);
   const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
-  k_swar<CH, LW, M, NW><<<grid, dim3(64 * NW), 0, s>>>(a.src, a.dst, a.pitch, a.dst_pitch ? a.dst_pitch : a.pitch,
+  if (interior_first_enabled())
+    k_swar<CH, LW, M, NW, true><<<grid, dim3(64 * NW), 0, s>>>(a.src, a.dst, a.pitch, a.dst_pitch ? a.dst_pitch : a.pitch,
+                                                       static_cast<int>(a.row_bytes),
+                                                       static_cast<int>(a.r0), static_cast<int>(a.r1), steps,
+                                                       static_cast<int>(a.g_row0), static_cast<int>(hmax), nstrips,
+                                                       pair_stride, row_tiles, xcd_swizzle_enabled() ? 1 : 0);
+  else
+    k_swar<CH, LW, M, NW, false><<<grid, dim3(64 * NW), 0, s>>>(a.src, a.dst, a.pitch, a.dst_pitch ? a.dst_pitch : a.pitch,
                                                        static_cast<int>(a.row_bytes),
                                                        static_cast<int>(a.r0), static_cast<int>(a.r1), steps,
                                                        static_cast<int>(a.g_row0), static_cast<int>(hmax), nstrips,
@@ -429,7 +529,9 @@ KernelRes query_res(SwarShape sh) {
   hipError_t e = hipErrorInvalidValue;
 #define PCONV_SWAR(LW_, M_, NW_)                                                                     \
   if (sh.lw == LW_ && sh.m == M_ && sh.nw == NW_)                                                   \
-    e = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_swar<CH, LW_, M_, NW_>));
+    e = hipFuncGetAttributes(&at, interior_first_enabled()                                          \
+                                      ? reinterpret_cast<const void*>(&k_swar<CH, LW_, M_, NW_, true>)  \
+                                      : reinterpret_cast<const void*>(&k_swar<CH, LW_, M_, NW_, false>));
   PCONV_SWAR(8, 8, 8)
   PCONV_SWAR(8, 8, 4)
   PCONV_SWAR(8, 16, 4)
@@ -460,9 +562,9 @@ KernelRes query_res(SwarShape sh) {
 
 KernelRes kernel_res(SwarShape sh, int ch) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, int, int>, KernelRes> cache;
+  static std::map<std::tuple<int, int, int, int, bool>, KernelRes> cache;
   std::lock_guard<std::mutex> lk(mu);
-  const auto key = std::make_tuple(ch, sh.lw, sh.m, sh.nw);
+  const auto key = std::make_tuple(ch, sh.lw, sh.m, sh.nw, interior_first_enabled());
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const KernelRes r = ch == 1 ? query_res<1>(sh) : ch == 3 ? query_res<3>(sh) : query_res<4>(sh);
@@ -488,6 +590,7 @@ KernelRes kernel_res(SwarShape sh, int ch) {
 // tools/fit_swar_data.py + tools/fit_swar_model.py); they pick the measured
 // best shape in 6 of 6 configurations of the current kernel.
 void set_xcd_swizzle(bool on) { g_xcd_swizzle.store(on ? 1 : 0, std::memory_order_relaxed); }
+void set_interior_first(bool on) { g_interior_first.store(on ? 1 : 0, std::memory_order_relaxed); }
 
 SwarResources swar_resources(SwarShape s, int ch) {
   const KernelRes r = kernel_res(s, ch);
@@ -537,13 +640,116 @@ SwarShape pick_swar_shape(int steps, int ch, int64_t rows, int64_t row_bytes) {
   return best;
 }
 
-void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream) {
-  const SwarShape sh = pick_swar_shape(a.steps, channel_count(ch), a.r1 - a.r0, a.row_bytes);
+namespace {
+
+void launch_shape(const StencilLaunch& a, Channels ch, hipStream_t stream, SwarShape sh) {
   switch (ch) {
     case Channels::Grey: launch_ch<1>(a, stream, sh); break;
     case Channels::Rgb: launch_ch<3>(a, stream, sh); break;
     case Channels::Rgba: launch_ch<4>(a, stream, sh); break;
   }
+}
+
+// Empirical shape tuning: the model ranks the shapes, the best few are timed
+// on the actual launch (same src -> dst, so the repeats are harmless: every
+// run writes the same bytes) and the fastest is cached per (channels, steps,
+// rows, row bytes, step variant).  Never while the stream is being captured
+// into a graph (the engine tunes a step's launches before capturing it).
+struct TuneKey {
+  int ch, steps;
+  int64_t rows, row_bytes;
+  bool interior_first;
+  bool operator<(const TuneKey& o) const {
+    return std::tie(ch, steps, rows, row_bytes, interior_first) <
+           std::tie(o.ch, o.steps, o.rows, o.row_bytes, o.interior_first);
+  }
+};
+std::mutex g_tune_mu;
+std::map<TuneKey, SwarShape> g_tuned;
+std::atomic<int> g_autotune{-1};
+
+bool autotune_enabled() {
+  int v = g_autotune.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = std::getenv("PCONV_AUTOTUNE");
+    v = (e && e[0] == '0') ? 0 : 1;
+    g_autotune.store(v, std::memory_order_relaxed);
+  }
+  return v != 0;
+}
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+constexpr int kTuneCandidates = 5;
+constexpr int kTuneRepeats = 3;
+
+SwarShape tuned_shape(const StencilLaunch& a, Channels ch, hipStream_t stream, bool may_measure) {
+  const int c = channel_count(ch);
+  const int64_t rows = a.r1 - a.r0;
+  SwarShape forced;
+  if (override_shape(forced) || !autotune_enabled()) return pick_swar_shape(a.steps, c, rows, a.row_bytes);
+  const TuneKey key{c, a.steps, rows, a.row_bytes, interior_first_enabled()};
+  {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    auto it = g_tuned.find(key);
+    if (it != g_tuned.end()) return it->second;
+  }
+  if (!may_measure || capturing(stream)) return pick_swar_shape(a.steps, c, rows, a.row_bytes);
+  std::vector<std::pair<double, SwarShape>> ranked;
+  for (const auto& sh : kShapes) {
+    const double cost = swar_launch_cycles(sh, a.steps, c, rows, a.row_bytes);
+    if (cost < 1e299) ranked.emplace_back(cost, sh);
+  }
+  PCONV_CHECK(!ranked.empty(), "swar temporal kernel: steps too large for every tile shape");
+  std::sort(ranked.begin(), ranked.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+  if (ranked.size() > static_cast<size_t>(kTuneCandidates)) ranked.resize(kTuneCandidates);
+  SwarShape best = ranked.front().second;
+  if (ranked.size() > 1) {
+    Event e0 = Event::create(true), e1 = Event::create(true);
+    float best_ms = 1e30f;
+    for (const auto& cand : ranked) {
+      launch_shape(a, ch, stream, cand.second);  // warm (code object, caches)
+      e0.record(stream);
+      for (int r = 0; r < kTuneRepeats; ++r) launch_shape(a, ch, stream, cand.second);
+      e1.record(stream);
+      PCONV_HIP_CHECK(hipEventSynchronize(e1.get()));
+      const float ms = Event::elapsed_ms(e0, e1);
+      if (ms < best_ms) {
+        best_ms = ms;
+        best = cand.second;
+      }
+    }
+  }
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  g_tuned.emplace(key, best);
+  return best;
+}
+
+}  // namespace
+
+void set_autotune(bool on) { g_autotune.store(on ? 1 : 0, std::memory_order_relaxed); }
+
+void clear_swar_tuning() {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  g_tuned.clear();
+}
+
+std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned() {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  std::vector<std::pair<std::vector<int64_t>, SwarShape>> out;
+  for (const auto& kv : g_tuned)
+    out.push_back({{kv.first.ch, kv.first.steps, kv.first.rows, kv.first.row_bytes, kv.first.interior_first ? 1 : 0},
+                   kv.second});
+  return out;
+}
+
+void prepare_swar(const StencilLaunch& a, Channels ch, hipStream_t stream) { (void)tuned_shape(a, ch, stream, true); }
+
+void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream) {
+  launch_shape(a, ch, stream, tuned_shape(a, ch, stream, true));
 }
 
 }  // namespace pconv

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <utility>
 #include <vector>
 
 #include "pconv/kernels.hpp"
@@ -19,9 +20,17 @@ struct SwarShape {
 double swar_launch_cycles(SwarShape s, int steps, int ch, int64_t rows, int64_t row_bytes);
 SwarShape pick_swar_shape(int steps, int ch, int64_t rows, int64_t row_bytes);
 
-// Enqueue the fused gaussian for `a.steps` repetitions (shape from the model
-// or from PCONV_SWAR_SHAPE="lw,m,nw").
+// Enqueue the fused gaussian for `a.steps` repetitions.  Shape: forced
+// (PCONV_SWAR_SHAPE="lw,m,nw" / set_swar_shape), else tuned on first use
+// (the model's best candidates timed on this launch; PCONV_AUTOTUNE=0: model
+// only), else the model's pick while a graph is being captured.
 void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
+// Tune (if needed) without enqueueing the launch — before a graph capture.
+void prepare_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
+void set_autotune(bool on);
+void clear_swar_tuning();
+// Tuned entries: ({channels, steps, rows, row_bytes, interior_first}, shape).
+std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned();
 
 // Force a tile shape (lw = 0 restores the model) and list the instantiated ones.
 void set_swar_shape(int lw, int m, int nw);
@@ -36,5 +45,8 @@ struct SwarResources {
 SwarResources swar_resources(SwarShape s, int ch);
 // XCD-aware tile order of the SWAR kernel (default on; PCONV_XCD_SWIZZLE=0).
 void set_xcd_swizzle(bool on);
+// Interior-first repetition step (barrier wait hidden behind the interior
+// rows; default on; PCONV_INTERIOR_FIRST=0) vs exchange-first.
+void set_interior_first(bool on);
 
 }  // namespace pconv

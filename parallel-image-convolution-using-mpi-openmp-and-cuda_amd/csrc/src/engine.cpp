@@ -124,6 +124,32 @@ std::vector<Phase> BandEngine::plan(int reps) const {
   return plan_band(band_, reps, c);
 }
 
+StencilLaunch BandEngine::make_launch(const LaunchSpec& l, int cur, uint8_t* dst, int64_t dst_pitch) const {
+  StencilLaunch a;
+  a.src = frame_[cur].data() + lay_.offset(0);
+  a.dst = dst ? dst : frame_[cur ^ 1].data() + lay_.offset(0);
+  a.dst_pitch = dst ? dst_pitch : 0;
+  a.pitch = lay_.pitch;
+  a.row_bytes = lay_.row_bytes;
+  a.r0 = l.lo;
+  a.r1 = l.hi;
+  a.frame_lo = -lay_.halo;
+  a.frame_hi = lay_.rows + lay_.halo;
+  a.steps = l.steps;
+  a.g_row0 = band_.y0;
+  a.height = geom_.height;
+  return a;
+}
+
+void BandEngine::prepare(const std::vector<Phase>& ph) {
+  int cur = cur_;
+  for (const auto& p : ph) {
+    for (const auto& l : p.launches)
+      prepare_stencil(filter_, geom_.channels, make_launch(l, cur, nullptr, 0), cs_, opt_.variant);
+    cur ^= 1;
+  }
+}
+
 void BandEngine::launch(const LaunchSpec& l, hipStream_t s, uint8_t* dst, int64_t dst_pitch) {
   StencilLaunch a;
   a.src = src_frame();
@@ -193,6 +219,7 @@ void BandEngine::run(int reps) {
     auto it = graphs_.find(key);
     if (it == graphs_.end()) {
       hipGraph_t g = nullptr;
+      prepare(ph);
       PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeThreadLocal));
       for (const auto& p : ph) enqueue_phase(p);
       PCONV_HIP_CHECK(hipStreamEndCapture(cs_, &g));
@@ -245,6 +272,7 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
                     ph.back().launches[0].lo == 0 && ph.back().launches[0].hi == band_.rows && filter_.binomial121 &&
                     (opt_.variant == KernelVariant::Auto || opt_.variant == KernelVariant::Temporal) && rb % 4 == 0 &&
                     reinterpret_cast<uintptr_t>(host_out) % 16 == 0;
+    prepare(ph);  // tile-shape tuning cannot run inside the capture
     PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
     upload_rows(host_in, rb, in_r0, in_r1, cs_);
     for (size_t i = 0; i + (zc ? 1 : 0) < ph.size(); ++i) enqueue_phase(ph[i]);

@@ -319,6 +319,17 @@ PYBIND11_MODULE(_pconv_native, m) {
                               swar_launch_cycles(s, steps, channel_count(parse_channels(ch)), rows, row_bytes));
       },
       py::arg("steps"), py::arg("channels"), py::arg("rows"), py::arg("row_bytes"));
+  m.def("set_autotune", &set_autotune, py::arg("on"),
+        "Time the model's best SWAR tile shapes on first use of a launch geometry (default on).");
+  m.def("clear_swar_tuning", &clear_swar_tuning);
+  m.def("swar_tuned", []() {
+    py::list out;
+    for (const auto& kv : swar_tuned())
+      out.append(py::make_tuple(py::cast(kv.first), py::make_tuple(kv.second.lw, kv.second.m, kv.second.nw)));
+    return out;
+  });
+  m.def("set_interior_first", &set_interior_first, py::arg("on"),
+        "SWAR step order: interior rows before the LDS/barrier exchange (on) or after it.");
   m.def("set_xcd_swizzle", &set_xcd_swizzle, py::arg("on"),
         "XCD-aware (bijective, per-XCD contiguous) tile order of the SWAR kernel.");
   m.def(

@@ -3,7 +3,7 @@ sys.path.insert(0, '.')
 import pconv
 n=pconv.native
 V={}
-for l in open('profiles/r01/swar_kernel_resources.txt'):
+for l in open('profiles/r01b/swar_kernel_resources_interior_first.txt'):
     d=dict(kv.split('=') for kv in l.split())
     V[(int(d['ch']),int(d['lw']),int(d['m']),int(d['nw']))]=(int(d['vgpr']),int(d['lds']))
 CH={'grey':1,'rgb':3,'rgba':4}

@@ -2,7 +2,7 @@ import json, math, numpy as np
 from scipy.optimize import least_squares
 D=json.load(open('gpurun_out/fit_data.json'))
 V={}
-for l in open('profiles/r01/swar_kernel_resources.txt'):
+for l in open('profiles/r01b/swar_kernel_resources_interior_first.txt'):
     d=dict(kv.split('=') for kv in l.split())
     V[(int(d['ch']),int(d['lw']),int(d['m']),int(d['nw']))]=(int(d['vgpr']),int(d['lds']))
 def launch_cycles(p, sh, ch, rb, R, s):
