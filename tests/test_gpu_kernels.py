@@ -187,3 +187,25 @@ def test_every_swar_shape_bit_exact(native, rng):
                 assert np.array_equal(gpu[11:61], cpu[11:61]), (lw, m, nw, channels, steps, "band")
     finally:
         native.set_swar_shape(0, 0, 0)
+
+
+def test_frame_beyond_2gib_offsets(pconv_mod, native):
+    """64-bit offsets end to end: a 2.16 GB grey frame
+    (65536 x 33000) through the fused kernel; rows near the top, the middle
+    and the bottom are checked against the NumPy oracle on sub-windows (a row
+    after `reps` repetitions depends only on the `reps` rows around it)."""
+    import numpy as np
+
+    w, h, reps = 65536, 33000, 3
+    img = np.empty((h, w), np.uint8)
+    native.synth_rows(img.reshape(-1), w, h, "grey", 11, 0, h)
+    out = pconv_mod.convolve(img, reps, backend="hip", fuse=3)
+    assert out.shape == img.shape
+    for y0 in (0, h // 2 - 4, h - 8):
+        lo, hi = max(0, y0 - reps), min(h, y0 + 8 + reps)
+        # oracle on the window; rows [lo, hi) with zero padding is exact only
+        # where the window edge is the image edge or >= reps rows away
+        ref = pconv_mod.numpy_convolve(img[lo:hi, :2048], reps)
+        got = out[y0:y0 + 8, :2048 - reps]
+        exp = ref[y0 - lo:y0 - lo + 8, :2048 - reps]
+        assert np.array_equal(got, exp), y0
