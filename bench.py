@@ -114,6 +114,16 @@ def check_bands(blur, a) -> int:
     return int(sum_over_ranks(bad))
 
 
+def gather_floats(v: float):
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [float(v)]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, float(v))
+    return [float(x) for x in out]
+
+
 def exchange_check(a, blur, world, rank, device, transport):
     """Secondary measurement for N>1: the same images with halo rows exchanged
     GPU-to-GPU (RCCL over xGMI, one communicator per slot) instead of
@@ -202,8 +212,9 @@ def main():
     blur.drain()
     torch.cuda.synchronize()
     barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = blur.comm.allreduce_max(elapsed) if blur.comm is not None else max_over_ranks(elapsed)
+    mine = time.perf_counter() - t0
+    elapsed = blur.comm.allreduce_max(mine) if blur.comm is not None else max_over_ranks(mine)
+    per_rank = gather_floats(mine)  # diagnostics: load balance across ranks
     stats = blur.stats
     mismatches = check_bands(blur, a) if a.check else None
     if a.emulate:
@@ -275,7 +286,9 @@ def main():
                 "us_per_rep": round(loop_elapsed / ls / a.reps * 1e6, 3) if ls else None,
             },
             "device": torch.cuda.get_device_name(device),
+            "rccl": pconv.native.rccl_version() if world > 1 else None,
             "pconv": pconv.__version__,
+            "per_rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in per_rank],
         }
         if mismatches is not None:
             out["mismatches"] = mismatches
