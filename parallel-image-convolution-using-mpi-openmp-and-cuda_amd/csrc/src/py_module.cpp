@@ -400,6 +400,8 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_property_readonly("row_bytes", [](const BandEngine& e) { return e.layout().row_bytes; })
       .def_property_readonly("compute_stream",
                              [](const BandEngine& e) { return reinterpret_cast<uintptr_t>(e.compute_stream()); })
+      .def_property_readonly("comm_stream",
+                             [](const BandEngine& e) { return reinterpret_cast<uintptr_t>(e.comm_stream()); })
       .def_property_readonly("src_ptr", [](const BandEngine& e) { return reinterpret_cast<uintptr_t>(e.src_frame()); })
       .def("plan", &BandEngine::plan, py::arg("reps"))
       .def(

@@ -68,6 +68,7 @@ def parse(argv: List[str]) -> argparse.Namespace:
     p.add_argument("--check", action="store_true")
     p.add_argument("--json", action="store_true")
     p.add_argument("--quiet", action="store_true")
+    p.add_argument("--timeout", type=float, default=600.0, help="RCCL watchdog (seconds) on the halo waits")
     a = p.parse_args(argv)
     if a.width < 1 or a.height < 1 or a.reps < 0:
         sys.stderr.write(usage(prog))
@@ -89,6 +90,7 @@ class _HipBand:
                                 fuse=int(fuse), overlap=not a.no_overlap)
         self.band, self.halo, self.fuse = self.eng.band, self.eng.halo, self.eng.fuse
         self.comm = self.transport = None
+        self.timeout_s = float(a.timeout)
         if world > 1:
             if a.transport == "rccl":
                 from .bootstrap import make_rccl_comm
@@ -108,6 +110,9 @@ class _HipBand:
 
     def run(self, reps: int) -> None:
         self.eng.run(reps)
+        if self.comm is not None:  # poll RCCL errors; abort + raise instead of hanging on a dead peer
+            self.comm.wait(self.eng.comm_stream, self.timeout_s)
+            self.comm.wait(self.eng.compute_stream, self.timeout_s)
         self.eng.synchronize()
 
     def result(self, out: np.ndarray) -> None:
