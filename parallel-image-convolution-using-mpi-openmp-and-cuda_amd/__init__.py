@@ -27,7 +27,8 @@ __version__ = "0.1.0"
 
 from ._native import native, native_available  # noqa: E402  (loads torch first)
 from .models.filters import Filter, get_filter, list_filters  # noqa: E402
-from .ops.stencil import convolve, Engine  # noqa: E402
+from .ops.stencil import convolve, convolve_file, Engine  # noqa: E402
+from .models.pipeline import FilterPipeline  # noqa: E402
 from .ops.reference import numpy_convolve  # noqa: E402
 from .utils.raw_io import read_raw, write_raw, output_path_for, synthetic_image  # noqa: E402
 
@@ -38,7 +39,9 @@ __all__ = [
     "get_filter",
     "list_filters",
     "convolve",
+    "convolve_file",
     "Engine",
+    "FilterPipeline",
     "numpy_convolve",
     "read_raw",
     "write_raw",

@@ -160,3 +160,17 @@ def convolve(image, reps: int = 1, filter="gaussian", backend: str = "auto", dev
         return eng(image, reps)
 
     raise ValueError(f"unknown backend {backend!r} (hip|omp|cpu|numpy|auto)")
+
+
+def convolve_file(path: str, width: int, height: int, reps: int, channels: str = "grey", filter="gaussian",
+                  out: Optional[str] = None, backend: str = "auto", device: Optional[int] = None) -> str:
+    """The reference program in one call (``cuda/main.c:10-53``): read the raw
+    image, ``reps`` repetitions, write ``blur_<name>`` (or ``out``); returns the
+    output path."""
+    from ..utils.raw_io import output_path_for, read_raw, write_raw
+
+    img = read_raw(path, width, height, channels)
+    res = convolve(img, reps, filter, backend=backend, device=device)
+    dst = out or output_path_for(path)
+    write_raw(dst, res)
+    return dst

@@ -95,3 +95,25 @@ def test_convolve_backends_agree(pconv_mod, rng):
     c = pconv_mod.convolve(img, 3, backend="omp")
     d = pconv_mod.convolve(torch.from_numpy(img), 3, backend="omp")
     assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, d.numpy())
+
+
+def test_filter_pipeline_cpu(pconv_mod, rng):
+    """Multi-stage pipelines = composition of single-filter runs (omp backend
+    vs the NumPy oracle of the whole chain)."""
+    img = rng.integers(0, 256, size=(29, 31, 3), dtype=np.uint8)
+    p = pconv_mod.FilterPipeline.from_spec("gaussian:3, box:2, edge")
+    assert p.total_reps == 6 and [s.filter.name for s in p.stages] == ["gaussian", "box", "edge"]
+    assert np.array_equal(p.apply(img, backend="omp"), p.reference(img))
+    q = pconv_mod.FilterPipeline([("gaussian", 2), (([1, 1, 1, 1, 8, 1, 1, 1, 1], 16), 1)])
+    assert np.array_equal(q.apply(img, backend="cpu"), q.reference(img))
+    with pytest.raises(ValueError):
+        pconv_mod.FilterPipeline.from_spec("gaussian:-1")
+
+
+def test_convolve_file_cpu(pconv_mod, tmp_path, rng):
+    img = rng.integers(0, 256, size=(17, 23), dtype=np.uint8)
+    src = str(tmp_path / "g.raw")
+    pconv_mod.write_raw(src, img)
+    dst = pconv_mod.convolve_file(src, 23, 17, 4, "grey", backend="omp")
+    assert dst.endswith("blur_g.raw")
+    assert np.array_equal(pconv_mod.read_raw(dst, 23, 17, "grey"), pconv_mod.numpy_convolve(img, 4))

@@ -212,3 +212,14 @@ def test_xcd_swizzle_off_and_model_table(pconv_mod, native, rng):
     assert len(table) == len(native.swar_shapes())
     for lw, m, nw, vgpr, lds, measured, cycles in table:
         assert measured and 0 < vgpr <= 512 and lds >= 16384 and cycles > 0
+
+
+def test_filter_pipeline_hip(pconv_mod, rng):
+    """A gaussian/box/edge/custom pipeline on the GPU equals the NumPy chain."""
+    img = rng.integers(0, 256, size=(64, 77, 3), dtype=np.uint8)
+    p = pconv_mod.FilterPipeline.from_spec("gaussian:9,box:2,edge:1,gaussian:3")
+    assert np.array_equal(p.apply(img, backend="hip"), p.reference(img))
+    import torch
+
+    t = torch.from_numpy(img).cuda()
+    assert np.array_equal(p.apply(t).cpu().numpy(), p.reference(img))
