@@ -153,76 +153,24 @@ __device__ __forceinline__ void store_bytes(uint8_t* p, const typename Chunk<NP>
   for (int k = 0; k < n; ++k) p[k] = static_cast<uint8_t>(w[k >> 2] >> (8 * (k & 3)));
 }
 
-// One repetition of a wave's M register rows: swap boundary rows with the
-// neighbouring waves through LDS (double-buffered by `par`, one barrier),
-// horizontal pass per row, rolling vertical sum, truncation, re-zeroing of
-// everything outside the image.
-template <int CH, int NP, int M, int NW>
-__device__ __forceinline__ void swar_step(u32 (&D)[M][NP], uint4 (&lds)[2][NW][2][NP / 4][64], int par, int w,
-                                          int lane, bool needs_mask, const u32 (&cm)[NP], int out_top, int out_bot) {
-  constexpr int NQ = NP / 4;
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    lds[par][w][0][q][lane] = make_uint4(D[0][4 * q], D[0][4 * q + 1], D[0][4 * q + 2], D[0][4 * q + 3]);
-    lds[par][w][1][q][lane] = make_uint4(D[M - 1][4 * q], D[M - 1][4 * q + 1], D[M - 1][4 * q + 2], D[M - 1][4 * q + 3]);
-  }
-  __syncthreads();
-  u32 A[NP], B[NP];
-  {
-    const int wa = w > 0 ? w - 1 : 0;       // wave 0: tile top halo, value irrelevant
-    const int wb = w < NW - 1 ? w + 1 : w;  // last wave: tile bottom halo
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const uint4 av = lds[par][wa][1][q][lane], bv = lds[par][wb][0][q][lane];
-      A[4 * q] = av.x; A[4 * q + 1] = av.y; A[4 * q + 2] = av.z; A[4 * q + 3] = av.w;
-      B[4 * q] = bv.x; B[4 * q + 1] = bv.y; B[4 * q + 2] = bv.z; B[4 * q + 3] = bv.w;
-    }
-  }
-  u32 Hc[NP], Sc[NP];
-  {
-    u32 Ha[NP];
-    horiz<CH, NP>(A, Ha);
-    horiz<CH, NP>(D[0], Hc);
-#pragma unroll
-    for (int k = 0; k < NP; ++k) Sc[k] = Ha[k] + Hc[k];
-  }
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    u32 Hn[NP];
-    if (i + 1 < M)
-      horiz<CH, NP>(D[i + 1], Hn);
-    else
-      horiz<CH, NP>(B, Hn);
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const u32 Sn = Hc[k] + Hn[k];
-      D[i][k] = ((Sc[k] + Sn) >> 4) & 0x00ff00ffu;  // floor(sum of the 9 taps / 16), both fields
-      Sc[k] = Sn;
-      Hc[k] = Hn[k];
-    }
-  }
-  if (needs_mask) {
-#pragma unroll
-    for (int i = 0; i < M; ++i)
-#pragma unroll
-      for (int k = 0; k < NP; ++k) D[i][k] &= cm[k];
-  }
-  if (out_top > 0 || out_bot < M) {
-#pragma unroll
-    for (int i = 0; i < M; ++i)
-      if (i < out_top || i >= out_bot)
-#pragma unroll
-        for (int k = 0; k < NP; ++k) D[i][k] = 0;
-  }
+// One repetition of a wave's M register rows, interior first: the wave
+// publishes its two boundary rows to LDS, computes its interior rows 1..M-2
+// (they need only its own registers) while the other waves catch up, and only
+// then meets them at the barrier to finish rows 0 and M-1 with the
+// neighbours' rows — the LDS round trip and the barrier wait hide behind M-2
+// rows of arithmetic (measured 2-13 % over exchanging first).  MODE picks the
+// truncation: 0 floor(S/16); 1 keeps 16 x floor(S/16) (one AND; the next step
+// then sums values < 2^12 into fields < 2^16); 2 floor(S/256) of such a step.
+// Out-of-image rows and columns are re-zeroed after every step.
+template <int MODE>
+__device__ __forceinline__ u32 trunc_sum(u32 S) {
+  if constexpr (MODE == 0) return (S >> 4) & 0x00ff00ffu;
+  else if constexpr (MODE == 1) return S & 0x0ff00ff0u;
+  else return (S >> 8) & 0x00ff00ffu;
 }
 
-// Interior-first variant: the wave publishes its boundary rows, computes its
-// interior rows 1..M-2 (they need only its own registers) while the other
-// waves catch up, and only then meets them at the barrier to finish rows 0
-// and M-1 with the neighbours' rows — the LDS round trip and the barrier wait
-// hide behind M-2 rows of arithmetic.
-template <int CH, int NP, int M, int NW>
-__device__ __forceinline__ void swar_step_if(u32 (&D)[M][NP], uint4 (&lds)[2][NW][2][NP / 4][64], int par, int w,
+template <int CH, int NP, int M, int NW, int MODE = 0>
+__device__ __forceinline__ void swar_step(u32 (&D)[M][NP], uint4 (&lds)[2][NW][2][NP / 4][64], int par, int w,
                                              int lane, bool needs_mask, const u32 (&cm)[NP], int out_top,
                                              int out_bot) {
   static_assert(M >= 2, "interior-first step needs two register rows per wave");
@@ -250,7 +198,7 @@ __device__ __forceinline__ void swar_step_if(u32 (&D)[M][NP], uint4 (&lds)[2][NW
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       const u32 Sn = Hc[k] + Hn[k];
-      D[i][k] = ((Sc[k] + Sn) >> 4) & 0x00ff00ffu;
+      D[i][k] = trunc_sum<MODE>(Sc[k] + Sn);
       Sc[k] = Sn;
       Hp[k] = Hc[k];
       Hc[k] = Hn[k];
@@ -273,8 +221,8 @@ __device__ __forceinline__ void swar_step_if(u32 (&D)[M][NP], uint4 (&lds)[2][NW
     horiz<CH, NP>(B, Hb);
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      D[0][k] = (((Ha[k] + H0[k]) + (H0[k] + H1[k])) >> 4) & 0x00ff00ffu;
-      D[M - 1][k] = (((Hp[k] + Hc[k]) + (Hc[k] + Hb[k])) >> 4) & 0x00ff00ffu;
+      D[0][k] = trunc_sum<MODE>((Ha[k] + H0[k]) + (H0[k] + H1[k]));
+      D[M - 1][k] = trunc_sum<MODE>((Hp[k] + Hc[k]) + (Hc[k] + Hb[k]));
     }
   }
   if (needs_mask) {
@@ -292,7 +240,7 @@ __device__ __forceinline__ void swar_step_if(u32 (&D)[M][NP], uint4 (&lds)[2][NW
   }
 }
 
-template <int CH, int LW, int M, int NW, bool IF>
+template <int CH, int LW, int M, int NW, bool ALT>
 __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                   int64_t pitch, int64_t dst_pitch, int row_bytes, int r0, int r1,
                                                   int steps, int g_row0, int height, int nstrips, int pair_stride,
@@ -347,14 +295,19 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
   const int out_top = min(max(-g_row0 - row_base, 0), M);
   const int out_bot = min(max(height - g_row0 - row_base, 0), M);
 
-  // (Measured and rejected: steps in pairs keeping 16 x the truncated value
-  // in between — one AND instead of shift + AND every other step — the two
-  // step bodies per iteration cost up to +40 VGPRs and a wave per SIMD.)
-  for (int s = 0; s < steps; ++s) {
-    if constexpr (IF)
-      swar_step_if<CH, NP, M, NW>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
-    else
-      swar_step<CH, NP, M, NW>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
+  // ALT: steps in pairs keeping 16 x the truncated value in between (one AND
+  // instead of shift + AND every other step).  Two step bodies per iteration
+  // cost registers (up to +40 VGPRs on grey tiles), so both forms exist and
+  // the tuner picks per launch geometry.
+  if constexpr (ALT) {  // pairs of steps: scale-16 intermediate, one AND saved per pair
+    int s = 0;
+    for (; s + 2 <= steps; s += 2) {
+      swar_step<CH, NP, M, NW, 1>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+      swar_step<CH, NP, M, NW, 2>(D, lds, 1, w, lane, needs_mask, cm, out_top, out_bot);
+    }
+    if (s < steps) swar_step<CH, NP, M, NW, 0>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+  } else {
+    for (int s = 0; s < steps; ++s) swar_step<CH, NP, M, NW, 0>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
   }
 
   const bool lane_in = lane >= hl && lane < 64 - hl;
@@ -404,20 +357,24 @@ bool xcd_swizzle_enabled() {
   return v != 0;
 }
 
-std::atomic<int> g_interior_first{-1};  // -1: PCONV_INTERIOR_FIRST on first use (default on)
+std::atomic<int> g_alt_mode{-2};  // -2: PCONV_SWAR_ALT on first use; -1 tune, 0 off, 1 on
 
-bool interior_first_enabled() {
-  int v = g_interior_first.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = std::getenv("PCONV_INTERIOR_FIRST");
-    v = (e && e[0] == '0') ? 0 : 1;
-    g_interior_first.store(v, std::memory_order_relaxed);
+int alt_mode() {
+  int v = g_alt_mode.load(std::memory_order_relaxed);
+  if (v == -2) {
+    const char* e = std::getenv("PCONV_SWAR_ALT");
+    v = !e ? -1 : e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
+    g_alt_mode.store(v, std::memory_order_relaxed);
   }
-  return v != 0;
+  return v;
 }
 
+// Step form when nothing was tuned (graph capture, autotune off): the paired
+// form is faster in most measured geometries.
+bool default_alt() { return alt_mode() != 0; }
+
 template <int CH, int LW, int M, int NW>
-void launch_one(const StencilLaunch& a, hipStream_t s) {
+void launch_one(const StencilLaunch& a, hipStream_t s, bool alt) {
   const int steps = a.steps;
   const int hl = (steps * CH + LW - 1) / LW;
   const int vbytes = (64 - 2 * hl) * LW;
@@ -428,7 +385,7 @@ void launch_one(const StencilLaunch& a, hipStream_t s) {
   const int row_tiles = ceil_div(static_cast<int>(a.r1 - a.r0), vrows);
   const dim3 grid(pair_stride * row_tiles);
   const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
-  if (interior_first_enabled())
+  if (alt)
     k_swar<CH, LW, M, NW, true><<<grid, dim3(64 * NW), 0, s>>>(a.src, a.dst, a.pitch, a.dst_pitch ? a.dst_pitch : a.pitch,
                                                        static_cast<int>(a.row_bytes),
                                                        static_cast<int>(a.r0), static_cast<int>(a.r1), steps,
@@ -443,10 +400,10 @@ void launch_one(const StencilLaunch& a, hipStream_t s) {
 }
 
 template <int CH>
-void launch_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh) {
+void launch_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh, bool alt) {
 #define PCONV_SWAR(LW_, M_, NW_)                            \
   if (sh.lw == LW_ && sh.m == M_ && sh.nw == NW_) {         \
-    launch_one<CH, LW_, M_, NW_>(a, s);                     \
+    launch_one<CH, LW_, M_, NW_>(a, s, alt);                \
     return;                                                 \
   }
   PCONV_SWAR(8, 8, 8)
@@ -524,13 +481,12 @@ struct KernelRes {
 };
 
 template <int CH>
-KernelRes query_res(SwarShape sh) {
+KernelRes query_res(SwarShape sh, bool alt) {
   hipFuncAttributes at{};
   hipError_t e = hipErrorInvalidValue;
 #define PCONV_SWAR(LW_, M_, NW_)                                                                     \
   if (sh.lw == LW_ && sh.m == M_ && sh.nw == NW_)                                                   \
-    e = hipFuncGetAttributes(&at, interior_first_enabled()                                          \
-                                      ? reinterpret_cast<const void*>(&k_swar<CH, LW_, M_, NW_, true>)  \
+    e = hipFuncGetAttributes(&at, alt ? reinterpret_cast<const void*>(&k_swar<CH, LW_, M_, NW_, true>)   \
                                       : reinterpret_cast<const void*>(&k_swar<CH, LW_, M_, NW_, false>));
   PCONV_SWAR(8, 8, 8)
   PCONV_SWAR(8, 8, 4)
@@ -560,14 +516,14 @@ KernelRes query_res(SwarShape sh) {
   return r;
 }
 
-KernelRes kernel_res(SwarShape sh, int ch) {
+KernelRes kernel_res(SwarShape sh, int ch, bool alt) {
   static std::mutex mu;
   static std::map<std::tuple<int, int, int, int, bool>, KernelRes> cache;
   std::lock_guard<std::mutex> lk(mu);
-  const auto key = std::make_tuple(ch, sh.lw, sh.m, sh.nw, interior_first_enabled());
+  const auto key = std::make_tuple(ch, sh.lw, sh.m, sh.nw, alt);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  const KernelRes r = ch == 1 ? query_res<1>(sh) : ch == 3 ? query_res<3>(sh) : query_res<4>(sh);
+  const KernelRes r = ch == 1 ? query_res<1>(sh, alt) : ch == 3 ? query_res<3>(sh, alt) : query_res<4>(sh, alt);
   if (r.measured) cache.emplace(key, r);  // estimates (no device) are not cached
   return r;
 }
@@ -590,10 +546,10 @@ KernelRes kernel_res(SwarShape sh, int ch) {
 // tools/fit_swar_data.py + tools/fit_swar_model.py); they pick the measured
 // best shape in 6 of 6 configurations of the current kernel.
 void set_xcd_swizzle(bool on) { g_xcd_swizzle.store(on ? 1 : 0, std::memory_order_relaxed); }
-void set_interior_first(bool on) { g_interior_first.store(on ? 1 : 0, std::memory_order_relaxed); }
+void set_swar_alt(int mode) { g_alt_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
 
 SwarResources swar_resources(SwarShape s, int ch) {
-  const KernelRes r = kernel_res(s, ch);
+  const KernelRes r = kernel_res(s, ch, default_alt());
   return SwarResources{r.vgpr, r.lds, r.measured};
 }
 
@@ -607,7 +563,7 @@ double swar_launch_cycles(SwarShape s, int steps, int ch, int64_t rows, int64_t 
   const int vrows = s.m * s.nw - 2 * steps;
   if (vrows <= 0 || np < ch) return 1e300;
   const double g = static_cast<double>(pairs * ceil_div<int64_t>(rows, vrows));
-  const KernelRes res = kernel_res(s, ch);
+  const KernelRes res = kernel_res(s, ch, default_alt());
   const int vgpr_waves = std::max(1, std::min(8, 512 / round_up(std::max(res.vgpr, 1), 8)));
   const int lds_wgs = res.lds > 0 ? (160 * 1024) / res.lds : 8;
   const int L = std::max(1, std::min({lds_wgs, vgpr_waves * 4 / s.nw, 32 / s.nw}));
@@ -642,30 +598,33 @@ SwarShape pick_swar_shape(int steps, int ch, int64_t rows, int64_t row_bytes) {
 
 namespace {
 
-void launch_shape(const StencilLaunch& a, Channels ch, hipStream_t stream, SwarShape sh) {
+struct SwarChoice {
+  SwarShape shape;
+  bool alt = true;
+};
+
+void launch_choice(const StencilLaunch& a, Channels ch, hipStream_t stream, SwarChoice c) {
   switch (ch) {
-    case Channels::Grey: launch_ch<1>(a, stream, sh); break;
-    case Channels::Rgb: launch_ch<3>(a, stream, sh); break;
-    case Channels::Rgba: launch_ch<4>(a, stream, sh); break;
+    case Channels::Grey: launch_ch<1>(a, stream, c.shape, c.alt); break;
+    case Channels::Rgb: launch_ch<3>(a, stream, c.shape, c.alt); break;
+    case Channels::Rgba: launch_ch<4>(a, stream, c.shape, c.alt); break;
   }
 }
 
-// Empirical shape tuning: the model ranks the shapes, the best few are timed
-// on the actual launch (same src -> dst, so the repeats are harmless: every
-// run writes the same bytes) and the fastest is cached per (channels, steps,
-// rows, row bytes, step variant).  Never while the stream is being captured
-// into a graph (the engine tunes a step's launches before capturing it).
+// Empirical tuning: the model ranks the shapes, the best few are timed in both
+// step forms on the actual launch (same src -> dst, so the repeats are
+// harmless: every run writes the same bytes) and the fastest (shape, form) is
+// cached per (channels, steps, rows, row bytes).  Never while the stream is
+// being captured into a graph (the engine tunes a step's launches first).
 struct TuneKey {
   int ch, steps;
   int64_t rows, row_bytes;
-  bool interior_first;
   bool operator<(const TuneKey& o) const {
-    return std::tie(ch, steps, rows, row_bytes, interior_first) <
-           std::tie(o.ch, o.steps, o.rows, o.row_bytes, o.interior_first);
+    return std::tie(ch, steps, rows, row_bytes) < std::tie(o.ch, o.steps, o.rows, o.row_bytes);
   }
 };
 std::mutex g_tune_mu;
-std::map<TuneKey, SwarShape> g_tuned;
+std::map<TuneKey, SwarChoice> g_tuned;
 std::atomic<int> g_autotune{-1};
 
 bool autotune_enabled() {
@@ -686,18 +645,28 @@ bool capturing(hipStream_t s) {
 constexpr int kTuneCandidates = 5;
 constexpr int kTuneRepeats = 3;
 
-SwarShape tuned_shape(const StencilLaunch& a, Channels ch, hipStream_t stream, bool may_measure) {
+SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream, bool may_measure) {
   const int c = channel_count(ch);
   const int64_t rows = a.r1 - a.r0;
-  SwarShape forced;
-  if (override_shape(forced) || !autotune_enabled()) return pick_swar_shape(a.steps, c, rows, a.row_bytes);
-  const TuneKey key{c, a.steps, rows, a.row_bytes, interior_first_enabled()};
+  const int mode = alt_mode();
+  SwarChoice fallback;
+  fallback.alt = default_alt();
+  if (override_shape(fallback.shape) || !autotune_enabled()) {
+    if (!override_shape(fallback.shape)) fallback.shape = pick_swar_shape(a.steps, c, rows, a.row_bytes);
+    return fallback;
+  }
+  const TuneKey key{c, a.steps, rows, a.row_bytes};
   {
     std::lock_guard<std::mutex> lk(g_tune_mu);
     auto it = g_tuned.find(key);
-    if (it != g_tuned.end()) return it->second;
+    if (it != g_tuned.end()) {
+      SwarChoice r = it->second;
+      if (mode >= 0) r.alt = mode == 1;  // forced form (the shape stays tuned)
+      return r;
+    }
   }
-  if (!may_measure || capturing(stream)) return pick_swar_shape(a.steps, c, rows, a.row_bytes);
+  fallback.shape = pick_swar_shape(a.steps, c, rows, a.row_bytes);
+  if (!may_measure || capturing(stream)) return fallback;
   std::vector<std::pair<double, SwarShape>> ranked;
   for (const auto& sh : kShapes) {
     const double cost = swar_launch_cycles(sh, a.steps, c, rows, a.row_bytes);
@@ -706,20 +675,24 @@ SwarShape tuned_shape(const StencilLaunch& a, Channels ch, hipStream_t stream, b
   PCONV_CHECK(!ranked.empty(), "swar temporal kernel: steps too large for every tile shape");
   std::sort(ranked.begin(), ranked.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
   if (ranked.size() > static_cast<size_t>(kTuneCandidates)) ranked.resize(kTuneCandidates);
-  SwarShape best = ranked.front().second;
-  if (ranked.size() > 1) {
+  std::vector<SwarChoice> cands;
+  for (const auto& r : ranked)
+    for (int alt = 0; alt <= 1; ++alt)
+      if (mode < 0 || mode == alt) cands.push_back(SwarChoice{r.second, alt == 1});
+  SwarChoice best = cands.front();
+  if (cands.size() > 1) {
     Event e0 = Event::create(true), e1 = Event::create(true);
     float best_ms = 1e30f;
-    for (const auto& cand : ranked) {
-      launch_shape(a, ch, stream, cand.second);  // warm (code object, caches)
+    for (const auto& cand : cands) {
+      launch_choice(a, ch, stream, cand);  // warm (code object, caches)
       e0.record(stream);
-      for (int r = 0; r < kTuneRepeats; ++r) launch_shape(a, ch, stream, cand.second);
+      for (int r = 0; r < kTuneRepeats; ++r) launch_choice(a, ch, stream, cand);
       e1.record(stream);
       PCONV_HIP_CHECK(hipEventSynchronize(e1.get()));
       const float ms = Event::elapsed_ms(e0, e1);
       if (ms < best_ms) {
         best_ms = ms;
-        best = cand.second;
+        best = cand;
       }
     }
   }
@@ -741,15 +714,15 @@ std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned() {
   std::lock_guard<std::mutex> lk(g_tune_mu);
   std::vector<std::pair<std::vector<int64_t>, SwarShape>> out;
   for (const auto& kv : g_tuned)
-    out.push_back({{kv.first.ch, kv.first.steps, kv.first.rows, kv.first.row_bytes, kv.first.interior_first ? 1 : 0},
-                   kv.second});
+    out.push_back({{kv.first.ch, kv.first.steps, kv.first.rows, kv.first.row_bytes, kv.second.alt ? 1 : 0},
+                   kv.second.shape});
   return out;
 }
 
-void prepare_swar(const StencilLaunch& a, Channels ch, hipStream_t stream) { (void)tuned_shape(a, ch, stream, true); }
+void prepare_swar(const StencilLaunch& a, Channels ch, hipStream_t stream) { (void)tuned_choice(a, ch, stream, true); }
 
 void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream) {
-  launch_shape(a, ch, stream, tuned_shape(a, ch, stream, true));
+  launch_choice(a, ch, stream, tuned_choice(a, ch, stream, true));
 }
 
 }  // namespace pconv

@@ -29,7 +29,7 @@ void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
 void prepare_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
 void set_autotune(bool on);
 void clear_swar_tuning();
-// Tuned entries: ({channels, steps, rows, row_bytes, interior_first}, shape).
+// Tuned entries: ({channels, steps, rows, row_bytes, paired_form}, shape).
 std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned();
 
 // Force a tile shape (lw = 0 restores the model) and list the instantiated ones.
@@ -45,8 +45,8 @@ struct SwarResources {
 SwarResources swar_resources(SwarShape s, int ch);
 // XCD-aware tile order of the SWAR kernel (default on; PCONV_XCD_SWIZZLE=0).
 void set_xcd_swizzle(bool on);
-// Interior-first repetition step (barrier wait hidden behind the interior
-// rows; default on; PCONV_INTERIOR_FIRST=0) vs exchange-first.
-void set_interior_first(bool on);
+// Step form: -1 tuned per launch geometry (default), 0 truncate every step,
+// 1 steps in pairs with a scale-16 intermediate (PCONV_SWAR_ALT=0/1).
+void set_swar_alt(int mode);
 
 }  // namespace pconv

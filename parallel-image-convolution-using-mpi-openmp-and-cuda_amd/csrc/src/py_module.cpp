@@ -328,8 +328,8 @@ PYBIND11_MODULE(_pconv_native, m) {
       out.append(py::make_tuple(py::cast(kv.first), py::make_tuple(kv.second.lw, kv.second.m, kv.second.nw)));
     return out;
   });
-  m.def("set_interior_first", &set_interior_first, py::arg("on"),
-        "SWAR step order: interior rows before the LDS/barrier exchange (on) or after it.");
+  m.def("set_swar_alt", &set_swar_alt, py::arg("mode"),
+        "SWAR step form: -1 tuned (default), 0 truncate every step, 1 pairs of steps with a x16 intermediate.");
   m.def("set_xcd_swizzle", &set_xcd_swizzle, py::arg("on"),
         "XCD-aware (bijective, per-XCD contiguous) tile order of the SWAR kernel.");
   m.def(

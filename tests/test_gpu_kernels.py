@@ -170,13 +170,16 @@ def test_temporal_equals_repeated_single_steps(pconv_mod, rng):
         assert np.array_equal(got, pconv_mod.numpy_convolve(img, t)), t
 
 
-def test_every_swar_shape_bit_exact(native, rng):
+@pytest.mark.parametrize("form", [0, 1])
+def test_every_swar_shape_bit_exact(native, rng, form):
     """Force each instantiated SWAR tile shape (lane width, rows/wave, waves)
-    and compare a fused launch with the CPU fused-launch reference."""
+    in each step form (0: truncate every step, 1: pairs of steps with a x16
+    intermediate) and compare a fused launch with the CPU fused reference."""
     try:
+        native.set_swar_alt(form)
         for (lw, m, nw) in native.swar_shapes():
             native.set_swar_shape(lw, m, nw)
-            for channels, steps in (("grey", 3), ("rgb", 4), ("rgba", 2), ("rgb", 8)):
+            for channels, steps in (("grey", 3), ("rgb", 4), ("rgba", 2), ("rgb", 8), ("grey", 7), ("rgb", 1)):
                 if m * nw <= 2 * steps or lw < CH[channels]:
                     continue
                 c = CH[channels]
@@ -187,6 +190,7 @@ def test_every_swar_shape_bit_exact(native, rng):
                 assert np.array_equal(gpu[11:61], cpu[11:61]), (lw, m, nw, channels, steps, "band")
     finally:
         native.set_swar_shape(0, 0, 0)
+        native.set_swar_alt(-1)
 
 
 def test_frame_beyond_2gib_offsets(pconv_mod, native):
