@@ -172,7 +172,7 @@ def main():
     import torch
 
     import pconv
-    from pconv.parallel.bootstrap import barrier, init_distributed, max_over_ranks, shutdown
+    from pconv.parallel.bootstrap import barrier, bind_to_device_numa, init_distributed, max_over_ranks, shutdown
     from pconv.parallel.dist_engine import DistributedBlur
 
     ctx = init_distributed("gloo")
@@ -189,6 +189,8 @@ def main():
         a.preload_halo, transport = True, "none"
     device = ctx.local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
+    # host thread + first-touch pinned buffers on the GPU's own socket
+    cpu_bind = bind_to_device_numa(device)
 
     blur = DistributedBlur(a.width, a.height, a.channels, a.filter, a.reps, rank=rank, world=world,
                            device=device, halo=a.halo, fuse=a.fuse, overlap=not a.no_overlap,
@@ -289,6 +291,7 @@ def main():
             "rccl": pconv.native.rccl_version() if world > 1 else None,
             "pconv": pconv.__version__,
             "per_rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in per_rank],
+            "rank0_cpus_bound": cpu_bind,
         }
         if mismatches is not None:
             out["mismatches"] = mismatches

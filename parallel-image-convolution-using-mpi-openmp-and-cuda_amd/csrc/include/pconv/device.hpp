@@ -28,6 +28,12 @@ namespace pconv {
 int device_count();
 void set_device(int device);
 std::string device_name(int device);
+// PCI address of a device, lower case ("0000:75:00.0").
+std::string device_pci_bus_id(int device);
+// Restrict the calling process to the CPUs local to `device` (sysfs
+// local_cpulist of its PCI function, intersected with the current affinity);
+// PCONV_NUMA_BIND=0 disables.  Returns the CPUs kept, 0 if nothing changed.
+int bind_to_device_numa(int device);
 
 class DeviceBuffer {
  public:

@@ -248,6 +248,7 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
               "need " + std::to_string(world) + " GPUs, " + std::to_string(ndev) + " visible (try --transport shm)");
   const int device = rank % ndev;
   set_device(device);
+  if (world > 1) (void)bind_to_device_numa(device);  // this rank's host work on its GPU's socket
   const Filter f = Filter::by_name(c.filter);
   const Band b = row_band(g.height, world, rank);
   const EngineOptions o = engine_options(c, g, world, device);

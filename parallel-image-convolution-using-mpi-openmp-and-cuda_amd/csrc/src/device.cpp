@@ -1,6 +1,13 @@
 // HIP runtime RAII wrappers (see device.hpp).
 #include "pconv/device.hpp"
 
+#include <sched.h>
+
+#include <cctype>
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
+
 namespace pconv {
 
 int device_count() {
@@ -14,6 +21,38 @@ void set_device(int device) {
   PCONV_CHECK(device >= 0 && device < n,
               "device " + std::to_string(device) + " out of range (" + std::to_string(n) + " visible)");
   PCONV_HIP_CHECK(hipSetDevice(device));
+}
+
+std::string device_pci_bus_id(int device) {
+  char buf[64] = {0};
+  PCONV_HIP_CHECK(hipDeviceGetPCIBusId(buf, static_cast<int>(sizeof(buf)), device));
+  std::string id(buf);
+  for (auto& c : id) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  return id;
+}
+
+int bind_to_device_numa(int device) {
+  const char* env = std::getenv("PCONV_NUMA_BIND");
+  if (env && std::string(env) == "0") return 0;
+  std::ifstream f("/sys/bus/pci/devices/" + device_pci_bus_id(device) + "/local_cpulist");
+  std::string text;
+  if (!f || !std::getline(f, text)) return 0;
+  cpu_set_t allowed, keep;
+  CPU_ZERO(&keep);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return 0;
+  std::stringstream ss(text);
+  std::string part;
+  while (std::getline(ss, part, ',')) {
+    if (part.empty()) continue;
+    const auto dash = part.find('-');
+    const int a = std::stoi(part.substr(0, dash));
+    const int b = dash == std::string::npos ? a : std::stoi(part.substr(dash + 1));
+    for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, &allowed)) CPU_SET(c, &keep);
+  }
+  const int n = CPU_COUNT(&keep);
+  if (n == 0 || CPU_EQUAL(&keep, &allowed)) return 0;
+  return sched_setaffinity(0, sizeof(keep), &keep) == 0 ? n : 0;
 }
 
 std::string device_name(int device) {

@@ -270,6 +270,9 @@ PYBIND11_MODULE(_pconv_native, m) {
   m.def("device_count", &device_count);
   m.def("device_name", &device_name);
   m.def("set_device", &set_device);
+  m.def("device_pci_bus_id", &device_pci_bus_id);
+  m.def("bind_to_device_numa", &bind_to_device_numa,
+        "Restrict this process to the CPUs local to the GPU (0: unchanged; PCONV_NUMA_BIND=0 disables)");
 
   py::class_<PinnedBuffer>(m, "PinnedBuffer", py::buffer_protocol())
       .def(py::init<size_t>())

@@ -103,3 +103,50 @@ def barrier(group=None) -> None:
 def shutdown(ctx: DistContext) -> None:
     if ctx.initialized_here and dist.is_initialized():
         dist.destroy_process_group()
+
+
+def parse_cpulist(text: str) -> set:
+    """Parse a sysfs cpulist ("0-3,8,10-11") into a set of CPU ids."""
+    cpus = set()
+    for part in text.strip().split(","):
+        part = part.strip()
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-", 1)
+            cpus.update(range(int(a), int(b) + 1))
+        else:
+            cpus.add(int(part))
+    return cpus
+
+
+def device_local_cpus(device: int, sysfs: str = "/sys/bus/pci/devices") -> Optional[set]:
+    """CPUs on the NUMA node of GPU `device` (its PCIe root), or None if the
+    platform does not say.  The pinned staging buffers of a rank are written
+    by its host thread and read by its GPU's copy engines over that GPU's own
+    PCIe link; keeping the thread (and so first-touch allocations) on the
+    GPU's socket avoids crossing the inter-socket fabric on every copy."""
+    try:
+        bdf = require_native().device_pci_bus_id(device)
+        with open(os.path.join(sysfs, bdf, "local_cpulist")) as f:
+            cpus = parse_cpulist(f.read())
+    except Exception:  # no device / no sysfs entry: leave the affinity alone
+        return None
+    return cpus or None
+
+
+def bind_to_device_numa(device: int) -> Optional[int]:
+    """Restrict this process to the CPUs local to its GPU (intersected with
+    the CPUs it may use).  Off with PCONV_NUMA_BIND=0.  Returns the number of
+    CPUs kept, or None when nothing was changed."""
+    if os.environ.get("PCONV_NUMA_BIND", "1") == "0" or not hasattr(os, "sched_setaffinity"):
+        return None
+    local = device_local_cpus(device)
+    if not local:
+        return None
+    allowed = os.sched_getaffinity(0)
+    keep = local & allowed
+    if not keep or keep == allowed:
+        return None
+    os.sched_setaffinity(0, keep)
+    return len(keep)

@@ -173,6 +173,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         if a.backend == "hip":
             device = ctx.local_rank % max(1, n.device_count())
             n.set_device(device)
+            if world > 1:
+                n.bind_to_device_numa(device)
             runner = _HipBand(a, rank, world, device)
         else:
             runner = _CpuBand(a, rank, world, omp=a.backend == "omp")

@@ -113,3 +113,23 @@ def test_torchrun_usage_error(tmp_path):
     r = _torchrun(1, ["pic.raw", "29", "37", "7", "purple"], tmp_path)
     assert r.returncode != 0
     assert "Error Input!" in r.stderr
+
+
+def test_parse_cpulist():
+    from pconv.parallel.bootstrap import parse_cpulist
+
+    assert parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert parse_cpulist("5") == {5}
+    assert parse_cpulist("") == set()
+
+
+def test_numa_bind_is_a_noop_without_a_gpu(pconv_mod, monkeypatch):
+    """No device (or PCONV_NUMA_BIND=0): binding changes nothing, raises nothing."""
+    from pconv.parallel.bootstrap import bind_to_device_numa
+
+    before = os.sched_getaffinity(0)
+    monkeypatch.setenv("PCONV_NUMA_BIND", "0")
+    assert bind_to_device_numa(0) is None
+    monkeypatch.setenv("PCONV_NUMA_BIND", "1")
+    assert bind_to_device_numa(0) is None  # this container has no GPU
+    assert os.sched_getaffinity(0) == before

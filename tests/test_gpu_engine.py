@@ -223,3 +223,26 @@ def test_filter_pipeline_hip(pconv_mod, rng):
 
     t = torch.from_numpy(img).cuda()
     assert np.array_equal(p.apply(t).cpu().numpy(), p.reference(img))
+
+
+@pytest.mark.gpu
+def test_device_pci_id_and_numa_bind(pconv_mod):
+    """PCI address of the device and the per-rank NUMA binding used by the
+    multi-GPU launchers (kept CPUs are local to the GPU and a subset of the
+    previously allowed ones)."""
+    import os
+    import re
+
+    from pconv.parallel.bootstrap import bind_to_device_numa, device_local_cpus
+
+    bdf = pconv_mod.native.device_pci_bus_id(0)
+    assert re.fullmatch(r"[0-9a-f]{4}:[0-9a-f]{2}:[0-9a-f]{2}\.[0-7]", bdf), bdf
+    before = os.sched_getaffinity(0)
+    try:
+        kept = bind_to_device_numa(0)
+        after = os.sched_getaffinity(0)
+        assert after <= before
+        if kept is not None:
+            assert kept == len(after) and after <= (device_local_cpus(0) or set())
+    finally:
+        os.sched_setaffinity(0, before)
