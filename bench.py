@@ -83,11 +83,20 @@ def parse():
     p.add_argument("--emulate", default=None, metavar="WORLD:RANK",
                    help="time ONE rank of a WORLD-way split on this GPU (pre-loaded halos, no peers): a "
                         "single-GPU proxy of the per-rank step; reported as emulated, never as the headline")
+    p.add_argument("--emulate-rccl", action="store_true",
+                   help="with --emulate: also hold a 1-rank RCCL communicator during the timed region (its "
+                        "streams and queues, as a real N>1 rank has)")
     p.add_argument("--exchange-check", choices=["auto", "on", "off"], default="auto",
                    help="N>1: after the headline timing, also time the RCCL halo-exchange pipeline (ghost rows "
                         "moved GPU-to-GPU, one communicator per image slot) and compare its bytes with the "
                         "headline result; reported under 'halo_exchange' (auto: on for N>1)")
     p.add_argument("--exchange-timeout", type=float, default=60.0, help="seconds before the exchange check aborts")
+    p.add_argument("--hw-queues", type=int, default=0,
+                   help="GPU_MAX_HW_QUEUES for this process (default: max(8, slots + 3))")
+    p.add_argument("--trace", type=int, default=0, metavar="IMAGES",
+                   help="after the timed region, time the stages of IMAGES more images (needs a directly issued "
+                        "pipeline: --graph-capture off or --step-graphs off) and write them to --trace-out")
+    p.add_argument("--trace-out", default="gpurun_out/pipeline_trace.json")
     p.add_argument("--check", action="store_true",
                    help="after timing, verify every rank's band against the CPU oracle (not timed)")
     return p.parse_args()
@@ -166,9 +175,9 @@ def main():
     # One hardware queue per stream of the serving pipeline (H2D, D2H, comm and
     # one compute stream per image in flight) so independent streams never
     # alias a queue; must be set before the HIP runtime initialises.
-    want = max(8, a.slots + 3)
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < want:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(want)
+    want = a.hw_queues if a.hw_queues else max(8, a.slots + 3)
+    if a.hw_queues or int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < want:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(want, 32))
     import torch
 
     import pconv
@@ -219,6 +228,16 @@ def main():
     per_rank = gather_floats(mine)  # diagnostics: load balance across ranks
     stats = blur.stats
     mismatches = check_bands(blur, a) if a.check else None
+    if a.trace:
+        blur.pipe.enable_trace(a.trace)
+        for _ in range(a.trace):
+            blur.submit(a.reps)
+        rows = blur.pipe.trace()
+        if ctx.rank == 0:
+            os.makedirs(os.path.dirname(a.trace_out) or ".", exist_ok=True)
+            with open(a.trace_out, "w") as f:
+                json.dump({"stages": ["slot", "h2d_start", "h2d_end", "reps_end", "d2h_end"], "ms": rows,
+                           "args": vars(a)}, f)
     if a.emulate:
         world = 1
 

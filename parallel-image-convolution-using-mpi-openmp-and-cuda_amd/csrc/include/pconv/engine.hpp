@@ -209,8 +209,15 @@ class BandPipeline {
   bool concurrent() const { return concurrent_; }
   bool graphs() const { return graphs_; }
   bool step_graphs() const { return graphs_ && step_graphs_; }
+  // Stage timeline of the next `images` submits (not with captured step
+  // graphs): per image {slot, H2D start, H2D end, reps end, D2H end} in ms
+  // from the first image's H2D start, read after drain().  Timing events
+  // between the stages: a few microseconds per image of extra work.
+  void enable_trace(int images);
+  std::vector<std::vector<double>> trace();
 
  private:
+  void trace_mark(int stage, hipStream_t s);
   Stream h2d_, d2h_, comm_;
   std::vector<Stream> computes_;
   bool concurrent_ = false;
@@ -220,6 +227,9 @@ class BandPipeline {
   std::vector<Event> ev_up_, ev_done_, ev_free_, ev_halo_;
   std::vector<bool> used_;
   int64_t count_ = 0;
+  std::vector<Event> trace_ev_;  // 4 per traced image
+  std::vector<int> trace_slot_;
+  int64_t trace_first_ = 0;
 };
 
 // N row bands of one image on ONE device, halos moved by D2D copies.  Used to

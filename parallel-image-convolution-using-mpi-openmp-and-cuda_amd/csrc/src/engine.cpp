@@ -403,15 +403,21 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
     // ghost rows are not pre-loaded) through this slot's own transport, in
     // stream order between the upload and the launches.
     const bool preloaded = in_r0 < 0 || in_r1 > e.band().rows;
+    hipStream_t cs = e.compute_stream();
+    trace_mark(0, cs);
     e.upload_rows(host_in, e.layout().row_bytes, in_r0, in_r1);
+    trace_mark(1, cs);
     e.set_halo_valid(preloaded);
     e.run(reps);
+    trace_mark(2, cs);
     e.download_rows(host_out, e.layout().row_bytes, 0, e.band().rows);
+    trace_mark(3, cs);
     used_[k] = true;
     ++count_;
     return;
   }
   if (graphs_) {
+    PCONV_CHECK(trace_ev_.empty(), "pipeline trace needs directly issued images (graph capture off)");
     e.process_graph(host_in, in_r0, in_r1, host_out, reps);
     used_[k] = true;
     ++count_;
@@ -419,7 +425,9 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   }
   // H2D into slot k once its previous image has been downloaded.
   if (used_[k]) ev_free_[k].wait_on(h2d_.get());
+  trace_mark(0, h2d_.get());
   e.upload_rows(host_in, e.layout().row_bytes, in_r0, in_r1, h2d_.get());
+  trace_mark(1, h2d_.get());
   ev_up_[k].record(h2d_.get());
   const bool preloaded = in_r0 < 0 || in_r1 > e.band().rows;
   e.set_halo_valid(preloaded);
@@ -435,13 +443,42 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   }
   // reps on the shared compute stream (later exchanges on the comm stream)
   e.run(reps);
+  trace_mark(2, e.compute_stream());
   ev_done_[k].record(e.compute_stream());
   // D2H of the owned rows
   ev_done_[k].wait_on(d2h_.get());
   e.download_rows(host_out, e.layout().row_bytes, 0, e.band().rows, d2h_.get());
+  trace_mark(3, d2h_.get());
   ev_free_[k].record(d2h_.get());
   used_[k] = true;
   ++count_;
+}
+
+void BandPipeline::enable_trace(int images) {
+  PCONV_CHECK(images >= 0, "trace capacity must be >= 0");
+  PCONV_CHECK(!step_graphs(), "pipeline trace needs directly issued images (graph capture off)");
+  trace_ev_.clear();
+  trace_slot_.clear();
+  for (int i = 0; i < 4 * images; ++i) trace_ev_.push_back(Event::create(true));
+  trace_first_ = count_;
+}
+
+void BandPipeline::trace_mark(int stage, hipStream_t s) {
+  const int64_t i = count_ - trace_first_;
+  if (i < 0 || 4 * i + 3 >= static_cast<int64_t>(trace_ev_.size())) return;
+  if (stage == 0) trace_slot_.push_back(static_cast<int>(count_ % static_cast<int64_t>(slots_.size())));
+  trace_ev_[4 * i + stage].record(s);
+}
+
+std::vector<std::vector<double>> BandPipeline::trace() {
+  drain();
+  std::vector<std::vector<double>> out;
+  for (size_t i = 0; i < trace_slot_.size(); ++i) {
+    std::vector<double> row{static_cast<double>(trace_slot_[i])};
+    for (int st = 0; st < 4; ++st) row.push_back(Event::elapsed_ms(trace_ev_[0], trace_ev_[4 * i + st]));
+    out.push_back(row);
+  }
+  return out;
 }
 
 void BandPipeline::drain() {

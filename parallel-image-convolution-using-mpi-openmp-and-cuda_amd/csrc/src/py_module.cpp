@@ -525,7 +525,11 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_property_readonly("submitted", &BandPipeline::submitted)
       .def_property_readonly("concurrent", &BandPipeline::concurrent)
       .def_property_readonly("graphs", &BandPipeline::graphs)
-      .def_property_readonly("step_graphs", &BandPipeline::step_graphs);
+      .def_property_readonly("step_graphs", &BandPipeline::step_graphs)
+      .def("enable_trace", &BandPipeline::enable_trace, py::arg("images"),
+           "Time the stages of the next `images` submits (directly issued pipelines only)")
+      .def("trace", &BandPipeline::trace, py::call_guard<py::gil_scoped_release>(),
+           "Per traced image: [slot, H2D start, H2D end, reps end, D2H end] in ms");
 
   py::class_<LocalCluster>(m, "LocalCluster")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int bands, int device, int halo,
