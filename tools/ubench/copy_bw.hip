@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #define CHECK(x)                                                        \
@@ -28,7 +29,10 @@ __global__ void k_copy_rows(const uint8_t* __restrict__ src, size_t sp, uint8_t*
 }
 
 int main(int argc, char** argv) {
-  const size_t W = 5760, H = 2520, P = 5888;  // 1920x2520 RGB row bytes, frame pitch
+  // 1920x2520 RGB row bytes, frame pitch; optional argv[1] = rows (e.g. 395:
+  // one rank's band + ghost rows of the 8-way split), argv[2] = iterations.
+  const size_t W = 5760, P = 5888;
+  const size_t H = argc > 1 ? static_cast<size_t>(atol(argv[1])) : 2520;
   const size_t bytes = W * H;
   void *h_in, *h_out, *d_a, *d_b;
   CHECK(hipHostMalloc(&h_in, bytes, 0));
@@ -41,7 +45,8 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  const int iters = 20;
+  const int iters = argc > 2 ? atoi(argv[2]) : 20;
+  printf("rows %zu, %.2f MB per copy, %d iterations\n", H, W * H / 1e6, iters);
   auto report = [&](const char* name, float ms, double gb) {
     printf("%-34s %8.3f ms/iter  %6.1f GB/s\n", name, ms / iters, gb * iters / (ms * 1e-3));
   };
