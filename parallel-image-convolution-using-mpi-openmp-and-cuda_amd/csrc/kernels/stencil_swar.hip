@@ -42,6 +42,7 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <type_traits>
 
 #include "pconv/device.hpp"
 #include "swar.hpp"
@@ -338,6 +339,164 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
   }
 }
 
+// Row-streaming form of the same fused gaussian, for large frames.
+//
+// The tile kernel above pays for its independence with a trapezoid: a
+// 64-row tile advanced 8 steps keeps only 48 rows (25 % of its arithmetic is
+// halo), and every step ends at a workgroup barrier.  Here one wave owns a
+// column-strip pair (the same pair layout and DPP taps as k_swar) and walks
+// DOWN a segment of rows, holding T time levels as rolling row sums in
+// registers: each input row it loads climbs all T levels at once (level t
+// emits row i - 2t + 1, levels skewed by one row for ILP), and the last
+// level's row is stored.  Vertical redundancy
+// is only the 2T-row run-in/run-out of each segment (a few %), there is no
+// LDS and no barrier — waves are independent; loads are prefetched two rows
+// ahead.  Per pair per level: 2 ops horizontal, 2 vertical, 2 (or, with ALT,
+// 1.5 on average) truncation — the tile kernel's arithmetic without its halo
+// rows.  Chosen by the tuner where it wins (large frames; small bands leave
+// too few segments to fill the chip).
+template <int CH, int NP, int T, bool ALT>
+__global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                int64_t pitch, int64_t dst_pitch, int row_bytes, int r0, int r1,
+                                                int g_row0, int height, int nstrips, int pair_stride, int seg_rows,
+                                                int nwaves) {
+  static_assert(!ALT || T % 2 == 0, "paired levels need an even level count");
+  using CT = typename Chunk<NP>::T;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + (static_cast<int>(threadIdx.x) >> 6));
+  if (wid >= nwaves) return;  // whole wave (uniform)
+  constexpr int hl = (T * CH + NP - 1) / NP;  // halo lanes per side
+  constexpr int vbytes = (64 - 2 * hl) * NP;
+  const int col = wid % pair_stride, seg = wid / pair_stride;
+  const int sA = col, sB = col + pair_stride;
+  const bool hasB = sB < nstrips;
+  const int baseA = sA * vbytes - hl * NP, baseB = sB * vbytes - hl * NP;
+  const int xA = baseA + lane * NP, xB = baseB + lane * NP;
+  const int validA = (xA >= 0) ? min(max(row_bytes - xA, 0), NP) : 0;
+  const int validB = (hasB && xB >= 0) ? min(max(row_bytes - xB, 0), NP) : 0;
+  const bool needs_mask = baseA < 0 || baseA + 64 * NP > row_bytes || !hasB || baseB + 64 * NP > row_bytes;
+  u32 cm[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) cm[k] = (k < validA ? 0xffffu : 0u) | (k < validB ? 0xffff0000u : 0u);
+
+  const int s0 = r0 + seg * seg_rows;
+  const int s1 = min(r1, s0 + seg_rows);
+  const int lo_ok = max(r0 - T, -g_row0), hi_ok = min(r1 + T, height - g_row0);
+  const int img_lo = -g_row0, img_hi = height - g_row0;  // frame rows inside the image
+  const int st_hi = min(s1, img_hi);
+  const bool lane_in = lane >= hl && lane < 64 - hl;
+  const bool stA = lane_in && validA > 0, stB = lane_in && validB > 0;
+
+  auto load = [&](int fr, CT& a, CT& b) {
+    a = Chunk<NP>::zero();
+    b = Chunk<NP>::zero();
+    if (fr >= lo_ok && fr < hi_ok) {
+      const uint8_t* rowp = src + static_cast<int64_t>(fr) * pitch;
+      if (validA > 0) a = *reinterpret_cast<const CT*>(rowp + xA);
+      if (validB > 0) b = *reinterpret_cast<const CT*>(rowp + xB);
+    }
+  };
+
+  // Rolling state per level, double-buffered by row parity so the unrolled
+  // two-row body never copies registers: level t holds Hc = horizontal sum
+  // of its previous input row and Sc = that of the two previous rows.
+  // Levels are SKEWED: level t consumes the row level t-1 emitted in the
+  // PREVIOUS iteration (Y[t-1]), so the T levels of one iteration are
+  // independent (T x NP-way ILP instead of a T-long dependency chain); level
+  // t emits row i - 2t + 1 at iteration i.
+  u32 S[2][T][NP], H[2][T][NP], Y[T][NP];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int k = 0; k < NP; ++k) S[0][t][k] = H[0][t][k] = Y[t][k] = 0u;
+  // Input rows are prefetched PF rows ahead (a ring of PF raw rows): one
+  // row's T levels are ~T x 6 x NP instructions, far less than a load's
+  // latency from HBM.
+  constexpr int PF = 8;
+  CT ra[PF], rb[PF];
+  const int i0 = s0 - T, iend = s1 + 2 * T - 1;
+#pragma unroll
+  for (int q = 0; q < PF; ++q) load(i0 + q, ra[q], rb[q]);
+
+  auto row = [&](auto slot_c, auto safe_c, int i) {
+    constexpr int Q = decltype(slot_c)::value;
+    constexpr int P = Q & 1;  // state parity (PF is even, so parity follows the slot)
+    constexpr bool SAFE = decltype(safe_c)::value;  // every emitted row inside the image, no edge columns
+    u32 X0[NP];
+    unpack<NP>(ra[Q], rb[Q], X0);
+    load(i + PF, ra[Q], rb[Q]);
+    // Highest level first: level t reads Y[t-1] before level t-1 replaces it.
+#pragma unroll
+    for (int t = T - 1; t >= 0; --t) {
+      u32 Hn[NP], X[NP];
+      if (t == 0)
+        horiz<CH, NP>(X0, Hn);
+      else
+        horiz<CH, NP>(Y[t - 1], Hn);
+      const int j = i - 2 * t - 1;  // row emitted by level t + 1
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const u32 Sn = H[P][t][k] + Hn[k];
+        const u32 sum = S[P][t][k] + Sn;
+        if constexpr (!ALT)
+          X[k] = trunc_sum<0>(sum);
+        else  // unrolled: the level parity folds at compile time
+          X[k] = ((T - 1 - t) & 1) ? trunc_sum<1>(sum) /* keeps 16 x floor */ : trunc_sum<2>(sum);
+        S[P ^ 1][t][k] = Sn;
+        H[P ^ 1][t][k] = Hn[k];
+      }
+      if constexpr (!SAFE) {
+        if (j < img_lo || j >= img_hi) {
+#pragma unroll
+          for (int k = 0; k < NP; ++k) X[k] = 0u;
+        }
+        if (needs_mask) {
+#pragma unroll
+          for (int k = 0; k < NP; ++k) X[k] &= cm[k];
+        }
+      }
+      if (t < T - 1) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) Y[t][k] = X[k];
+      } else if (j >= s0 && j < st_hi) {  // the last level's row is finished
+        CT a, b;
+        pack<NP>(X, a, b);
+        uint8_t* rowq = dst + static_cast<int64_t>(j) * dst_pitch;
+        if (stA) {
+          if (validA == NP)
+            *reinterpret_cast<CT*>(rowq + xA) = a;
+          else
+            store_bytes<NP>(rowq + xA, a, validA);
+        }
+        if (stB) {
+          if (validB == NP)
+            *reinterpret_cast<CT*>(rowq + xB) = b;
+          else
+            store_bytes<NP>(rowq + xB, b, validB);
+        }
+      }
+    }
+  };
+  using Safe = std::true_type;
+  using Edge = std::false_type;
+  static_assert(PF == 8, "the block below unrolls 8 ring slots");
+  auto block = [&](auto safe_c, int i, bool partial) {
+    // PF consecutive rows, ring slots 0..PF-1 (compile-time indices)
+#define PCONV_STREAM_ROW(Q_) \
+  if (!partial || i + Q_ < iend) row(std::integral_constant<int, Q_>{}, safe_c, i + Q_);
+    PCONV_STREAM_ROW(0) PCONV_STREAM_ROW(1) PCONV_STREAM_ROW(2) PCONV_STREAM_ROW(3)
+    PCONV_STREAM_ROW(4) PCONV_STREAM_ROW(5) PCONV_STREAM_ROW(6) PCONV_STREAM_ROW(7)
+#undef PCONV_STREAM_ROW
+  };
+  int i = i0;
+  // Run-in near the image top / edge strips: per-level zero rows and masks.
+  for (; i < iend && (needs_mask || i - 2 * T + 1 < img_lo); i += PF) block(Edge{}, i, true);
+  // Body: every level's row inside the image (rows i - 2T + 1 .. i + PF - 1).
+  const int safe_end = min(iend, img_hi);
+  for (; i + PF <= safe_end; i += PF) block(Safe{}, i, false);
+  for (; i < iend; i += PF) block(Edge{}, i, true);
+}
+
 // Instantiated tile shapes (LW, M, NW).
 constexpr SwarShape kShapes[] = {
     {8, 8, 8}, {8, 8, 4}, {8, 16, 4}, {8, 4, 8},              // 8-byte lanes: large images
@@ -365,6 +524,22 @@ int alt_mode() {
     const char* e = std::getenv("PCONV_SWAR_ALT");
     v = !e ? -1 : e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
     g_alt_mode.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+
+// Off by default: measured slower than the tile kernel on every geometry
+// (16384^2 grey 43.7 vs 37.1 us/rep: ~190 VGPRs leave 2 waves per SIMD and
+// the level chain is latency-bound; docs/PERFORMANCE.md).  PCONV_STREAM=-1
+// lets the tuner time it, =1 forces it (tests).
+std::atomic<int> g_stream_mode{-2};  // -2: PCONV_STREAM on first use; -1 tune, 0 off, 1 forced
+
+int stream_mode() {
+  int v = g_stream_mode.load(std::memory_order_relaxed);
+  if (v == -2) {
+    const char* e = std::getenv("PCONV_STREAM");
+    v = !e ? 0 : e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
+    g_stream_mode.store(v, std::memory_order_relaxed);
   }
   return v;
 }
@@ -422,6 +597,87 @@ void launch_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh, bool alt) {
   PCONV_SWAR(8, 4, 16)
 #undef PCONV_SWAR
   PCONV_FAIL("swar temporal kernel: unsupported tile shape");
+}
+
+// Row-streaming launches: (NP, T) instantiations, T = the launch's steps.
+struct StreamCfg {
+  int np = 0;    // 0: tile kernel
+  int segf = 1;  // waves per resident slot (segments = resident waves x segf / strip pairs)
+};
+
+template <int CH, int NP, int T>
+const void* stream_fn(bool alt) {
+  return alt ? reinterpret_cast<const void*>(&k_stream<CH, NP, T, true>)
+             : reinterpret_cast<const void*>(&k_stream<CH, NP, T, false>);
+}
+
+// Resident waves per SIMD of one instantiation (VGPR-bound; no LDS).
+int stream_occupancy(const void* fn) {
+  static std::mutex mu;
+  static std::map<const void*, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(fn);
+  if (it != cache.end()) return it->second;
+  hipFuncAttributes at{};
+  int occ = 4;
+  if (hipFuncGetAttributes(&at, fn) == hipSuccess && at.numRegs > 0) {
+    occ = std::max(1, std::min(8, 512 / round_up(at.numRegs, 8)));
+    cache.emplace(fn, occ);
+  } else {
+    (void)hipGetLastError();
+  }
+  return occ;
+}
+
+struct StreamGrid {
+  int nstrips = 0, pair_stride = 0, seg_rows = 0, nseg = 0, nwaves = 0;
+};
+
+StreamGrid stream_grid(int ch, int np, int t, int64_t rows, int64_t row_bytes, int occ, int segf) {
+  StreamGrid g;
+  const int hl = (t * ch + np - 1) / np;
+  const int vbytes = (64 - 2 * hl) * np;
+  if (vbytes <= 0 || rows <= 0) return g;
+  g.nstrips = static_cast<int>(ceil_div<int64_t>(row_bytes, vbytes));
+  g.pair_stride = (g.nstrips + 1) / 2;
+  const int64_t target = int64_t(1024) * occ * std::max(1, segf);  // 256 CUs x 4 SIMDs x resident waves
+  const int64_t nseg_want = std::max<int64_t>(1, target / g.pair_stride);
+  g.seg_rows = static_cast<int>(std::max<int64_t>(ceil_div<int64_t>(rows, nseg_want), 2 * t));
+  g.nseg = static_cast<int>(ceil_div<int64_t>(rows, g.seg_rows));
+  g.nwaves = g.pair_stride * g.nseg;
+  return g;
+}
+
+template <int CH, int NP, int T>
+void launch_stream_one(const StencilLaunch& a, hipStream_t s, bool alt, int segf) {
+  PCONV_CHECK(a.steps == T, "stream kernel: steps must equal its level count");
+  const int occ = stream_occupancy(stream_fn<CH, NP, T>(alt));
+  const StreamGrid g = stream_grid(CH, NP, T, a.r1 - a.r0, a.row_bytes, occ, segf);
+  PCONV_CHECK(g.nwaves > 0, "stream kernel: empty launch");
+  const dim3 grid(static_cast<unsigned>(ceil_div(g.nwaves, 4)));
+  const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
+  const int64_t dp = a.dst_pitch ? a.dst_pitch : a.pitch;
+  if (alt)
+    k_stream<CH, NP, T, true><<<grid, dim3(256), 0, s>>>(a.src, a.dst, a.pitch, dp, static_cast<int>(a.row_bytes),
+                                                         static_cast<int>(a.r0), static_cast<int>(a.r1),
+                                                         static_cast<int>(a.g_row0), static_cast<int>(hmax), g.nstrips,
+                                                         g.pair_stride, g.seg_rows, g.nwaves);
+  else
+    k_stream<CH, NP, T, false><<<grid, dim3(256), 0, s>>>(a.src, a.dst, a.pitch, dp, static_cast<int>(a.row_bytes),
+                                                          static_cast<int>(a.r0), static_cast<int>(a.r1),
+                                                          static_cast<int>(a.g_row0), static_cast<int>(hmax), g.nstrips,
+                                                          g.pair_stride, g.seg_rows, g.nwaves);
+}
+
+// Instantiated (NP, T): 4-byte lanes, 8 levels (~190 VGPRs: the rolling
+// state of 8 levels x 4 pairs, double-buffered, plus an 8-row load ring);
+// 16 levels or 8-byte lanes do not fit the register file.
+bool stream_supported(int ch, int np, int steps) { return np >= ch && np == 4 && steps == 8; }
+
+template <int CH>
+void launch_stream_ch(const StencilLaunch& a, hipStream_t s, StreamCfg c, bool alt) {
+  if (c.np == 4 && a.steps == 8) return launch_stream_one<CH, 4, 8>(a, s, alt, c.segf);
+  PCONV_FAIL("stream kernel: unsupported (lanes, steps)");
 }
 
 bool known_shape(const SwarShape& s) {
@@ -547,6 +803,7 @@ KernelRes kernel_res(SwarShape sh, int ch, bool alt) {
 // best shape in 6 of 6 configurations of the current kernel.
 void set_xcd_swizzle(bool on) { g_xcd_swizzle.store(on ? 1 : 0, std::memory_order_relaxed); }
 void set_swar_alt(int mode) { g_alt_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
+void set_stream_mode(int mode) { g_stream_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
 
 SwarResources swar_resources(SwarShape s, int ch) {
   const KernelRes r = kernel_res(s, ch, default_alt());
@@ -601,9 +858,18 @@ namespace {
 struct SwarChoice {
   SwarShape shape;
   bool alt = true;
+  StreamCfg stream;  // np > 0: row-streaming kernel instead of the tile kernel
 };
 
 void launch_choice(const StencilLaunch& a, Channels ch, hipStream_t stream, SwarChoice c) {
+  if (c.stream.np > 0) {
+    switch (ch) {
+      case Channels::Grey: launch_stream_ch<1>(a, stream, c.stream, c.alt); break;
+      case Channels::Rgb: launch_stream_ch<3>(a, stream, c.stream, c.alt); break;
+      case Channels::Rgba: launch_stream_ch<4>(a, stream, c.stream, c.alt); break;
+    }
+    return;
+  }
   switch (ch) {
     case Channels::Grey: launch_ch<1>(a, stream, c.shape, c.alt); break;
     case Channels::Rgb: launch_ch<3>(a, stream, c.shape, c.alt); break;
@@ -651,6 +917,11 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   const int mode = alt_mode();
   SwarChoice fallback;
   fallback.alt = default_alt();
+  if (stream_mode() == 1 && !autotune_enabled() && stream_supported(c, 4, a.steps)) {
+    fallback.shape = pick_swar_shape(a.steps, c, rows, a.row_bytes);
+    fallback.stream = StreamCfg{4, 1};  // forced streaming kernel, untuned
+    return fallback;
+  }
   if (override_shape(fallback.shape) || !autotune_enabled()) {
     if (!override_shape(fallback.shape)) fallback.shape = pick_swar_shape(a.steps, c, rows, a.row_bytes);
     return fallback;
@@ -678,7 +949,27 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   std::vector<SwarChoice> cands;
   for (const auto& r : ranked)
     for (int alt = 0; alt <= 1; ++alt)
-      if (mode < 0 || mode == alt) cands.push_back(SwarChoice{r.second, alt == 1});
+      if (mode < 0 || mode == alt) cands.push_back(SwarChoice{r.second, alt == 1, StreamCfg{}});
+  // Row-streaming candidates where the segments stay long against their
+  // 2T-row run-in (large frames / bands): 8 segments' worth of rows per
+  // strip pair at least.
+  if (stream_mode() != 0) {
+    for (int np : {4}) {
+      if (!stream_supported(c, np, a.steps)) continue;
+      for (int segf : {1, 2}) {
+        const StreamGrid g = stream_grid(c, np, a.steps, rows, a.row_bytes, 4, segf);
+        if (g.nwaves == 0 || (stream_mode() != 1 && g.seg_rows < 8 * a.steps)) continue;
+        for (int alt = 0; alt <= 1; ++alt)
+          if (mode < 0 || mode == alt) cands.push_back(SwarChoice{fallback.shape, alt == 1, StreamCfg{np, segf}});
+      }
+    }
+    if (stream_mode() == 1) {  // forced: only streaming candidates (tests / A-B)
+      std::vector<SwarChoice> only;
+      for (const auto& x : cands)
+        if (x.stream.np > 0) only.push_back(x);
+      if (!only.empty()) cands.swap(only);
+    }
+  }
   SwarChoice best = cands.front();
   if (cands.size() > 1) {
     Event e0 = Event::create(true), e1 = Event::create(true);
@@ -714,7 +1005,8 @@ std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned() {
   std::lock_guard<std::mutex> lk(g_tune_mu);
   std::vector<std::pair<std::vector<int64_t>, SwarShape>> out;
   for (const auto& kv : g_tuned)
-    out.push_back({{kv.first.ch, kv.first.steps, kv.first.rows, kv.first.row_bytes, kv.second.alt ? 1 : 0},
+    out.push_back({{kv.first.ch, kv.first.steps, kv.first.rows, kv.first.row_bytes, kv.second.alt ? 1 : 0,
+                    kv.second.stream.np, kv.second.stream.segf},
                    kv.second.shape});
   return out;
 }

@@ -29,7 +29,8 @@ void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
 void prepare_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
 void set_autotune(bool on);
 void clear_swar_tuning();
-// Tuned entries: ({channels, steps, rows, row_bytes, paired_form}, shape).
+// Tuned entries: ({channels, steps, rows, row_bytes, paired_form, stream_lanes, stream_segf}, shape);
+// stream_lanes > 0: the row-streaming kernel won (shape unused).
 std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned();
 
 // Force a tile shape (lw = 0 restores the model) and list the instantiated ones.
@@ -48,5 +49,8 @@ void set_xcd_swizzle(bool on);
 // Step form: -1 tuned per launch geometry (default), 0 truncate every step,
 // 1 steps in pairs with a scale-16 intermediate (PCONV_SWAR_ALT=0/1).
 void set_swar_alt(int mode);
+// Row-streaming kernel: -1 among the tuned candidates, 0 never (default:
+// measured slower), 1 forced where it applies (PCONV_STREAM=-1/0/1).
+void set_stream_mode(int mode);
 
 }  // namespace pconv

@@ -331,6 +331,9 @@ PYBIND11_MODULE(_pconv_native, m) {
       out.append(py::make_tuple(py::cast(kv.first), py::make_tuple(kv.second.lw, kv.second.m, kv.second.nw)));
     return out;
   });
+  m.def("set_stream_mode", &set_stream_mode, py::arg("mode"),
+        "Row-streaming temporal kernel: -1 tuned against the tile kernel, 0 never (default), 1 forced where it "
+        "applies (8-step launches)");
   m.def("set_swar_alt", &set_swar_alt, py::arg("mode"),
         "SWAR step form: -1 tuned (default), 0 truncate every step, 1 pairs of steps with a x16 intermediate.");
   m.def("set_xcd_swizzle", &set_xcd_swizzle, py::arg("on"),
