@@ -43,6 +43,7 @@ void pwrite_all(int fd, const uint8_t* src, int64_t n, int64_t off, const std::s
       if (errno == EINTR) continue;
       PCONV_FAIL("write " + path + ": " + errno_str());
     }
+    if (r == 0) PCONV_FAIL("write " + path + ": no progress at byte " + std::to_string(off + done));
     done += r;
   }
 }
