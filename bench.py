@@ -26,9 +26,11 @@ comparison with the headline result — measured after the headline's timed
 region, bounded by --exchange-timeout, never fatal for the headline line.
 Measured on one GPU (tools: --emulate), preload is the faster per-rank step:
 the 40-row ghost zone costs ~25% more H2D at N=8, the exchange path costs
-more host API calls and RCCL latency per image.  The RCCL communicator is
-created in both modes and reduces the elapsed time (max over ranks, the
-reference's MPI_Send/Recv max-gather).
+more host API calls and RCCL latency per image.  In preload mode the headline
+pipeline holds no communicator at all (its images are exchange-free); the
+elapsed time is reduced with a gloo all-reduce (max over ranks, the
+reference's MPI_Send/Recv max-gather).  The halo_exchange measurement runs
+under a watchdog, so it can never take the headline line down with it.
 value = W*H*reps*steps / max-over-ranks elapsed / 1e6 (whole-job Mpix/s).
 Extra fields report the device-resident loop alone (no PCIe copies).
 
@@ -91,6 +93,10 @@ def parse():
                         "moved GPU-to-GPU, one communicator per image slot) and compare its bytes with the "
                         "headline result; reported under 'halo_exchange' (auto: on for N>1)")
     p.add_argument("--exchange-timeout", type=float, default=60.0, help="seconds before the exchange check aborts")
+    p.add_argument("--watchdog", type=float, default=None,
+                   help="seconds the whole halo_exchange measurement may take, communicator set-up included, "
+                        "before every rank exits with the headline line printed (default 2 x timeout + 30)")
+    p.add_argument("--stall-exchange", action="store_true", help=argparse.SUPPRESS)  # tests: a hung peer
     p.add_argument("--hw-queues", type=int, default=0,
                    help="GPU_MAX_HW_QUEUES for this process (default: max(8, slots + 3))")
     p.add_argument("--trace", type=int, default=0, metavar="IMAGES",
@@ -143,6 +149,8 @@ def exchange_check(a, blur, world, rank, device, transport):
     from pconv.parallel.dist_engine import DistributedBlur
 
     res = {"transport": transport, "status": "ok"}
+    if a.stall_exchange and rank == world - 1:  # tests: the last rank never joins
+        time.sleep(3600)
     try:
         xb = DistributedBlur(a.width, a.height, a.channels, a.filter, a.reps, rank=rank, world=world, device=device,
                              halo=a.halo, fuse=a.fuse, preload_halo=False, slots=a.slots, variant=a.variant,
@@ -191,11 +199,16 @@ def main():
     rank = ctx.rank
     transport = a.transport
     a.preload_halo = a.preload_halo or a.halo_mode == "preload"
+    # Pre-loaded ghost rows make every image exchange-free: the headline
+    # pipeline then needs no communicator (the max over ranks goes through
+    # gloo), so an RCCL problem can only affect the secondary halo_exchange
+    # measurement, never the headline line.
+    head_transport = "none" if (a.preload_halo and world > 1) else transport
     if a.emulate:
         if world != 1:
             raise SystemExit("--emulate runs in a single process")
         world, rank = (int(v) for v in a.emulate.split(":"))
-        a.preload_halo, transport = True, "none"
+        a.preload_halo, transport, head_transport = True, "none", "none"
     device = ctx.local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     # host thread + first-touch pinned buffers on the GPU's own socket
@@ -204,10 +217,17 @@ def main():
     blur = DistributedBlur(a.width, a.height, a.channels, a.filter, a.reps, rank=rank, world=world,
                            device=device, halo=a.halo, fuse=a.fuse, overlap=not a.no_overlap,
                            preload_halo=a.preload_halo, slots=a.slots, variant=a.variant,
-                           transport=transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
+                           transport=head_transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
                            step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
                            zero_copy_out=a.zero_copy_out == "on", graph_capture=a.graph_capture == "on")
     blur.load_synthetic(a.seed)
+    # --emulate-rccl: hold a (1-rank) RCCL communicator through the timed
+    # region, as every real N>1 rank of the exchange path does.
+    held_comm = None
+    if a.emulate and a.emulate_rccl:
+        from pconv.parallel.bootstrap import make_rccl_comm
+
+        held_comm = make_rccl_comm(device)
 
     for _ in range(a.warmup):
         blur.submit(a.reps)
@@ -224,7 +244,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     mine = time.perf_counter() - t0
-    elapsed = blur.comm.allreduce_max(mine) if blur.comm is not None else max_over_ranks(mine)
+    elapsed = max_over_ranks(mine)
     per_rank = gather_floats(mine)  # diagnostics: load balance across ranks
     stats = blur.stats
     mismatches = check_bands(blur, a) if a.check else None
@@ -262,13 +282,10 @@ def main():
     barrier()
     loop_elapsed = max_over_ranks(time.perf_counter() - t1)
 
-    halo_exchange = None
-    if world > 1 and not a.emulate and (a.exchange_check == "on" or (a.exchange_check == "auto" and world > 1)):
-        halo_exchange = exchange_check(a, blur, world, rank, device, transport)
-
     px = a.width * a.height * a.reps
     value = px * a.steps / elapsed / 1e6
     loop_value = px * ls / loop_elapsed / 1e6 if ls else None
+    out = None
     if ctx.rank == 0:
         out = {
             "metric": METRIC,
@@ -307,19 +324,49 @@ def main():
                 "us_per_rep": round(loop_elapsed / ls / a.reps * 1e6, 3) if ls else None,
             },
             "device": torch.cuda.get_device_name(device),
-            "rccl": pconv.native.rccl_version() if world > 1 else None,
+            "rccl": pconv.native.rccl_version() if world > 1 or held_comm is not None else None,
+            "headline_transport": head_transport if world > 1 else None,
             "pconv": pconv.__version__,
             "per_rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in per_rank],
             "rank0_cpus_bound": cpu_bind,
         }
         if mismatches is not None:
             out["mismatches"] = mismatches
-        if halo_exchange is not None:
-            out["halo_exchange"] = halo_exchange
         if a.emulate:
             out["emulated"] = f"rank {rank} of a {a.emulate.split(':')[0]}-way split on one GPU; value = this " \
                               "rank's step rate x full-image pixels (proxy, not a multi-GPU measurement)"
-        print(json.dumps(out), flush=True)
+
+    import threading
+
+    emit_lock = threading.Lock()
+    emitted = []
+
+    def emit(line):  # the one JSON line, printed once whichever path gets here first
+        with emit_lock:
+            if line is not None and not emitted:
+                print(json.dumps(line), flush=True)
+                emitted.append(True)
+
+    if world > 1 and not a.emulate and (a.exchange_check == "on" or (a.exchange_check == "auto" and world > 1)):
+        # Secondary measurement after the headline is final.  A watchdog on
+        # every rank bounds it (communicator set-up included): on expiry rank
+        # 0 prints the headline line with the exchange marked as timed out and
+        # every rank exits, so a stuck peer can never cost the headline.
+        def expire():
+            if out is not None:
+                emit(dict(out, halo_exchange={"transport": transport, "status": "watchdog timeout"}))
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+
+        dog = threading.Timer(a.watchdog if a.watchdog is not None else 2 * a.exchange_timeout + 30.0, expire)
+        dog.daemon = True
+        dog.start()
+        halo_exchange = exchange_check(a, blur, world, rank, device, transport)
+        dog.cancel()
+        if out is not None:
+            out["halo_exchange"] = halo_exchange
+    emit(out)
     shutdown(ctx)
 
 

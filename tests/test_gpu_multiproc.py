@@ -95,6 +95,32 @@ def test_bench_torchrun_rehearsal(world, extra):
     assert hx["mismatches_vs_headline"] == 0 and hx["exchanges_per_step"] >= 1
 
 
+def test_bench_exchange_watchdog():
+    """A peer that never joins the secondary halo_exchange measurement: the
+    watchdog still prints the headline line (exchange marked timed out) and
+    every rank exits 0, so the driver's N-GPU run always yields its number."""
+    import json
+    import subprocess
+    import sys
+    import time
+
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--transport", "gloo-host", "--stall-exchange",
+           "--watchdog", "8"]
+    t0 = time.time()
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    meta = json.loads(lines[0])
+    assert meta["n_gpus"] == 2 and meta["value"] > 0
+    assert meta["halo_exchange"]["status"] == "watchdog timeout"
+    assert meta["headline_transport"] == "none"
+    assert time.time() - t0 < 250
+
+
 @pytest.mark.parametrize("world,extra", [(2, []), (3, ["--exchange-halo", "--halo", "3", "--fuse", "3"]),
                                          (2, ["--filter", "box"])])
 def test_torchrun_per_rank_program_hip(pconv_mod, tmp_path, world, extra):
