@@ -80,6 +80,8 @@ class BandEngine {
   const Filter& filter() const { return filter_; }
   const FrameLayout& layout() const { return lay_; }
   const EngineOptions& options() const { return opt_; }
+  static constexpr size_t kMaxCachedGraphs = 64;
+  size_t cached_graphs() const { return graphs_.size() + step_graphs_.size(); }
   hipStream_t compute_stream() const { return cs_; }
   hipStream_t comm_stream() const { return ms_; }
 
@@ -169,7 +171,10 @@ class BandEngine {
     int launches = 0;
     bool zero_copy = false;
   };
-  // (reps, start buffer, in, in_r0, in_r1, out) -> whole-step graph
+  // (reps, start buffer, in, in_r0, in_r1, out) -> whole-step graph.  Keyed
+  // on host pointers, so both caches are bounded: past kMaxCachedGraphs
+  // entries the stream is drained and the cache is emptied.
+  void trim_graph_caches();
   std::map<std::tuple<int, int, const uint8_t*, int64_t, int64_t, uint8_t*>, StepGraph> step_graphs_;
 };
 

@@ -60,10 +60,20 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
 }
 
 BandEngine::~BandEngine() {
+  // Drain first: a cached graph may still be executing on the stream.
+  if (cs_) (void)hipStreamSynchronize(cs_);
+  if (ms_ && ms_ != cs_) (void)hipStreamSynchronize(ms_);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : step_graphs_) (void)hipGraphExecDestroy(kv.second.exec);
-  if (cs_) (void)hipStreamSynchronize(cs_);
-  if (ms_) (void)hipStreamSynchronize(ms_);
+}
+
+void BandEngine::trim_graph_caches() {
+  if (graphs_.size() < kMaxCachedGraphs && step_graphs_.size() < kMaxCachedGraphs) return;
+  PCONV_HIP_CHECK(hipStreamSynchronize(cs_));  // no cached graph may still be running
+  for (auto& kv : graphs_) PCONV_HIP_CHECK(hipGraphExecDestroy(kv.second));
+  for (auto& kv : step_graphs_) PCONV_HIP_CHECK(hipGraphExecDestroy(kv.second.exec));
+  graphs_.clear();
+  step_graphs_.clear();
 }
 
 void BandEngine::clear() {
@@ -218,6 +228,7 @@ void BandEngine::run(int reps) {
     const auto key = std::make_pair(reps, cur_);
     auto it = graphs_.find(key);
     if (it == graphs_.end()) {
+      trim_graph_caches();
       hipGraph_t g = nullptr;
       prepare(ph);
       PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeThreadLocal));
@@ -264,6 +275,7 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
   auto it = step_graphs_.find(key);
   stats_ = RunStats{};
   if (it == step_graphs_.end()) {
+    trim_graph_caches();
     const int64_t rb = lay_.row_bytes;
     hipGraph_t g = nullptr;
     // Zero-copy output: the last launch must produce exactly the owned rows

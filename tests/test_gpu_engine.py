@@ -32,6 +32,21 @@ def test_convolve_hip_tensor(pconv_mod, rng, filt):
     assert np.array_equal(x.cpu().numpy(), img)  # input untouched
 
 
+def test_engine_graph_cache_bounded(pconv_mod, rng):
+    """Graphs are cached per (reps, start buffer): many distinct repetition
+    counts must not grow the cache past its bound, and results stay exact
+    across the eviction."""
+    eng = pconv_mod.Engine(37, 29, "grey", device=0, fuse=4, graph=True)
+    cap = eng._eng.max_cached_graphs
+    img = rng.integers(0, 256, size=(29, 37), dtype=np.uint8)
+    for reps in range(1, cap + 12):
+        got = eng.run_numpy(img, reps)
+        assert eng._eng.cached_graphs <= cap
+        if reps in (1, cap - 1, cap, cap + 1, cap + 11):
+            assert np.array_equal(got, pconv_mod.numpy_convolve(img, reps)), reps
+    assert eng._eng.cached_graphs < cap
+
+
 @pytest.mark.parametrize("fuse", [1, 2, 5, 8])
 @pytest.mark.parametrize("graph", [False, True])
 def test_engine_reuse_fuse_graph(pconv_mod, rng, fuse, graph):
