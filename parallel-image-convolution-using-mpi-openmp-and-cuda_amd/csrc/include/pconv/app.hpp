@@ -29,6 +29,11 @@ struct AppReport {
   int64_t mismatches = -1; // --check result (-1 = not checked)
   std::string kernel;
   std::string output;
+  // End-to-end breakdown (seconds, in order): the reference's timer covers
+  // everything after argument parsing (cuda/main.c:20-49), HIP/CUDA context
+  // creation included; these phases say where that time goes.
+  std::vector<std::pair<std::string, double>> phases;
+  double since_exec_s = 0;  // process start (exec) -> report, 10 ms resolution (/proc)
 };
 
 // Runs the CLI (argv as given).  Returns the process exit code.

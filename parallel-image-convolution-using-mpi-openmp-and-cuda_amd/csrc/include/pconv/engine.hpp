@@ -90,6 +90,9 @@ class BandEngine {
   // Frame pointers at (owned row 0, data column 0).
   uint8_t* src_frame() const { return frame_[cur_].data() + lay_.offset(0); }
   uint8_t* dst_frame() const { return frame_[cur_ ^ 1].data() + lay_.offset(0); }
+  // Frame `which` (0/1) at (owned row 0, data column 0); cur() = the source frame.
+  uint8_t* frame_at(int which) const { return frame_[which & 1].data() + lay_.offset(0); }
+  int cur() const { return cur_; }
 
   // Copy frame-local rows [r_begin, r_end) from host (pointer at row r_begin).
   // Rows in the ghost zone are accepted (pre-loaded halos).  Async on the
@@ -101,6 +104,10 @@ class BandEngine {
   void upload_rows_device(const uint8_t* dev, int64_t dev_pitch, int64_t r_begin, int64_t r_end);
   // Declare whether the ghost rows currently hold valid neighbour data.
   void set_halo_valid(bool v) { halo_valid_ = v; }
+  // Serving-step input rows [in_r0, in_r1): false for exactly the owned rows,
+  // true for the owned rows plus the full ghost zone on both sides (clipped at
+  // the image edges); throws for any other range (a partial ghost zone).
+  bool input_preloaded(int64_t in_r0, int64_t in_r1) const;
   // Copy owned rows [r_begin, r_end) of the newest result to host / device.
   void download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begin, int64_t r_end,
                      hipStream_t stream = nullptr);
@@ -140,7 +147,12 @@ class BandEngine {
   // Zero both frames (ghost rows, pads and data).
   void clear();
 
+  // Debug / tests: copy FRAME rows [r_begin, r_end) of the current source
+  // frame, ghost rows included (r_begin >= -halo, r_end <= rows + halo).
+  void read_frame_rows(uint8_t* host, int64_t r_begin, int64_t r_end);
+
  private:
+  friend class LocalCluster;
   void enqueue_phase(const Phase& p);
   void launch(const LaunchSpec& l, hipStream_t s, uint8_t* dst = nullptr, int64_t dst_pitch = 0);
   StencilLaunch make_launch(const LaunchSpec& l, int cur, uint8_t* dst, int64_t dst_pitch) const;
@@ -247,13 +259,19 @@ class LocalCluster {
   BandEngine& engine(int i) { return *engines_.at(i); }
   // Host image (contiguous) in/out.
   void upload(const uint8_t* host, bool preload_halo);
-  void run(int reps);
+  // device_async = false: phase by phase with host synchronisation (exchange,
+  // sync, compute, sync).  true: every band enqueues its phases through the
+  // production path (comm stream || interior launch, edge launches after the
+  // halo event), bands ordered only by per-phase events — the overlap and
+  // event ordering of a real multi-GPU rank, with D2D copies as transport.
+  void run(int reps, bool device_async = false);
   void download(uint8_t* host);
   void synchronize();
 
  private:
   ImageGeom geom_;
   std::vector<std::unique_ptr<BandEngine>> engines_;
+  std::vector<Event> ev_phase_;  // per band: end of its previous phase
 };
 
 // Timing-only transport: moves nothing.  Measures a band's compute schedule

@@ -29,6 +29,9 @@ constexpr int kUniqueIdBytes = 128;
 // Generate a fresh unique id (call on ONE rank, distribute the bytes).
 std::vector<uint8_t> rccl_unique_id();
 std::string rccl_version();
+// True once librccl is mapped into this process (it is dlopen'ed on the first
+// RCCL call, never at start-up).
+bool rccl_loaded();
 
 class RcclComm {
  public:

@@ -126,22 +126,67 @@ AppReport run_cpu(const CliConfig& c) {
   return r;
 }
 
+// Phase clock for the end-to-end breakdown.
+struct PhaseClock {
+  std::vector<std::pair<std::string, double>>* out;
+  double t;
+  explicit PhaseClock(std::vector<std::pair<std::string, double>>* o) : out(o), t(wall_seconds()) {}
+  void mark(const char* name) {
+    const double now = wall_seconds();
+    out->emplace_back(name, now - t);
+    t = now;
+  }
+};
+
+// Seconds since this process was exec'ed (/proc/self/stat field 22, in clock
+// ticks since boot, against CLOCK_BOOTTIME): covers the dynamic loader and
+// static initialisers that no in-process timer sees.  10 ms resolution.
+double seconds_since_exec() {
+  FILE* f = std::fopen("/proc/self/stat", "r");
+  if (!f) return 0;
+  char buf[1024];
+  const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  const char* p = std::strrchr(buf, ')');  // comm may contain spaces
+  if (!p) return 0;
+  unsigned long long start = 0;
+  int field = 2;
+  for (const char* q = p + 1; *q && field < 22; ++q)
+    if (*q == ' ' && ++field == 22) start = std::strtoull(q + 1, nullptr, 10);
+  timespec ts{};
+  clock_gettime(CLOCK_BOOTTIME, &ts);
+  const double hz = static_cast<double>(sysconf(_SC_CLK_TCK));
+  return (ts.tv_sec + ts.tv_nsec * 1e-9) - static_cast<double>(start) / hz;
+}
+
 // ------------------------------------------------------------------ 1 GPU
 AppReport run_gpu1(const CliConfig& c) {
+  AppReport r;
   const double t0 = wall_seconds();
+  PhaseClock pc(&r.phases);
   const ImageGeom g = geom_of(c);
   if (!c.synthetic) validate_input_file(c.image, g);
   const Filter f = Filter::by_name(c.filter);
   set_device(0);
+  PCONV_HIP_CHECK(hipFree(nullptr));  // the runtime + device context (cudaMalloc's hidden cost in the reference)
+  pc.mark("hip_init");
   PinnedBuffer host(static_cast<size_t>(g.bytes()));
+  pc.mark("pinned_alloc");
   load_rows(c, g, 0, g.height, host.data(), g.row_bytes());
+  pc.mark(c.synthetic ? "synthesize" : "read");
   const EngineOptions o = engine_options(c, g, 1, 0);
   BandEngine eng(g, row_band(g.height, 1, 0), f, o);
+  pc.mark("device_alloc");
   if (c.explain) std::fprintf(stderr, "%s", describe_plan(eng.plan(c.reps)).c_str());
   for (int i = 0; i < c.warmup; ++i) eng.run(c.reps);  // zero frames stay zero
+  if (c.warmup > 0) {
+    eng.synchronize();
+    pc.mark("warmup");
+  }
   eng.upload_rows(host.data(), g.row_bytes(), 0, g.height);
   eng.synchronize();
-  AppReport r;
+  pc.mark("h2d");
   r.output = out_path(c);
   const double l0 = wall_seconds();
   int done = 0;
@@ -159,14 +204,18 @@ AppReport run_gpu1(const CliConfig& c) {
     }
   }
   r.loop_s = wall_seconds() - l0;
+  pc.mark("loop");
   eng.download_rows(host.data(), g.row_bytes(), 0, g.height);
   eng.synchronize();
+  pc.mark("d2h");
   write_image(r.output, g, host.data());
+  pc.mark("write");
   r.e2e_s = wall_seconds() - t0;
   r.halo = eng.options().halo_depth;
   r.fuse = eng.options().fuse;
   r.kernel = kernel_variant_name(eng.options().variant);
   if (c.check) r.mismatches = compare_with_oracle(c, g, host.data());
+  r.since_exec_s = seconds_since_exec();
   return r;
 }
 
@@ -297,15 +346,32 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
   eng.synchronize();
   shm_barrier(sh, world, c.timeout_s);  // MPI_Barrier before the timer (mpi_convolution.c:151)
   const double l0 = wall_seconds();
-  eng.run(c.reps);
-  if (comm) {
-    comm->wait(eng.compute_stream(), c.timeout_s);
-    comm->wait(eng.comm_stream(), c.timeout_s);
-  }
-  eng.synchronize();
+  // --checkpoint-every K: the run in chunks of K repetitions; after each
+  // chunk but the last every rank pwrites its band into <out>.rep<done>
+  // (pre-sized by the launcher).  A later chunk exchanges its ghost rows
+  // (run() invalidates the pre-loaded ones).
+  const int chunk = c.checkpoint_every > 0 ? c.checkpoint_every : std::max(1, c.reps);
+  int done = 0, launches = 0, exchanges = 0;
+  do {
+    const int k = std::min(chunk, c.reps - done);
+    eng.run(k);
+    if (comm) {
+      comm->wait(eng.compute_stream(), c.timeout_s);
+      comm->wait(eng.comm_stream(), c.timeout_s);
+    }
+    eng.synchronize();
+    launches += eng.last_stats().launches;
+    exchanges += eng.last_stats().exchanges;
+    done += k;
+    if (c.checkpoint_every > 0 && done < c.reps) {
+      eng.download_rows(host.data(), rb, 0, b.rows);
+      eng.synchronize();
+      write_rows(out_path(c) + ".rep" + std::to_string(done), g, b.y0, b.rows, host.data(), rb);
+    }
+  } while (done < c.reps);
   sh->loop_s[rank] = wall_seconds() - l0;
-  sh->launches[rank] = eng.last_stats().launches;
-  sh->exchanges[rank] = eng.last_stats().exchanges;
+  sh->launches[rank] = launches;
+  sh->exchanges[rank] = exchanges;
   eng.download_rows(host.data(), rb, 0, b.rows);
   eng.synchronize();
   {
@@ -322,6 +388,9 @@ AppReport run_multi(const CliConfig& c) {
   PCONV_CHECK(g.height >= c.gpus, "image has fewer rows than ranks");
   if (!c.synthetic) validate_input_file(c.image, g);
   create_output(out_path(c), g);  // sized + truncated once, ranks pwrite their bands
+  if (c.checkpoint_every > 0)
+    for (int d = c.checkpoint_every; d < c.reps; d += c.checkpoint_every)
+      create_output(out_path(c) + ".rep" + std::to_string(d), g);
   void* mem = mmap(nullptr, sizeof(SharedState), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
   PCONV_CHECK(mem != MAP_FAILED, "mmap shared state failed");
   auto* sh = new (mem) SharedState();
@@ -421,7 +490,15 @@ std::string report_json(const CliConfig& c, const AppReport& r) {
      << ", \"fuse\": " << r.fuse << ", \"launches\": " << r.launches << ", \"exchanges\": " << r.exchanges
      << ", \"loop_s\": " << r.loop_s << ", \"e2e_s\": " << r.e2e_s << ", \"loop_mpix_per_s\": " << r.mpix_per_s
      << ", \"e2e_mpix_per_s\": " << (r.e2e_s > 0 ? px / r.e2e_s / 1e6 : 0.0)
-     << ", \"mismatches\": " << r.mismatches << ", \"output\": \"" << r.output << "\"}";
+     << ", \"mismatches\": " << r.mismatches << ", \"output\": \"" << r.output << "\""
+     << ", \"rccl_loaded\": " << (rccl_loaded() ? "true" : "false");
+  if (!r.phases.empty()) {
+    os << ", \"phases_s\": {";
+    for (size_t i = 0; i < r.phases.size(); ++i)
+      os << (i ? ", " : "") << "\"" << r.phases[i].first << "\": " << r.phases[i].second;
+    os << "}, \"since_exec_s\": " << r.since_exec_s;
+  }
+  os << "}";
   return os.str();
 }
 

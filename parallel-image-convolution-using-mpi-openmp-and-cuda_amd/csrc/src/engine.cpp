@@ -118,6 +118,15 @@ void BandEngine::download_rows_device(uint8_t* dev, int64_t dev_pitch, int64_t r
                                    r_end - r_begin, hipMemcpyDeviceToDevice, cs_));
 }
 
+void BandEngine::read_frame_rows(uint8_t* host, int64_t r_begin, int64_t r_end) {
+  PCONV_CHECK(r_begin >= -lay_.halo && r_end <= lay_.rows + lay_.halo && r_begin <= r_end,
+              "read_frame_rows: rows outside frame");
+  synchronize();
+  if (r_end == r_begin) return;
+  PCONV_HIP_CHECK(hipMemcpy2D(host, lay_.row_bytes, src_frame() + r_begin * lay_.pitch, lay_.pitch, lay_.row_bytes,
+                              r_end - r_begin, hipMemcpyDeviceToHost));
+}
+
 void BandEngine::wait_stream(hipStream_t s) {
   ev_sync_.record(s);
   ev_sync_.wait_on(cs_);
@@ -152,12 +161,29 @@ StencilLaunch BandEngine::make_launch(const LaunchSpec& l, int cur, uint8_t* dst
 }
 
 void BandEngine::prepare(const std::vector<Phase>& ph) {
-  int cur = cur_;
-  for (const auto& p : ph) {
+  // Tuning times real launches.  Every candidate runs frame_[cur_] ->
+  // frame_[cur_ ^ 1] whatever the phase parity: the live input (and its
+  // pre-loaded ghost rows) in frame_[cur_] is only ever READ here, and the
+  // scratch frame is overwritten by the first phase anyway.  The tune key
+  // depends only on (channels, steps, rows, row bytes), not on the frames.
+  for (const auto& p : ph)
     for (const auto& l : p.launches)
-      prepare_stencil(filter_, geom_.channels, make_launch(l, cur, nullptr, 0), cs_, opt_.variant);
-    cur ^= 1;
-  }
+      prepare_stencil(filter_, geom_.channels, make_launch(l, cur_, nullptr, 0), cs_, opt_.variant);
+}
+
+bool BandEngine::input_preloaded(int64_t in_r0, int64_t in_r1) const {
+  if (in_r0 == 0 && in_r1 == band_.rows) return false;
+  // Ghost rows are either absent or the full valid depth on BOTH sides
+  // (clipped at the global image edge): anything else would leave stale or
+  // zero ghost rows that the planner believes valid.
+  const int64_t want_lo = -std::min<int64_t>(lay_.halo, band_.y0);
+  const int64_t want_hi = band_.rows + std::min<int64_t>(lay_.halo, geom_.height - (band_.y0 + band_.rows));
+  PCONV_CHECK(in_r0 == want_lo && in_r1 == want_hi,
+              "input rows [" + std::to_string(in_r0) + ", " + std::to_string(in_r1) +
+                  ") are neither the owned rows [0, " + std::to_string(band_.rows) +
+                  ") nor the owned rows plus the full ghost zone [" + std::to_string(want_lo) + ", " +
+                  std::to_string(want_hi) + ")");
+  return true;
 }
 
 void BandEngine::launch(const LaunchSpec& l, hipStream_t s, uint8_t* dst, int64_t dst_pitch) {
@@ -266,8 +292,7 @@ bool BandEngine::exchange_free(int reps, bool halo_preloaded) const {
 void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
   TraceRange tr("pconv.step_graph");
   PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
-  const bool preloaded = in_r0 < 0 || in_r1 > band_.rows;
-  halo_valid_ = preloaded;
+  halo_valid_ = input_preloaded(in_r0, in_r1);
   const std::vector<Phase> ph = plan(reps);
   for (const auto& p : ph)
     PCONV_CHECK(p.exchange_depth == 0, "process_graph: this schedule needs halo exchanges (pre-load deeper ghost rows)");
@@ -414,7 +439,7 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
     // Everything of this image on the slot's stream; halo exchanges (if the
     // ghost rows are not pre-loaded) through this slot's own transport, in
     // stream order between the upload and the launches.
-    const bool preloaded = in_r0 < 0 || in_r1 > e.band().rows;
+    const bool preloaded = e.input_preloaded(in_r0, in_r1);
     hipStream_t cs = e.compute_stream();
     trace_mark(0, cs);
     e.upload_rows(host_in, e.layout().row_bytes, in_r0, in_r1);
@@ -435,13 +460,13 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
     ++count_;
     return;
   }
+  const bool preloaded = e.input_preloaded(in_r0, in_r1);
   // H2D into slot k once its previous image has been downloaded.
   if (used_[k]) ev_free_[k].wait_on(h2d_.get());
   trace_mark(0, h2d_.get());
   e.upload_rows(host_in, e.layout().row_bytes, in_r0, in_r1, h2d_.get());
   trace_mark(1, h2d_.get());
   ev_up_[k].record(h2d_.get());
-  const bool preloaded = in_r0 < 0 || in_r1 > e.band().rows;
   e.set_halo_valid(preloaded);
   if (!preloaded && comm_.get() && e.has_transport() && reps > 0) {
     // Exchange this image's ghost rows as soon as it is uploaded — on the
@@ -506,16 +531,21 @@ void LocalTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream) 
   const Band& b = e.band();
   const int64_t pitch = L.pitch;
   uint8_t* mine = e.src_frame() - kPadLeft;  // row 0, pitch-aligned start
+  // Bands of one cluster advance in lockstep (same phase count per run), so
+  // the peer's frame of the same parity holds the same time level — read by
+  // parity, not through the peer's current frame, which a device-async run
+  // may already have flipped to the next phase.
+  const int par = e.cur();
   if (b.up >= 0) {
     BandEngine& p = *peers_.at(b.up);
     PCONV_CHECK(p.layout().pitch == pitch && p.band().rows >= depth, "local halo: incompatible peer");
-    const uint8_t* from = p.src_frame() - kPadLeft + (p.band().rows - depth) * pitch;
+    const uint8_t* from = p.frame_at(par) - kPadLeft + (p.band().rows - depth) * pitch;
     PCONV_HIP_CHECK(hipMemcpyAsync(mine - depth * pitch, from, depth * pitch, hipMemcpyDeviceToDevice, stream));
   }
   if (b.down >= 0) {
     BandEngine& p = *peers_.at(b.down);
     PCONV_CHECK(p.layout().pitch == pitch && p.band().rows >= depth, "local halo: incompatible peer");
-    const uint8_t* from = p.src_frame() - kPadLeft;
+    const uint8_t* from = p.frame_at(par) - kPadLeft;
     PCONV_HIP_CHECK(hipMemcpyAsync(mine + b.rows * pitch, from, depth * pitch, hipMemcpyDeviceToDevice, stream));
   }
 }
@@ -527,6 +557,7 @@ LocalCluster::LocalCluster(const ImageGeom& geom, int bands, const Filter& filte
   for (const auto& b : bs) {
     engines_.push_back(std::make_unique<BandEngine>(geom, b, filter, opt));
     peers.push_back(engines_.back().get());
+    ev_phase_.push_back(Event::create());
   }
   auto t = std::make_shared<LocalTransport>(peers);
   for (auto& e : engines_) e->set_transport(t);
@@ -548,11 +579,38 @@ void LocalCluster::upload(const uint8_t* host, bool preload_halo) {
   synchronize();
 }
 
-void LocalCluster::run(int reps) {
+void LocalCluster::run(int reps, bool device_async) {
   std::vector<std::vector<Phase>> plans;
   for (auto& e : engines_) plans.push_back(e->plan(reps));
   const size_t n = plans.front().size();
   for (const auto& p : plans) PCONV_CHECK(p.size() == n, "local cluster: band plans diverge");
+  if (device_async) {
+    // Every band runs the production phase path (BandEngine::enqueue_phase):
+    // the D2D halo copy on its comm stream, the interior launch concurrently
+    // on its compute stream, the edge launches after ev_halo — nothing waits
+    // on the host.  The only cross-band ordering is one event per band per
+    // phase (the MPI_Wait pairs of mpi/mpi_convolution.c:199-234): before
+    // phase i a band waits for its neighbours to finish phase i-1, which
+    // (a) makes their owned rows final before its exchange reads them and
+    // (b) makes their phase i-1 exchange, which read ITS owned rows, done
+    // before its phase i launches overwrite that frame.
+    const size_t nb = engines_.size();
+    for (size_t i = 0; i < n; ++i) {
+      for (size_t k = 0; k < nb; ++k) ev_phase_[k].record(engines_[k]->compute_stream());
+      for (size_t k = 0; k < nb; ++k) {
+        const Band& b = engines_[k]->band();
+        for (int peer : {b.up, b.down})
+          if (peer >= 0) ev_phase_.at(peer).wait_on(engines_[k]->compute_stream());
+      }
+      // LocalTransport reads a peer's frame by the exchanging band's parity
+      // (frame_at(e.cur())), so enqueueing band k after band k-1 has flipped
+      // its frames is safe.
+      for (size_t k = 0; k < nb; ++k) engines_[k]->enqueue_phase(plans[k][i]);
+    }
+    synchronize();
+    for (auto& e : engines_) e->set_halo_valid(false);
+    return;
+  }
   for (size_t i = 0; i < n; ++i) {
     for (size_t k = 0; k < engines_.size(); ++k) engines_[k]->exec_exchange(plans[k][i]);
     synchronize();

@@ -476,6 +476,38 @@ PYBIND11_MODULE(_pconv_native, m) {
           },
           py::arg("in_ptr"), py::arg("in_r0"), py::arg("in_r1"), py::arg("out_ptr"), py::arg("reps"))
       .def("exchange_free", &BandEngine::exchange_free, py::arg("reps"), py::arg("halo_preloaded"))
+      .def("input_preloaded", &BandEngine::input_preloaded, py::arg("in_r0"), py::arg("in_r1"))
+      .def(
+          "exchange_now",
+          [](BandEngine& e, uintptr_t stream) { e.exchange_now(reinterpret_cast<hipStream_t>(stream)); },
+          py::arg("stream") = 0, "Fill the whole ghost zone now (transport on `stream`, 0 = the comm stream)")
+      .def(
+          "read_frame",
+          [](BandEngine& e, py::buffer host, int64_t r_begin, int64_t r_end) {
+            const HostView v = host_view(host, true);
+            PCONV_CHECK(v.size >= (r_end - r_begin) * e.layout().row_bytes, "host buffer too small");
+            py::gil_scoped_release nogil;
+            e.read_frame_rows(v.ptr, r_begin, r_end);
+          },
+          py::arg("host"), py::arg("r_begin"), py::arg("r_end"),
+          "Copy source-frame rows [r_begin, r_end), ghost rows included (tests / debugging)")
+      .def_static(
+          "for_band",
+          [](int64_t w, int64_t h, const std::string& ch, py::object filter, const Band& band, int device, int halo,
+             int fuse, bool overlap, const std::string& variant) {
+            // An explicit band (tests: e.g. a single rank whose up/down
+            // neighbour is itself, to drive RCCL send/recv-to-self).
+            EngineOptions o;
+            o.device = device;
+            o.halo_depth = halo;
+            o.fuse = fuse;
+            o.overlap = overlap;
+            o.variant = parse_variant(variant);
+            return std::make_unique<BandEngine>(make_geom(w, h, ch), band, make_filter(filter), o);
+          },
+          py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter"), py::arg("band"),
+          py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1, py::arg("overlap") = true,
+          py::arg("variant") = "auto")
       .def("attach_rccl",
            [](BandEngine& e, std::shared_ptr<RcclComm> c) {
              e.set_transport(std::make_shared<RcclTransport>(std::move(c)));
@@ -538,23 +570,26 @@ PYBIND11_MODULE(_pconv_native, m) {
 
   py::class_<LocalCluster>(m, "LocalCluster")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int bands, int device, int halo,
-                       int fuse, const std::string& variant) {
+                       int fuse, const std::string& variant, bool overlap) {
              EngineOptions o;
              o.device = device;
              o.halo_depth = halo;
              o.fuse = fuse;
+             o.overlap = overlap;
              o.variant = parse_variant(variant);
              return std::make_unique<LocalCluster>(make_geom(w, h, ch), bands, make_filter(filter), o);
            }),
            py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
            py::arg("bands") = 2, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
-           py::arg("variant") = "auto")
+           py::arg("variant") = "auto", py::arg("overlap") = true)
       .def("upload",
            [](LocalCluster& c, py::buffer host, bool preload_halo) {
              c.upload(host_view(host, false).ptr, preload_halo);
            },
            py::arg("host"), py::arg("preload_halo") = false)
-      .def("run", &LocalCluster::run, py::call_guard<py::gil_scoped_release>())
+      .def("run", &LocalCluster::run, py::arg("reps"), py::arg("device_async") = false,
+           py::call_guard<py::gil_scoped_release>(),
+           "device_async: every band through the production phase path (comm stream || interior, event-ordered)")
       .def("download", [](LocalCluster& c, py::buffer host) { c.download(host_view(host, true).ptr); })
       .def("exchanges", [](LocalCluster& c) { return c.engine(0).last_stats().exchanges; })
       .def_property_readonly("size", &LocalCluster::size);
@@ -565,6 +600,7 @@ PYBIND11_MODULE(_pconv_native, m) {
     return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
   });
   m.def("rccl_version", &rccl_version);
+  m.def("rccl_loaded", &rccl_loaded, "True once librccl is mapped (loaded lazily on the first RCCL call)");
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def(py::init([](py::bytes id, int rank, int world, int device) {
              const std::string s = id;

@@ -2,23 +2,98 @@
 #include "pconv/rccl_comm.hpp"
 #include "pconv/trace.hpp"
 
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 
 namespace pconv {
 
-#define PCONV_RCCL_CHECK(expr)                                                                      \
-  do {                                                                                              \
-    ncclResult_t _r = (expr);                                                                       \
-    if (_r != ncclSuccess && _r != ncclInProgress)                                                  \
-      ::pconv::raise_error(__FILE__, __LINE__, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+namespace {
+
+// librccl is loaded on first use (dlopen), not at process start: the library
+// is ~570 MB with a large symbol table, and a 1-GPU `conv` run or a Python
+// process that never builds a communicator should not pay its load and
+// relocation in its start-up (the reference's CUDA program, timed end to end
+// by cuda/main.c:20-49, links no communication library at all).
+struct RcclApi {
+  decltype(&::ncclGetVersion) GetVersion = nullptr;
+  decltype(&::ncclGetUniqueId) GetUniqueId = nullptr;
+  decltype(&::ncclCommInitRank) CommInitRank = nullptr;
+  decltype(&::ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&::ncclCommAbort) CommAbort = nullptr;
+  decltype(&::ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&::ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+  decltype(&::ncclAllReduce) AllReduce = nullptr;
+  decltype(&::ncclSend) Send = nullptr;
+  decltype(&::ncclRecv) Recv = nullptr;
+  decltype(&::ncclGroupStart) GroupStart = nullptr;
+  decltype(&::ncclGroupEnd) GroupEnd = nullptr;
+};
+
+const RcclApi& rccl() {
+  static RcclApi api;
+  static std::once_flag once;
+  static std::string err;
+  std::call_once(once, [] {
+    std::vector<std::string> names;
+    if (const char* p = std::getenv("PCONV_RCCL_LIB")) names.emplace_back(p);
+    names.emplace_back("librccl.so.1");
+    names.emplace_back("librccl.so");
+    const char* rocm = std::getenv("ROCM_PATH");
+    names.emplace_back(std::string(rocm ? rocm : "/opt/rocm") + "/lib/librccl.so.1");
+    void* h = nullptr;
+    for (const auto& n : names)
+      if ((h = dlopen(n.c_str(), RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+    if (!h) {
+      const char* e = dlerror();
+      err = std::string("cannot load librccl (") + (e ? e : "not found") + ")";
+      return;
+    }
+    auto sym = [&](const char* name) {
+      void* f = dlsym(h, name);
+      if (!f) err = std::string("librccl lacks ") + name;
+      return f;
+    };
+    api.GetVersion = reinterpret_cast<decltype(api.GetVersion)>(sym("ncclGetVersion"));
+    api.GetUniqueId = reinterpret_cast<decltype(api.GetUniqueId)>(sym("ncclGetUniqueId"));
+    api.CommInitRank = reinterpret_cast<decltype(api.CommInitRank)>(sym("ncclCommInitRank"));
+    api.CommDestroy = reinterpret_cast<decltype(api.CommDestroy)>(sym("ncclCommDestroy"));
+    api.CommAbort = reinterpret_cast<decltype(api.CommAbort)>(sym("ncclCommAbort"));
+    api.GetErrorString = reinterpret_cast<decltype(api.GetErrorString)>(sym("ncclGetErrorString"));
+    api.CommGetAsyncError = reinterpret_cast<decltype(api.CommGetAsyncError)>(sym("ncclCommGetAsyncError"));
+    api.AllReduce = reinterpret_cast<decltype(api.AllReduce)>(sym("ncclAllReduce"));
+    api.Send = reinterpret_cast<decltype(api.Send)>(sym("ncclSend"));
+    api.Recv = reinterpret_cast<decltype(api.Recv)>(sym("ncclRecv"));
+    api.GroupStart = reinterpret_cast<decltype(api.GroupStart)>(sym("ncclGroupStart"));
+    api.GroupEnd = reinterpret_cast<decltype(api.GroupEnd)>(sym("ncclGroupEnd"));
+  });
+  PCONV_CHECK(err.empty(), err);
+  return api;
+}
+
+}  // namespace
+
+bool rccl_loaded() {
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+  if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+  if (h) dlclose(h);
+  return h != nullptr;
+}
+
+#define PCONV_RCCL_CHECK(expr)                                                                            \
+  do {                                                                                                    \
+    ncclResult_t _r = (expr);                                                                             \
+    if (_r != ncclSuccess && _r != ncclInProgress)                                                        \
+      ::pconv::raise_error(__FILE__, __LINE__, std::string(#expr) + ": " + rccl().GetErrorString(_r));    \
   } while (0)
 
 std::vector<uint8_t> rccl_unique_id() {
   ncclUniqueId id;
-  PCONV_RCCL_CHECK(ncclGetUniqueId(&id));
+  PCONV_RCCL_CHECK(rccl().GetUniqueId(&id));
   std::vector<uint8_t> v(kUniqueIdBytes);
   std::memcpy(v.data(), id.internal, kUniqueIdBytes);
   return v;
@@ -26,7 +101,7 @@ std::vector<uint8_t> rccl_unique_id() {
 
 std::string rccl_version() {
   int v = 0;
-  PCONV_RCCL_CHECK(ncclGetVersion(&v));
+  PCONV_RCCL_CHECK(rccl().GetVersion(&v));
   return std::to_string(v / 10000) + "." + std::to_string((v / 100) % 100) + "." + std::to_string(v % 100);
 }
 
@@ -39,23 +114,23 @@ RcclComm::RcclComm(const std::vector<uint8_t>& unique_id, int rank, int world, i
   ncclUniqueId id;
   std::memcpy(id.internal, unique_id.data(), kUniqueIdBytes);
   ncclComm_t c = nullptr;
-  PCONV_RCCL_CHECK(ncclCommInitRank(&c, world, id, rank));
+  PCONV_RCCL_CHECK(rccl().CommInitRank(&c, world, id, rank));
   comm_ = c;
   stream_ = Stream::create(0);
   scratch_ = DeviceBuffer(64);
 }
 
 RcclComm::~RcclComm() {
-  if (comm_) (void)ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+  if (comm_) (void)rccl().CommDestroy(static_cast<ncclComm_t>(comm_));
 }
 
 void RcclComm::check_async_error() {
   ncclResult_t r = ncclSuccess;
-  PCONV_RCCL_CHECK(ncclCommGetAsyncError(static_cast<ncclComm_t>(comm_), &r));
+  PCONV_RCCL_CHECK(rccl().CommGetAsyncError(static_cast<ncclComm_t>(comm_), &r));
   if (r != ncclSuccess && r != ncclInProgress) {
-    (void)ncclCommAbort(static_cast<ncclComm_t>(comm_));
+    (void)rccl().CommAbort(static_cast<ncclComm_t>(comm_));
     comm_ = nullptr;
-    PCONV_FAIL(std::string("RCCL asynchronous error: ") + ncclGetErrorString(r));
+    PCONV_FAIL(std::string("RCCL asynchronous error: ") + rccl().GetErrorString(r));
   }
 }
 
@@ -67,7 +142,7 @@ void RcclComm::wait(hipStream_t stream, double timeout_s) {
     if (q != hipErrorNotReady) PCONV_HIP_CHECK(q);
     check_async_error();
     if (timeout_s > 0 && wall_seconds() - t0 > timeout_s) {
-      (void)ncclCommAbort(static_cast<ncclComm_t>(comm_));
+      (void)rccl().CommAbort(static_cast<ncclComm_t>(comm_));
       comm_ = nullptr;
       PCONV_FAIL("RCCL wait timed out after " + std::to_string(timeout_s) + " s (peer hung or died?)");
     }
@@ -77,7 +152,7 @@ void RcclComm::wait(hipStream_t stream, double timeout_s) {
 
 double RcclComm::allreduce(double v, int op) {
   PCONV_HIP_CHECK(hipMemcpyAsync(scratch_.data(), &v, sizeof(double), hipMemcpyHostToDevice, stream_.get()));
-  PCONV_RCCL_CHECK(ncclAllReduce(scratch_.data(), scratch_.data(), 1, ncclFloat64, static_cast<ncclRedOp_t>(op),
+  PCONV_RCCL_CHECK(rccl().AllReduce(scratch_.data(), scratch_.data(), 1, ncclFloat64, static_cast<ncclRedOp_t>(op),
                                  static_cast<ncclComm_t>(comm_), stream_.get()));
   double out = 0;
   PCONV_HIP_CHECK(hipMemcpyAsync(&out, scratch_.data(), sizeof(double), hipMemcpyDeviceToHost, stream_.get()));
@@ -99,16 +174,16 @@ void RcclTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream) {
   const size_t n = static_cast<size_t>(depth * pitch);
   auto comm = static_cast<ncclComm_t>(comm_->handle());
   PCONV_CHECK(comm != nullptr, "rccl halo: communicator was aborted");
-  PCONV_RCCL_CHECK(ncclGroupStart());
+  PCONV_RCCL_CHECK(rccl().GroupStart());
   if (b.up >= 0) {
-    PCONV_RCCL_CHECK(ncclSend(row0, n, ncclUint8, b.up, comm, stream));                     // my top rows
-    PCONV_RCCL_CHECK(ncclRecv(row0 - depth * pitch, n, ncclUint8, b.up, comm, stream));     // ghost above
+    PCONV_RCCL_CHECK(rccl().Send(row0, n, ncclUint8, b.up, comm, stream));                     // my top rows
+    PCONV_RCCL_CHECK(rccl().Recv(row0 - depth * pitch, n, ncclUint8, b.up, comm, stream));     // ghost above
   }
   if (b.down >= 0) {
-    PCONV_RCCL_CHECK(ncclSend(row0 + (b.rows - depth) * pitch, n, ncclUint8, b.down, comm, stream));
-    PCONV_RCCL_CHECK(ncclRecv(row0 + b.rows * pitch, n, ncclUint8, b.down, comm, stream));  // ghost below
+    PCONV_RCCL_CHECK(rccl().Send(row0 + (b.rows - depth) * pitch, n, ncclUint8, b.down, comm, stream));
+    PCONV_RCCL_CHECK(rccl().Recv(row0 + b.rows * pitch, n, ncclUint8, b.down, comm, stream));  // ghost below
   }
-  PCONV_RCCL_CHECK(ncclGroupEnd());
+  PCONV_RCCL_CHECK(rccl().GroupEnd());
 }
 
 }  // namespace pconv

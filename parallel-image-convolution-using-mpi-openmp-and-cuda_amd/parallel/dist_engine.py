@@ -25,15 +25,31 @@ DEFAULT_FUSE = 8
 AUTO_HALO_CAP = 64
 
 
-def auto_halo(height: int, world: int, reps: Optional[int], fuse: int) -> int:
+def auto_halo(height: int, world: int, reps: Optional[int], fuse: int, preload: bool = False) -> int:
     """Deep ghost zone: one exchange per `halo` reps, capped so the redundant
-    ghost-row compute stays small and the band can supply it."""
+    ghost-row compute stays small and the band can supply it.
+
+    preload: the ghost rows are uploaded with the band and never exchanged,
+    so the zone must cover ALL `reps` (a 200-rep run needs 200 ghost rows per
+    side; the redundant compute is the shrinking trapezoid, ~reps^2/fuse rows
+    per image — 5 % of a 4096-row band at 200 reps).  Bands shorter than
+    `reps` cannot supply that: they get the exchange cap and need a transport.
+    """
     if world <= 1:
         return fuse
-    d = min(AUTO_HALO_CAP, height // world)
+    band = height // world
+    if preload and reps and int(reps) <= band:
+        return max(int(reps), fuse, 1)
+    d = min(AUTO_HALO_CAP, band)
     if reps:
         d = min(d, int(reps))
     return max(d, fuse, 1)
+
+
+def preload_is_exchange_free(height: int, world: int, reps: int) -> bool:
+    """True when pre-loaded ghost rows can carry all `reps` (every band is at
+    least `reps` rows tall), so a run needs no halo transport at all."""
+    return world <= 1 or int(reps) <= height // world
 
 
 class DistributedBlur:
@@ -54,7 +70,7 @@ class DistributedBlur:
         if fuse is None:
             fuse = DEFAULT_FUSE if n.supports_fusion(nf, variant) else 1
         if halo is None:
-            halo = auto_halo(self.height, self.world, reps, fuse)
+            halo = auto_halo(self.height, self.world, reps, fuse, preload=bool(preload_halo) and not slot_exchange)
         kw = dict(halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant, slots=int(slots),
                   concurrent=int(concurrent))
         self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device, **kw)
@@ -63,6 +79,10 @@ class DistributedBlur:
         # streams) whenever the images need no halo exchange: one band, or
         # ghost rows pre-loaded deep enough for all `reps`.
         free = reps is not None and self.pipe.slot(0).exchange_free(int(reps), self.preload_halo)
+        if self.world > 1 and transport == "none" and not free:
+            raise ValueError(f"transport 'none' needs exchange-free images: {reps} reps with a "
+                             f"{self.pipe.slot(0).halo}-row ghost zone (preload_halo={self.preload_halo}) exchange "
+                             "halos; use transport rccl/gloo-host")
         if step_graphs and not free and not slot_exchange:
             raise ValueError("step_graphs needs exchange-free images (world 1, or preload_halo with halo >= reps)")
         # slot_exchange: images that DO exchange halos, each on its slot's own

@@ -69,8 +69,11 @@ def parse(argv: List[str]) -> argparse.Namespace:
     p.add_argument("--json", action="store_true")
     p.add_argument("--quiet", action="store_true")
     p.add_argument("--timeout", type=float, default=600.0, help="RCCL watchdog (seconds) on the halo waits")
+    p.add_argument("--checkpoint-every", type=int, default=0, metavar="K",
+                   help="every K repetitions write the whole image to <out>.rep<N> (each rank pwrites its band); "
+                        "resume = rerun on that file with the remaining repetitions")
     a = p.parse_args(argv)
-    if a.width < 1 or a.height < 1 or a.reps < 0:
+    if a.width < 1 or a.height < 1 or a.reps < 0 or a.checkpoint_every < 0:
         sys.stderr.write(usage(prog))
         raise SystemExit(1)
     return a
@@ -151,6 +154,7 @@ class _CpuBand:
 
     def run(self, reps: int) -> None:
         self.r.run(reps, halo_preloaded=self._preloaded)
+        self._preloaded = False  # a later run (after a checkpoint) exchanges its ghost rows
 
     def result(self, out: np.ndarray) -> None:
         out.reshape(self.band.rows, -1)[:] = self.r.result()
@@ -193,13 +197,30 @@ def main(argv: Optional[List[str]] = None) -> int:
             n.create_output(out_path, a.width, a.height, a.channels)
         runner.load(rows, -above, b.rows + below, preload)
 
+        # Checkpoints: the iteration is Markov in the image, so a checkpoint
+        # is just the whole image after `done` repetitions (every rank pwrites
+        # its band into <out>.rep<done>, pre-sized by rank 0).
+        ce = a.checkpoint_every
+        ck = [d for d in range(ce, a.reps, ce)] if ce > 0 else []
+        if rank == 0:
+            for d in ck:
+                n.create_output(f"{out_path}.rep{d}", a.width, a.height, a.channels)
+        res = np.empty(b.rows * rb, np.uint8)
         barrier()  # MPI_Barrier before MPI_Wtime (mpi_convolution.c:151-154)
         t0 = time.perf_counter()
-        runner.run(a.reps)
+        done = 0
+        while done < a.reps or (done == 0 and a.reps == 0):
+            k = min(ce, a.reps - done) if ce > 0 else a.reps
+            runner.run(k)
+            done += k
+            if done in ck:
+                runner.result(res)
+                n.write_raw_rows(f"{out_path}.rep{done}", res, a.width, a.height, a.channels, b.y0, b.rows)
+            if a.reps == 0:
+                break
         loop_s = time.perf_counter() - t0
 
         barrier()  # output file exists before any pwrite
-        res = np.empty(b.rows * rb, np.uint8)
         runner.result(res)
         n.write_raw_rows(out_path, res, a.width, a.height, a.channels, b.y0, b.rows)
         t_max = max_over_ranks(loop_s)
