@@ -52,8 +52,13 @@ struct Row16 {
   u32 L, d0, d1, d2, d3, R;  // bytes [-4,0) , [0,16) , [16,20)
 };
 
-__device__ __forceinline__ Row16 load_row(const uint8_t* __restrict__ p) {
-  Row16 r;
+// A row outside the global image reads as zeros whatever the frame holds
+// there (zero-padding semantics, mpi/mpi_convolution.c:111-118): the frame
+// invariant "ghost rows beyond the image edge stay zero" is then not needed
+// for correctness (e.g. a band whose ghost rows a transport filled).
+__device__ __forceinline__ Row16 load_row_in(const uint8_t* __restrict__ p, bool in_image) {
+  Row16 r{0, 0, 0, 0, 0, 0};
+  if (!in_image) return r;
   const uint4 v = *reinterpret_cast<const uint4*>(p);
   r.L = *reinterpret_cast<const u32*>(p - 4);
   r.R = *reinterpret_cast<const u32*>(p + 16);
@@ -116,7 +121,8 @@ __device__ __forceinline__ uint4 mask_tail(uint4 o, int valid) {
 // ---------------------------------------------------------------------------
 template <int CH, int RPT>
 __global__ __launch_bounds__(256) void k_binomial(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                  int64_t pitch, int row_bytes, int r0, int r1) {
+                                                  int64_t pitch, int row_bytes, int r0, int r1, int img_lo,
+                                                  int img_hi) {
   const int x = (blockIdx.x * 64 + threadIdx.x) * 16;
   const int rs = r0 + (blockIdx.y * 4 + threadIdx.y) * RPT;
   if (x >= row_bytes || rs >= r1) return;
@@ -124,16 +130,17 @@ __global__ __launch_bounds__(256) void k_binomial(const uint8_t* __restrict__ sr
   const uint8_t* p = src + static_cast<int64_t>(rs - 1) * pitch + x;
   uint8_t* q = dst + static_cast<int64_t>(rs) * pitch + x;
   const int valid = row_bytes - x;
+  auto inside = [&](int r) { return r >= img_lo && r < img_hi; };
 
   u32 Ha[8], Hb[8];
-  horiz<CH>(load_row(p), Ha);
-  horiz<CH>(load_row(p + pitch), Hb);
+  horiz<CH>(load_row_in(p, inside(rs - 1)), Ha);
+  horiz<CH>(load_row_in(p + pitch, inside(rs)), Hb);
   p += 2 * pitch;
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
     if (i >= n) break;
     u32 Hc[8];
-    horiz<CH>(load_row(p), Hc);
+    horiz<CH>(load_row_in(p, inside(rs + i + 1)), Hc);
     p += pitch;
     u32 V[8];
 #pragma unroll
@@ -165,14 +172,16 @@ __device__ __forceinline__ u32 byte_at(const u32 (&w)[6], int b) {  // b in [-4,
 
 template <int CH, bool FLOAT>
 __global__ __launch_bounds__(256) void k_generic9(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                  int64_t pitch, int row_bytes, int r0, int r1, Taps9 tp) {
+                                                  int64_t pitch, int row_bytes, int r0, int r1, Taps9 tp,
+                                                  int img_lo, int img_hi) {
   const int x = (blockIdx.x * 64 + threadIdx.x) * 16;
   const int r = r0 + blockIdx.y * 4 + threadIdx.y;
   if (x >= row_bytes || r >= r1) return;
   u32 rows[3][6];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const Row16 b = load_row(src + static_cast<int64_t>(r - 1 + k) * pitch + x);
+    const int rr = r - 1 + k;
+    const Row16 b = load_row_in(src + static_cast<int64_t>(rr) * pitch + x, rr >= img_lo && rr < img_hi);
     rows[k][0] = b.L;
     rows[k][1] = b.d0;
     rows[k][2] = b.d1;
@@ -422,12 +431,15 @@ constexpr int kRowsPerLane = 4;
 template <int CH>
 void launch_ch(const Filter& f, const StencilLaunch& a, hipStream_t s, KernelVariant v) {
   const int rows = static_cast<int>(a.r1 - a.r0);
+  // frame rows inside the global image (clamped to the frame; 32-bit indices checked by the caller)
+  const int lo = static_cast<int>(std::max<int64_t>(-a.g_row0, a.frame_lo));
+  const int hi = static_cast<int>(std::min<int64_t>(a.height - a.g_row0, a.frame_hi));
   const int chunks = static_cast<int>(ceil_div<int64_t>(a.row_bytes, 16));
   const dim3 block(64, 4);
   if (v == KernelVariant::Binomial) {
     const dim3 grid(ceil_div(chunks, 64), ceil_div(rows, 4 * kRowsPerLane));
     k_binomial<CH, kRowsPerLane><<<grid, block, 0, s>>>(a.src, a.dst, a.pitch, static_cast<int>(a.row_bytes),
-                                                         static_cast<int>(a.r0), static_cast<int>(a.r1));
+                                                         static_cast<int>(a.r0), static_cast<int>(a.r1), lo, hi);
   } else {
     Taps9 tp;
     for (int i = 0; i < 9; ++i) {
@@ -438,10 +450,10 @@ void launch_ch(const Filter& f, const StencilLaunch& a, hipStream_t s, KernelVar
     const dim3 grid(ceil_div(chunks, 64), ceil_div(rows, 4));
     if (v == KernelVariant::Float9)
       k_generic9<CH, true><<<grid, block, 0, s>>>(a.src, a.dst, a.pitch, static_cast<int>(a.row_bytes),
-                                                  static_cast<int>(a.r0), static_cast<int>(a.r1), tp);
+                                                  static_cast<int>(a.r0), static_cast<int>(a.r1), tp, lo, hi);
     else
       k_generic9<CH, false><<<grid, block, 0, s>>>(a.src, a.dst, a.pitch, static_cast<int>(a.row_bytes),
-                                                   static_cast<int>(a.r0), static_cast<int>(a.r1), tp);
+                                                   static_cast<int>(a.r0), static_cast<int>(a.r1), tp, lo, hi);
   }
 }
 

@@ -133,3 +133,52 @@ def test_numa_bind_is_a_noop_without_a_gpu(pconv_mod, monkeypatch):
     monkeypatch.setenv("PCONV_NUMA_BIND", "1")
     assert bind_to_device_numa(0) is None  # this container has no GPU
     assert os.sched_getaffinity(0) == before
+
+
+@pytest.mark.parametrize("world,extra", [(2, []), (3, ["--exchange-halo", "--backend", "cpu"])])
+def test_torchrun_checkpoints(pconv_mod, tmp_path, world, extra):
+    """--checkpoint-every K under torchrun: <out>.repK holds the whole image
+    after K repetitions (every rank pwrites its band); resuming from a
+    checkpoint with the remaining repetitions gives the final image."""
+    img = np.random.default_rng(5).integers(0, 256, size=(41, 23, 3), dtype=np.uint8)
+    pconv_mod.write_raw(str(tmp_path / "pic.raw"), img)
+    r = _torchrun(world, ["pic.raw", "23", "41", "10", "rgb", "--backend", "omp", "--checkpoint-every", "4",
+                          "--check", "--json"] + extra, tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for k in (4, 8):
+        got = pconv_mod.read_raw(str(tmp_path / f"blur_pic.raw.rep{k}"), 23, 41, "rgb")
+        assert np.array_equal(got, pconv_mod.numpy_convolve(img, k)), k
+    assert not (tmp_path / "blur_pic.raw.rep12").exists()
+    r = _torchrun(world, ["blur_pic.raw.rep8", "23", "41", "2", "rgb", "--backend", "omp", "--out", "resumed.raw"]
+                  + extra, tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert np.array_equal(pconv_mod.read_raw(str(tmp_path / "resumed.raw"), 23, 41, "rgb"),
+                          pconv_mod.numpy_convolve(img, 10))
+
+
+def test_preload_ghost_zone_covers_all_reps():
+    """Pre-loaded ghost rows must carry every repetition (no exchange at all);
+    bands shorter than `reps` fall back to the exchange cap."""
+    from pconv.parallel.dist_engine import AUTO_HALO_CAP, auto_halo, preload_is_exchange_free
+
+    assert auto_halo(8192, 8, 100, 8, preload=True) == 100
+    assert auto_halo(32768, 8, 200, 8, preload=True) == 200
+    assert auto_halo(32768, 8, 200, 8) == AUTO_HALO_CAP
+    assert auto_halo(200, 4, 100, 8, preload=True) == 50
+    assert preload_is_exchange_free(32768, 8, 200) and not preload_is_exchange_free(200, 4, 100)
+    assert auto_halo(2520, 1, 40, 8, preload=True) == 8
+
+
+def test_bench_metric_names():
+    import importlib.util
+    from types import SimpleNamespace
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    a = SimpleNamespace(width=1920, height=2520, channels="rgb", reps=40, filter="gaussian")
+    assert bench.metric_for(a) == bench.METRIC
+    a = SimpleNamespace(width=8192, height=8192, channels="rgb", reps=100, filter="gaussian")
+    assert bench.metric_for(a) == "Mpixels/sec (and wall-time) for 8192x8192 RGB, 100 reps at 1/2/4/8 MI355X"
+    a = SimpleNamespace(width=1920, height=2520, channels="rgb", reps=40, filter="box")
+    assert "box" in bench.metric_for(a) and bench.metric_for(a) != bench.METRIC

@@ -5,8 +5,11 @@ set -euo pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r02/probe2
 mkdir -p "$O"
-timeout -k 10 500 python3 -u -m pytest tests/test_gpu_halo.py -x -v --timeout 120 --timeout-method thread > "$O/pytest_halo.log" 2>&1 || { tail -n 60 "$O/pytest_halo.log"; exit 1; }
-tail -n 2 "$O/pytest_halo.log"
+rc=0
+timeout -k 10 500 python3 -u -m pytest tests/test_gpu_halo.py -v --timeout 120 --timeout-method thread > "$O/pytest_halo.log" 2>&1 || rc=$?
+tail -n 8 "$O/pytest_halo.log"
+# test failures (rc 1) are read afterwards; anything else (timeout, abort, crash) ends the call
+if [ "$rc" -gt 1 ]; then exit "$rc"; fi
 timeout -k 10 300 python3 -u tools/ref_tables.py cuda --out "$O/cuda.jsonl" > "$O/cuda.log" 2>&1
 echo cuda table ok
 timeout -k 10 120 python3 -u tools/ref_tables.py mpi-gpu --out "$O/mpi_gpu.jsonl" > "$O/mpi_gpu.log" 2>&1
