@@ -39,9 +39,15 @@ struct AppReport {
 // Runs the CLI (argv as given).  Returns the process exit code.
 int conv_main(int argc, char** argv);
 
+// Engines / staging kept by a resident server between jobs (service.hpp).
+struct JobCache;
+JobCache* new_job_cache(int device, int max_engines);
+void delete_job_cache(JobCache* c);
+
 // Library entry: run a parsed config in this process (1 GPU or CPU), or via
-// the fork launcher when cfg.gpus > 1.
-AppReport run_app(const CliConfig& cfg);
+// the fork launcher when cfg.gpus > 1.  With a cache (resident server) the
+// device context is already up and engines are reused across jobs.
+AppReport run_app(const CliConfig& cfg, JobCache* cache = nullptr);
 
 std::string report_json(const CliConfig& cfg, const AppReport& r);
 

@@ -48,6 +48,7 @@ struct CliConfig {
   std::string transport = "rccl";  // multi-GPU halo transport: rccl | shm (host-staged, shared memory)
   bool preload_halo = true;        // ranks read their ghost rows from the input (no exchange at start)
   int warmup = 1;                  // untimed runs of the whole schedule on the zeroed frames first
+  std::string server;              // client mode: run the job on the resident server at this socket
 };
 
 // Parse argv.  Throws pconv::Error with the message to print on bad input.

@@ -42,4 +42,16 @@ void cpu_fused_launch(const Filter& f, Channels ch, const FrameLayout& lay, cons
 void cpu_convolve(const Filter& f, const ImageGeom& geom, const uint8_t* in, uint8_t* out,
                   int reps, CpuBackend be, int threads = 0);
 
+// OpenMP team size when the user set none (OMP_NUM_THREADS unset, no
+// --threads): the CPUs this process may run on (affinity mask), capped by the
+// cgroup CPU quota (a container or GPU-box slice sees every CPU of the
+// machine but may use only its quota), minus one when more than two remain —
+// a fork/join team that claims EVERY available CPU while anything else runs
+// spins into the scheduler (measured 10 ms per parallel region with 8
+// threads on 8 busy vCPUs vs 5 us with 7).
+int default_cpu_threads();
+// Apply default_cpu_threads() unless OMP_NUM_THREADS is set; `share` divides
+// the CPUs between that many processes (ranks on one node).  Returns the team size.
+int configure_cpu_threads(int share = 1);
+
 }  // namespace pconv

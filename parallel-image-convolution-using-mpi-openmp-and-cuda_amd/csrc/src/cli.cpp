@@ -53,7 +53,12 @@ std::string help_text(const std::string& prog) {
          "  --exchange-halo           ranks load only their own rows; ghost rows come from neighbours\n"
          "  --warmup N                untimed runs of the schedule before loading the image (default 1;\n"
          "                            loads the kernels' code objects and sets up RCCL connections)\n"
-         "  --quiet                   suppress the timing lines\n";
+         "  --quiet                   suppress the timing lines\n"
+         "  --server SOCKET           run the job on a resident `conv --serve SOCKET` (warm GPU context)\n"
+         "\n"
+         "       " + prog + " --serve SOCKET [--device D] [--idle-timeout S] [--max-engines N]\n"
+         "                            resident service: initialise the GPU once, then run jobs sent by\n"
+         "                            `--server SOCKET` clients one at a time\n";
 }
 
 CliConfig parse_cli(const std::vector<std::string>& args) {
@@ -134,6 +139,8 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
         PCONV_FAIL("invalid --transport '" + c.transport + "' (rccl|shm)");
     } else if (a == "--exchange-halo") {
       c.preload_halo = false;
+    } else if (a == "--server") {
+      c.server = next("--server");
     } else if (a == "--warmup") {
       c.warmup = static_cast<int>(parse_int(next("--warmup"), "--warmup", 0, 100));
     } else {

@@ -6,8 +6,11 @@
 #include "pconv/cpu_stencil.hpp"
 
 #include <omp.h>
+#include <sched.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -128,6 +131,52 @@ void cpu_fused_launch(const Filter& f, Channels ch, const FrameLayout& lay, cons
   }
 }
 
+namespace {
+
+int cgroup_cpu_quota() {
+  // cgroup v2: "max 100000" or "<quota> <period>"; v1: cfs_quota_us / cfs_period_us.
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long period = 0;
+    const int n = std::fscanf(f, "%31s %lld", q, &period);
+    std::fclose(f);
+    if (n == 2 && std::strcmp(q, "max") != 0 && period > 0) {
+      const long long quota = std::atoll(q);
+      if (quota > 0) return static_cast<int>((quota + period - 1) / period);
+    }
+    return 0;
+  }
+  long long quota = -1, period = 0;
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+    if (std::fscanf(f, "%lld", &quota) != 1) quota = -1;
+    std::fclose(f);
+  }
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+    if (std::fscanf(f, "%lld", &period) != 1) period = 0;
+    std::fclose(f);
+  }
+  return quota > 0 && period > 0 ? static_cast<int>((quota + period - 1) / period) : 0;
+}
+
+}  // namespace
+
+int default_cpu_threads() {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : omp_get_num_procs();
+  const int q = cgroup_cpu_quota();
+  if (q > 0) n = std::min(n, q);
+  if (n > 2) n -= 1;
+  return std::max(1, n);
+}
+
+int configure_cpu_threads(int share) {
+  if (std::getenv("OMP_NUM_THREADS")) return omp_get_max_threads();
+  const int n = std::max(1, default_cpu_threads() / std::max(1, share));
+  omp_set_num_threads(n);
+  return n;
+}
+
 void cpu_convolve(const Filter& f, const ImageGeom& geom, const uint8_t* in, uint8_t* out, int reps, CpuBackend be,
                   int threads) {
   geom.validate();
@@ -137,6 +186,7 @@ void cpu_convolve(const Filter& f, const ImageGeom& geom, const uint8_t* in, uin
   std::vector<uint8_t> fa(static_cast<size_t>(lay.bytes()), 0), fb(static_cast<size_t>(lay.bytes()), 0);
   for (int64_t r = 0; r < geom.height; ++r) std::memcpy(fa.data() + lay.offset(r), in + r * rb, rb);
   const int saved = omp_get_max_threads();
+  if (be == CpuBackend::OpenMP && threads <= 0 && !std::getenv("OMP_NUM_THREADS")) threads = default_cpu_threads();
   if (be == CpuBackend::OpenMP && threads > 0) omp_set_num_threads(threads);
   uint8_t* src = fa.data();
   uint8_t* dst = fb.data();

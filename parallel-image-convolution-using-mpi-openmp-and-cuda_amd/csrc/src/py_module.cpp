@@ -181,6 +181,10 @@ PYBIND11_MODULE(_pconv_native, m) {
       },
       py::arg("src"), py::arg("dst"), py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("reps"),
       py::arg("filter") = "gaussian", py::arg("omp") = false, py::arg("threads") = 0);
+  m.def("default_cpu_threads", &default_cpu_threads,
+        "OpenMP team size used when none is set: affinity CPUs capped by the cgroup quota, minus one");
+  m.def("configure_cpu_threads", &configure_cpu_threads, py::arg("share") = 1,
+        "Size the OpenMP team (unless OMP_NUM_THREADS is set) for `share` processes on this node");
   m.def(
       "cpu_fused_launch",
       [](py::object filter, const std::string& ch, int64_t row_bytes, int64_t rows, int64_t halo, py::buffer src,

@@ -181,6 +181,8 @@ def main(argv: Optional[List[str]] = None) -> int:
                 n.bind_to_device_numa(device)
             runner = _HipBand(a, rank, world, device)
         else:
+            if a.backend == "omp":  # the node's CPUs split between the ranks on it (MPI+OpenMP hybrid)
+                n.configure_cpu_threads(int(os.environ.get("LOCAL_WORLD_SIZE", world)))
             runner = _CpuBand(a, rank, world, omp=a.backend == "omp")
         b = runner.band
         rb = a.width * _CH[a.channels]

@@ -1,0 +1,109 @@
+"""Resident service (`conv --serve` / `--server`): protocol, path handling
+and results on the CPU backends (a `--device -1` server), plus the GPU
+server under the gpu marker.  The server keeps the device context, engines,
+pinned staging and tuned kernels between jobs; the client prints the
+reference's timing lines with its own end-to-end clock."""
+import json
+import os
+import socket
+import struct
+import subprocess
+import time
+
+import numpy as np
+import pytest
+
+from conftest import CONV_BIN
+
+
+def _request(sock, *args):
+    s = socket.socket(socket.AF_UNIX)
+    s.connect(sock)
+    msg = struct.pack("I", len(args))
+    for a in args:
+        b = a.encode()
+        msg += struct.pack("I", len(b)) + b
+    s.sendall(msg)
+    n = struct.unpack("I", s.recv(4))[0]
+    data = b""
+    while len(data) < n:
+        data += s.recv(n - len(data))
+    s.close()
+    return json.loads(data)
+
+
+@pytest.fixture
+def server(tmp_path, request):
+    device = getattr(request, "param", -1)
+    sock = str(tmp_path / "pconv.sock")
+    p = subprocess.Popen([CONV_BIN, "--serve", sock, "--device", str(device), "--idle-timeout", "300"],
+                         stderr=subprocess.PIPE, text=True)
+    for _ in range(600):
+        if os.path.exists(sock):
+            break
+        if p.poll() is not None:
+            raise RuntimeError(p.stderr.read())
+        time.sleep(0.05)
+    yield sock
+    try:
+        _request(sock, "__shutdown__")
+    finally:
+        p.wait(timeout=60)
+
+
+def test_service_cpu_jobs(pconv_mod, server, tmp_path, rng):
+    img = rng.integers(0, 256, size=(37, 53, 3), dtype=np.uint8)
+    pconv_mod.write_raw(str(tmp_path / "in.raw"), img)
+    for backend, reps in (("cpu", 3), ("omp", 7), ("cpu", 0)):
+        r = subprocess.run([CONV_BIN, "in.raw", "53", "37", str(reps), "rgb", "--backend", backend, "--server",
+                            server, "--json", "--check", "--format", "both"], cwd=tmp_path, capture_output=True,
+                           text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        lines = r.stdout.strip().splitlines()
+        float(lines[0])
+        assert lines[1].startswith("Execution time:")
+        meta = json.loads(lines[2])
+        assert meta["served"] and meta["mismatches"] == 0 and meta["client_e2e_s"] > 0
+        # default output next to the input, resolved in the CLIENT's directory
+        out = pconv_mod.read_raw(str(tmp_path / "blur_in.raw"), 53, 37, "rgb")
+        assert np.array_equal(out, pconv_mod.numpy_convolve(img, reps))
+    assert _request(server, "__ping__")["jobs"] == 3
+
+
+def test_service_errors_are_reported(server, tmp_path):
+    r = subprocess.run([CONV_BIN, "missing.raw", "8", "8", "1", "grey", "--backend", "cpu", "--server", server],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "server:" in r.stderr
+    r = subprocess.run([CONV_BIN, "x.raw", "8", "8", "1", "grey", "--synthetic", "1", "--server", server],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "no GPU" in r.stderr  # a --device -1 server runs the CPU backends only
+    assert "error" in _request(server, "conv", "x.raw", "8")  # usage error comes back as JSON
+    assert _request(server, "__ping__")["ok"]  # the server survives bad jobs
+
+
+def test_client_without_server(tmp_path):
+    r = subprocess.run([CONV_BIN, "x.raw", "8", "8", "1", "grey", "--synthetic", "1", "--server",
+                        str(tmp_path / "none.sock")], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "conv --serve" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("server", [0], indirect=True)
+def test_service_gpu_jobs_reuse_engines(pconv_mod, server, tmp_path, rng):
+    """GPU jobs through one warm server: different geometries, repeated
+    geometries (cached engine), checkpoints; every output exact."""
+    jobs = [(61, 45, "rgb", 9), (200, 130, "grey", 40), (61, 45, "rgb", 13), (61, 45, "rgb", 9)]
+    times = []
+    for i, (w, h, ch, reps) in enumerate(jobs):
+        c = 3 if ch == "rgb" else 1
+        img = rng.integers(0, 256, size=(h, w, c) if c > 1 else (h, w), dtype=np.uint8)
+        pconv_mod.write_raw(str(tmp_path / f"j{i}.raw"), img)
+        r = subprocess.run([CONV_BIN, f"j{i}.raw", str(w), str(h), str(reps), ch, "--server", server, "--json",
+                            "--check"], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        meta = json.loads(r.stdout.strip().splitlines()[-1])
+        assert meta["mismatches"] == 0 and "hip_init" not in meta["phases_s"]
+        times.append(meta["client_e2e_s"])
+        out = pconv_mod.read_raw(str(tmp_path / f"blur_j{i}.raw"), w, h, ch)
+        assert np.array_equal(out, pconv_mod.numpy_convolve(img, reps))
+    assert _request(server, "__ping__")["jobs"] == len(jobs)
