@@ -204,32 +204,34 @@ def spawn_ranks(a) -> int:
     return subprocess.call(cmd)
 
 
-def pcie_floor_ms(in_bytes: int, out_bytes: int, device: int, iters: int = 8):
-    """This box's copy floor for one step: an H2D of the step's input bytes
-    and a D2H of its output bytes running CONCURRENTLY (pinned host memory,
-    two streams), median of `iters`.  The pipelined step cannot beat it; it
-    makes every BENCH line self-explaining across boxes with different PCIe
-    rates (the round-1 driver box measured 0.46 ms/step where others give 0.31)."""
+def copy_floor_ms(in_bytes: int, out_bytes: int, device: int, iters: int = 8):
+    """This box's copy floor for one step: the step's H2D alone and its D2H
+    alone (pinned host memory, one stream, median of `iters`).  A pipelined
+    step cannot be shorter than the slower of the two; it makes every BENCH
+    line self-explaining across boxes with different PCIe rates (the round-1
+    driver box measured 0.46 ms/step where others give 0.31)."""
     import torch
 
     hin = torch.empty(in_bytes, dtype=torch.uint8, pin_memory=True)
     hout = torch.empty(out_bytes, dtype=torch.uint8, pin_memory=True)
     din = torch.empty(in_bytes, dtype=torch.uint8, device=device)
     dout = torch.empty(out_bytes, dtype=torch.uint8, device=device)
-    s1, s2 = torch.cuda.Stream(device), torch.cuda.Stream(device)
-    times = []
-    for i in range(iters + 2):
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        with torch.cuda.stream(s1):
-            din.copy_(hin, non_blocking=True)
-        with torch.cuda.stream(s2):
-            hout.copy_(dout, non_blocking=True)
-        torch.cuda.synchronize(device)
-        if i >= 2:
-            times.append(time.perf_counter() - t0)
-    times.sort()
-    return round(times[len(times) // 2] * 1e3, 4)
+
+    def timed(fn):
+        ts = []
+        for i in range(iters + 2):
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(device)
+            if i >= 2:
+                ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return ts[len(ts) // 2] * 1e3
+
+    h2d = timed(lambda: din.copy_(hin, non_blocking=True))
+    d2h = timed(lambda: hout.copy_(dout, non_blocking=True))
+    return h2d, d2h
 
 
 def main():
@@ -327,7 +329,9 @@ def main():
     lat.sort()
     latency_ms = max_over_ranks(lat[len(lat) // 2]) * 1e3
     b = blur.band
-    floor_ms = max_over_ranks(pcie_floor_ms(blur.inputs[0].size, b.rows * blur.row_bytes, device) / 1e3) * 1e3
+    h2d_ms, d2h_ms = copy_floor_ms(blur.inputs[0].size, b.rows * blur.row_bytes, device)
+    h2d_ms = max_over_ranks(h2d_ms / 1e3) * 1e3
+    d2h_ms = max_over_ranks(d2h_ms / 1e3) * 1e3
     if a.emulate:
         world = 1
 
@@ -393,7 +397,8 @@ def main():
                 "exchanges_per_step": int(stats.exchanges),
             },
             "latency_ms": round(latency_ms, 4),
-            "pcie_floor_ms": round(floor_ms, 4),
+            "copy_floor": {"h2d_ms": round(h2d_ms, 4), "d2h_ms": round(d2h_ms, 4),
+                           "floor_ms": round(max(h2d_ms, d2h_ms), 4)},
             "loop_only": {
                 "ms_per_step": round(loop_elapsed / ls * 1e3, 4) if ls else None,
                 "mpix_per_s": round(loop_value, 2) if loop_value else None,

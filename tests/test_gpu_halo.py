@@ -236,4 +236,4 @@ def test_bench_spawns_its_ranks():
     assert len(lines) == 1, r.stdout
     meta = json.loads(lines[0])
     assert meta["n_gpus"] == 2 and meta["mismatches"] == 0
-    assert meta["latency_ms"] > 0 and meta["pcie_floor_ms"] > 0
+    assert meta["latency_ms"] > 0 and meta["copy_floor"]["floor_ms"] > 0
