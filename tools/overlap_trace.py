@@ -67,22 +67,24 @@ def run(a):
 def analyse(a):
     d = a.trace_dir
     ks = list(csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))))
-    cp_path = os.path.join(d, "run_memory_copy_trace.csv")
-    cps = list(csv.DictReader(open(cp_path))) if os.path.exists(cp_path) else []
     halo = []  # (start, end, what, stream)
     interior = []
+    stencil_streams = {k["Stream_Id"] for k in ks if "k_swar" in k["Kernel_Name"] or "k_binomial" in k["Kernel_Name"]}
+    blits = []
     for k in ks:
         name = k["Kernel_Name"]
         s, e, st = int(k["Start_Timestamp"]), int(k["End_Timestamp"]), k["Stream_Id"]
-        if "nccl" in name.lower() or "rccl" in name.lower():
-            halo.append((s, e, "rccl:" + name.split("(")[0][:40], st))
+        if "rccl" in name.lower() or "ncclkernel" in name.lower():
+            if a.kinds == "rccl":
+                halo.append((s, e, "rccl:" + name.split("(")[0].replace("void ", "")[:30], st))
         elif "k_swar" in name or "k_binomial" in name or "k_stream" in name:
             interior.append((s, e, name.split("(")[0][-40:], st))
-        elif "copyBuffer" in name:
-            halo.append((s, e, "blit-copy", st))
-    for c in cps:
-        halo.append((int(c["Start_Timestamp"]), int(c["End_Timestamp"]), "copy:" + c["Direction"][-14:],
-                     c["Stream_Id"]))
+        elif "copyBuffer" in name and st not in stencil_streams:
+            blits.append((s, e, "D2D halo copy (blit)", st))
+    if a.kinds == "blit":
+        # halo copies = blit copies on streams that run no stencil kernel
+        # (the bands' comm streams); uploads run on the compute streams
+        halo = blits
     halo.sort()
     lines = [f"# overlap trace: {d}", "",
              f"{len(halo)} halo transfers (RCCL kernels / copies), {len(interior)} stencil launches", "",
@@ -120,6 +122,8 @@ def main():
     an.add_argument("trace_dir")
     an.add_argument("--md", default=None)
     an.add_argument("--max-rows", type=int, default=40)
+    an.add_argument("--kinds", choices=["rccl", "blit"], default="rccl",
+                    help="which transfers are halo exchanges: RCCL kernels, or D2D blit copies on comm streams")
     a = p.parse_args()
     run(a) if a.cmd == "run" else analyse(a)
 
