@@ -28,6 +28,7 @@ struct AppReport {
   int launches = 0, exchanges = 0;
   int64_t mismatches = -1; // --check result (-1 = not checked)
   std::string kernel;
+  std::string copies;  // 1 GPU: "sdma" | "kernel" host<->device copies
   std::string output;
   // End-to-end breakdown (seconds, in order): the reference's timer covers
   // everything after argument parsing (cuda/main.c:20-49), HIP/CUDA context

@@ -49,6 +49,7 @@ struct CliConfig {
   bool preload_halo = true;        // ranks read their ghost rows from the input (no exchange at start)
   int warmup = 1;                  // untimed runs of the whole schedule on the zeroed frames first
   std::string server;              // client mode: run the job on the resident server at this socket
+  int copies = -1;                 // host<->device copies: -1 auto, 0 SDMA (hipMemcpy2DAsync), 1 CU kernels
 };
 
 // Parse argv.  Throws pconv::Error with the message to print on bad input.

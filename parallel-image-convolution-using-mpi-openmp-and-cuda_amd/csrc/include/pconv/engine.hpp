@@ -61,6 +61,11 @@ struct EngineOptions {
   // the pinned host output (zero-copy D2H fused into the producing kernel)
   // instead of a separate D2H copy — when the filter / row size allow it.
   bool zero_copy_out = false;
+  // Host <-> frame copies (upload_rows / download_rows) and the initial frame
+  // zeroing by kernels of this library instead of SDMA / the runtime's blit
+  // programs: a one-shot process (the `conv` CLI) skips their first-use
+  // set-up; the serving pipeline keeps SDMA (faster per byte, frees the CUs).
+  bool kernel_copies = false;
 };
 
 struct RunStats {

@@ -70,4 +70,15 @@ void prepare_stencil(const Filter& f, Channels ch, const StencilLaunch& a, hipSt
 // Whether `v` (or Auto) can fuse `steps` > 1 for this filter.
 bool supports_fusion(const Filter& f, KernelVariant v);
 
+// Row copy by the CUs: `rows` rows of `row_bytes` from src (row pitch sp) to
+// dst (row pitch dp); either side may be pinned host memory (the CUs move the
+// bytes over PCIe) or device memory.  No SDMA engine and no runtime blit
+// program is involved — a one-shot process saves their first-use set-up
+// (~8 ms per SDMA direction and the blit code object, profiles/r02/), at
+// 44-53 GB/s instead of SDMA's 54 (tools/ubench/copy_bw.hip).
+void launch_copy_rows(const uint8_t* src, int64_t sp, uint8_t* dst, int64_t dp, int64_t row_bytes, int64_t rows,
+                      hipStream_t stream);
+// Zero `bytes` (a multiple of 16, 16-byte aligned) with a kernel of this module.
+void launch_fill_zero(uint8_t* p, int64_t bytes, hipStream_t stream);
+
 }  // namespace pconv

@@ -1011,6 +1011,60 @@ std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned() {
   return out;
 }
 
+namespace {
+
+// 16 bytes per lane, grid-stride over (row, 16-byte chunk); rows whose start
+// is not 16-byte aligned on either side fall back to dwords or bytes.
+__global__ __launch_bounds__(256) void k_copy_rows(const uint8_t* __restrict__ src, int64_t sp,
+                                                   uint8_t* __restrict__ dst, int64_t dp, int64_t row_bytes,
+                                                   int64_t chunks_per_row, int64_t total) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t y = i / chunks_per_row, x = (i - y * chunks_per_row) * 16;
+    const uint8_t* s = src + y * sp + x;
+    uint8_t* d = dst + y * dp + x;
+    const int n = static_cast<int>(min<int64_t>(16, row_bytes - x));
+    const uintptr_t al = reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d);
+    if (n == 16 && (al & 15) == 0) {
+      *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+    } else if (n == 16 && (al & 3) == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) reinterpret_cast<u32*>(d)[k] = reinterpret_cast<const u32*>(s)[k];
+    } else {
+      for (int k = 0; k < n; ++k) d[k] = s[k];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fill_zero(uint4* __restrict__ p, int64_t n16) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += stride)
+    p[i] = make_uint4(0, 0, 0, 0);
+}
+
+unsigned copy_blocks(int64_t work) {
+  // enough waves to keep PCIe / HBM busy (256 CUs x 8), never more than the work
+  return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div<int64_t>(work, 256), 2048)));
+}
+
+}  // namespace
+
+void launch_copy_rows(const uint8_t* src, int64_t sp, uint8_t* dst, int64_t dp, int64_t row_bytes, int64_t rows,
+                      hipStream_t stream) {
+  PCONV_CHECK(row_bytes >= 0 && rows >= 0 && sp >= row_bytes && dp >= row_bytes, "copy_rows: bad geometry");
+  if (row_bytes == 0 || rows == 0) return;
+  const int64_t cpr = ceil_div<int64_t>(row_bytes, 16), total = cpr * rows;
+  k_copy_rows<<<dim3(copy_blocks(total)), dim3(256), 0, stream>>>(src, sp, dst, dp, row_bytes, cpr, total);
+  PCONV_HIP_CHECK(hipGetLastError());
+}
+
+void launch_fill_zero(uint8_t* p, int64_t bytes, hipStream_t stream) {
+  PCONV_CHECK(bytes % 16 == 0 && reinterpret_cast<uintptr_t>(p) % 16 == 0, "fill_zero: needs 16-byte granules");
+  if (bytes == 0) return;
+  k_fill_zero<<<dim3(copy_blocks(bytes / 16)), dim3(256), 0, stream>>>(reinterpret_cast<uint4*>(p), bytes / 16);
+  PCONV_HIP_CHECK(hipGetLastError());
+}
+
 void prepare_swar(const StencilLaunch& a, Channels ch, hipStream_t stream) { (void)tuned_choice(a, ch, stream, true); }
 
 void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream) {

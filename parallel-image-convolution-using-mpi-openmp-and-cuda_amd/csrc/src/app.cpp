@@ -175,7 +175,7 @@ double seconds_since_exec() {
 // (geometry, filter, launch options), least recently used first out, and one
 // pinned staging buffer grown on demand.
 struct JobCache {
-  using Key = std::tuple<int64_t, int64_t, int, std::string, int, int, int, bool, bool>;
+  using Key = std::tuple<int64_t, int64_t, int, std::string, int, int, int, bool, bool, bool>;
   std::list<std::pair<Key, std::unique_ptr<BandEngine>>> engines;
   PinnedBuffer host;
   int max_engines = 8;
@@ -184,7 +184,7 @@ struct JobCache {
   BandEngine& engine(const ImageGeom& g, const Filter& f, const EngineOptions& o, const std::string& fname,
                      bool* fresh) {
     const Key k{g.width, g.height, channel_count(g.channels), fname, o.fuse, o.halo_depth,
-                static_cast<int>(o.variant), o.overlap, o.use_graph};
+                static_cast<int>(o.variant), o.overlap, o.use_graph, o.kernel_copies};
     for (auto it = engines.begin(); it != engines.end(); ++it)
       if (it->first == k) {
         engines.splice(engines.begin(), engines, it);
@@ -240,6 +240,9 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   load_rows(c, g, 0, g.height, host, g.row_bytes());
   pc.mark(c.synthetic ? "synthesize" : "read");
   EngineOptions o = engine_options(c, g, 1, device);
+  // One-shot process: CU copies skip the SDMA / blit first-use set-up; a
+  // resident server has paid it once and keeps SDMA.
+  o.kernel_copies = c.copies < 0 ? cache == nullptr : c.copies == 1;
   std::unique_ptr<BandEngine> own_eng;
   bool fresh = true;
   if (cache) {
@@ -286,6 +289,7 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   r.halo = eng.options().halo_depth;
   r.fuse = eng.options().fuse;
   r.kernel = kernel_variant_name(eng.options().variant);
+  r.copies = eng.options().kernel_copies ? "kernel" : "sdma";
   if (c.check) r.mismatches = compare_with_oracle(c, g, host);
   r.since_exec_s = seconds_since_exec();
   return r;
@@ -565,6 +569,7 @@ std::string report_json(const CliConfig& c, const AppReport& r) {
      << ", \"e2e_mpix_per_s\": " << (r.e2e_s > 0 ? px / r.e2e_s / 1e6 : 0.0)
      << ", \"mismatches\": " << r.mismatches << ", \"output\": \"" << r.output << "\""
      << ", \"rccl_loaded\": " << (rccl_loaded() ? "true" : "false");
+  if (!r.copies.empty()) os << ", \"copies\": \"" << r.copies << "\"";
   if (!r.phases.empty()) {
     os << ", \"phases_s\": {";
     for (size_t i = 0; i < r.phases.size(); ++i)

@@ -55,6 +55,8 @@ std::string help_text(const std::string& prog) {
          "                            loads the kernels' code objects and sets up RCCL connections)\n"
          "  --quiet                   suppress the timing lines\n"
          "  --server SOCKET           run the job on a resident `conv --serve SOCKET` (warm GPU context)\n"
+         "  --copies {auto,sdma,kernel}  1-GPU host<->device copies: SDMA engines or CU kernels (auto:\n"
+         "                            kernels in a one-shot process, SDMA in a resident server)\n"
          "\n"
          "       " + prog + " --serve SOCKET [--device D] [--idle-timeout S] [--max-engines N]\n"
          "                            resident service: initialise the GPU once, then run jobs sent by\n"
@@ -139,6 +141,12 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
         PCONV_FAIL("invalid --transport '" + c.transport + "' (rccl|shm)");
     } else if (a == "--exchange-halo") {
       c.preload_halo = false;
+    } else if (a == "--copies") {
+      const std::string v = next("--copies");
+      if (v == "auto") c.copies = -1;
+      else if (v == "sdma") c.copies = 0;
+      else if (v == "kernel") c.copies = 1;
+      else PCONV_FAIL("invalid --copies '" + v + "' (auto|sdma|kernel)");
     } else if (a == "--server") {
       c.server = next("--server");
     } else if (a == "--warmup") {

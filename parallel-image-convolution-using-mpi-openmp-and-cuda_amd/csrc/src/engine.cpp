@@ -32,15 +32,21 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
   opt_.halo_depth = c.halo_depth;
   set_device(opt_.device);
   lay_ = FrameLayout::make(geom_.row_bytes(), band_.rows, std::max(1, opt_.halo_depth));
-  for (auto& f : frame_) {
-    f = DeviceBuffer(static_cast<size_t>(lay_.bytes()));
-    PCONV_HIP_CHECK(hipMemset(f.data(), 0, f.size()));
-  }
   if (opt_.compute_stream) {
     cs_ = opt_.compute_stream;
   } else {
     own_cs_ = Stream::create(0);
     cs_ = own_cs_.get();
+  }
+  // Zero the frames on the compute stream (not the null stream: a one-shot
+  // process then creates one hardware queue instead of two, ~10 ms each on
+  // first use; profiles/r02/raw/init_*.jsonl).
+  for (auto& f : frame_) {
+    f = DeviceBuffer(static_cast<size_t>(lay_.bytes()));
+    if (opt_.kernel_copies)
+      launch_fill_zero(f.data(), static_cast<int64_t>(f.size()), cs_);
+    else
+      PCONV_HIP_CHECK(hipMemsetAsync(f.data(), 0, f.size(), cs_));
   }
   // Communication stream only when the band has neighbours (or is borrowed).
   if (opt_.comm_stream) {
@@ -56,7 +62,7 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
   ev_sync_ = Event::create();
   ev_t0_ = Event::create(true);
   ev_t1_ = Event::create(true);
-  PCONV_HIP_CHECK(hipDeviceSynchronize());
+  PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
 }
 
 BandEngine::~BandEngine() {
@@ -78,7 +84,8 @@ void BandEngine::trim_graph_caches() {
 
 void BandEngine::clear() {
   synchronize();
-  for (auto& f : frame_) PCONV_HIP_CHECK(hipMemset(f.data(), 0, f.size()));
+  for (auto& f : frame_) PCONV_HIP_CHECK(hipMemsetAsync(f.data(), 0, f.size(), cs_));
+  PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
   halo_valid_ = false;
 }
 
@@ -90,6 +97,11 @@ void BandEngine::upload_rows(const uint8_t* host, int64_t host_pitch, int64_t r_
   // Rows beyond the global image edge must stay zero.
   PCONV_CHECK(band_.y0 + r_begin >= 0 && band_.y0 + r_end <= geom_.height, "upload_rows: rows outside image");
   if (r_end == r_begin) return;
+  if (opt_.kernel_copies) {
+    launch_copy_rows(host, host_pitch, src_frame() + r_begin * lay_.pitch, lay_.pitch, lay_.row_bytes,
+                     r_end - r_begin, stream ? stream : cs_);
+    return;
+  }
   PCONV_HIP_CHECK(hipMemcpy2DAsync(src_frame() + r_begin * lay_.pitch, lay_.pitch, host, host_pitch, lay_.row_bytes,
                                    r_end - r_begin, hipMemcpyHostToDevice, stream ? stream : cs_));
 }
@@ -107,6 +119,11 @@ void BandEngine::download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begi
                                hipStream_t stream) {
   PCONV_CHECK(r_begin >= 0 && r_end <= lay_.rows && r_begin <= r_end, "download_rows: rows outside band");
   if (r_end == r_begin) return;
+  if (opt_.kernel_copies) {
+    launch_copy_rows(src_frame() + r_begin * lay_.pitch, lay_.pitch, host, host_pitch, lay_.row_bytes, r_end - r_begin,
+                     stream ? stream : cs_);
+    return;
+  }
   PCONV_HIP_CHECK(hipMemcpy2DAsync(host, host_pitch, src_frame() + r_begin * lay_.pitch, lay_.pitch, lay_.row_bytes,
                                    r_end - r_begin, hipMemcpyDeviceToHost, stream ? stream : cs_));
 }

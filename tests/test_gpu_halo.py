@@ -237,3 +237,39 @@ def test_bench_spawns_its_ranks():
     meta = json.loads(lines[0])
     assert meta["n_gpus"] == 2 and meta["mismatches"] == 0
     assert meta["latency_ms"] > 0 and meta["copy_floor"]["floor_ms"] > 0
+
+
+@pytest.mark.parametrize("w,h,ch", [(61, 45, "rgb"), (1920, 64, "grey"), (33, 17, "rgba"), (1, 1, "grey"),
+                                    (257, 300, "rgb")])
+def test_kernel_copies_bit_exact(pconv_mod, rng, w, h, ch):
+    """Host<->frame copies by CU kernels (the one-shot CLI path): unaligned
+    row sizes and pinned or pageable host buffers, every byte exact, nothing
+    written past the host rows (guard bytes)."""
+    n = pconv_mod.native
+    c = {"grey": 1, "rgb": 3, "rgba": 4}[ch]
+    eng = n.BandEngine(w, h, ch, "gaussian", 0, 1, 0, halo=8, fuse=8, kernel_copies=True)
+    img = rng.integers(0, 256, size=h * w * c, dtype=np.uint8)
+    pin_in, pin_out = n.PinnedBuffer(img.size + 64), n.PinnedBuffer(img.size + 64)
+    np.asarray(pin_in)[:img.size] = img
+    np.asarray(pin_out)[:] = 0xAB
+    eng.upload_ptr(pin_in.ptr, w * c, 0, h)
+    eng.run(11)
+    eng.download_ptr(pin_out.ptr, w * c, 0, h)
+    eng.synchronize()
+    got = np.asarray(pin_out)
+    ref = pconv_mod.numpy_convolve(img.reshape(h, w, c) if c > 1 else img.reshape(h, w), 11).reshape(-1)
+    assert np.array_equal(got[:img.size], ref)
+    assert (got[img.size:] == 0xAB).all()
+
+
+@pytest.mark.parametrize("copies", ["kernel", "sdma"])
+def test_cli_copies_modes(pconv_mod, tmp_path, rng, copies):
+    from conftest import CONV_BIN
+
+    img = rng.integers(0, 256, size=(77, 61, 3), dtype=np.uint8)
+    pconv_mod.write_raw(str(tmp_path / "img.raw"), img)
+    r = subprocess.run([CONV_BIN, "img.raw", "61", "77", "9", "rgb", "--copies", copies, "--json", "--check"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    meta = json.loads(r.stdout.strip().splitlines()[-1])
+    assert meta["copies"] == copies and meta["mismatches"] == 0
