@@ -669,14 +669,20 @@ void launch_stream_one(const StencilLaunch& a, hipStream_t s, bool alt, int segf
                                                           g.pair_stride, g.seg_rows, g.nwaves);
 }
 
-// Instantiated (NP, T): 4-byte lanes, 8 levels (~190 VGPRs: the rolling
-// state of 8 levels x 4 pairs, double-buffered, plus an 8-row load ring);
-// 16 levels or 8-byte lanes do not fit the register file.
-bool stream_supported(int ch, int np, int steps) { return np >= ch && np == 4 && steps == 8; }
+// Instantiated (NP, T): 4-byte lanes, 4 / 6 / 8 levels.  The rolling state
+// is 2 x T x 4 pairs double-buffered plus T x 4 skewed rows and an 8-row load
+// ring: ~190 VGPRs at T = 8 (2 waves/SIMD), ~150 at 6, ~110 at 4 (4
+// waves/SIMD) — fewer levels per launch, more launches, but no vertical
+// redundancy at all, which matters most for frames beyond the Infinity Cache
+// (the tile kernel's fixed cost per launch is its trapezoid and its load/store
+// phases).  16 levels or 8-byte lanes do not fit the register file.
+bool stream_supported(int ch, int np, int steps) { return np >= ch && np == 4 && (steps == 4 || steps == 6 || steps == 8); }
 
 template <int CH>
 void launch_stream_ch(const StencilLaunch& a, hipStream_t s, StreamCfg c, bool alt) {
   if (c.np == 4 && a.steps == 8) return launch_stream_one<CH, 4, 8>(a, s, alt, c.segf);
+  if (c.np == 4 && a.steps == 6) return launch_stream_one<CH, 4, 6>(a, s, alt, c.segf);
+  if (c.np == 4 && a.steps == 4) return launch_stream_one<CH, 4, 4>(a, s, alt, c.segf);
   PCONV_FAIL("stream kernel: unsupported (lanes, steps)");
 }
 

@@ -193,8 +193,9 @@ def test_every_swar_shape_bit_exact(native, rng, form):
         native.set_swar_alt(-1)
 
 
+@pytest.mark.parametrize("steps", [4, 6, 8])
 @pytest.mark.parametrize("form", [0, 1])
-def test_row_streaming_kernel_bit_exact(native, rng, form):
+def test_row_streaming_kernel_bit_exact(native, rng, form, steps):
     """The row-streaming form of the fused gaussian (forced; off by default):
     whole images and band regions with ghost rows / image edges, guard-band
     canaries and untouched rows outside [r0, r1) (checked by _run_fused)."""
@@ -206,11 +207,11 @@ def test_row_streaming_kernel_bit_exact(native, rng, form):
             c = CH[channels]
             for (h, w) in [(1, 7), (9, 5), (71, 301), (200, 1000)]:
                 img = rng.integers(0, 256, size=(h, w, c) if c > 1 else (h, w), dtype=np.uint8)
-                gpu, cpu = _run_fused(native, img, 8, 0, h, 8, 0, h, variant="temporal")
+                gpu, cpu = _run_fused(native, img, steps, 0, h, steps, 0, h, variant="temporal")
                 assert np.array_equal(gpu, cpu), (channels, h, w)
             img = rng.integers(0, 256, size=(40, 301, c) if c > 1 else (40, 301), dtype=np.uint8)
             for g_row0, H in ((30, 200), (0, 45), (160, 200)):
-                gpu, cpu = _run_fused(native, img, 8, -5, 45, 16, g_row0, H, variant="temporal")
+                gpu, cpu = _run_fused(native, img, steps, -5, 45, 16, g_row0, H, variant="temporal")
                 assert np.array_equal(gpu[11:61], cpu[11:61]), (channels, g_row0, "band")
         assert any(k[5] > 0 for k, _ in native.swar_tuned()), "streaming kernel was not used"
     finally:

@@ -66,10 +66,12 @@ def main():
                     best = min(best, (time.perf_counter() - t0) / a.iters)
                 res[sh] = best
             n.set_swar_shape(0, 0, 0)
+            tuned = [list(k) for k, _ in n.swar_tuned() if k[1] == f and k[2] == b.rows + 0]
             for sh, t in res.items():
                 print(json.dumps({"world": world, "band_rows": b.rows, "halo": halo, "fuse": f, "ch": a.channels,
                                   "shape": "auto" if sh is None else "%d,%d,%d" % sh,
-                                  "launches": e.stats.launches,
+                                  "launches": e.stats.launches, "stream_mode": os.environ.get("PCONV_STREAM", "0"),
+                                  "tuned_keys": tuned,
                                   "us_per_rep": None if t is None else round(t / a.reps * 1e6, 3)}), flush=True)
 
 
