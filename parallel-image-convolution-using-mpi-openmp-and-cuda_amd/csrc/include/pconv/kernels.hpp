@@ -70,6 +70,13 @@ void prepare_stencil(const Filter& f, Channels ch, const StencilLaunch& a, hipSt
 // Whether `v` (or Auto) can fuse `steps` > 1 for this filter.
 bool supports_fusion(const Filter& f, KernelVariant v);
 
+// Default repetitions per launch for a band frame of `frame_bytes`: 1 without
+// fusion; 8 for frames the Infinity Cache holds (launch overhead dominates);
+// 6 beyond 256 MB, where the tuner's 6-level row-streaming kernel (no
+// trapezoid) beats the 8-step tile kernel (32768^2 grey: 128.8 vs 135.9
+// us/rep, profiles/r02/stream_sweep.md).
+int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes);
+
 // Row copy by the CUs: `rows` rows of `row_bytes` from src (row pitch sp) to
 // dst (row pitch dp); either side may be pinned host memory (the CUs move the
 // bytes over PCIe) or device memory.  No SDMA engine and no runtime blit

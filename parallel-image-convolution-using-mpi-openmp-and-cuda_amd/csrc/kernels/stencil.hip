@@ -476,6 +476,11 @@ bool supports_fusion(const Filter& f, KernelVariant v) {
          (v == KernelVariant::Auto || v == KernelVariant::Temporal || v == KernelVariant::TemporalPk);
 }
 
+int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes) {
+  if (!supports_fusion(f, v)) return 1;
+  return frame_bytes > (int64_t(256) << 20) ? 6 : 8;
+}
+
 
 void prepare_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hipStream_t stream, KernelVariant v) {
   StencilLaunch a = a_in;

@@ -397,18 +397,19 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ src,
     }
   };
 
-  // Rolling state per level, double-buffered by row parity so the unrolled
-  // two-row body never copies registers: level t holds Hc = horizontal sum
-  // of its previous input row and Sc = that of the two previous rows.
-  // Levels are SKEWED: level t consumes the row level t-1 emitted in the
-  // PREVIOUS iteration (Y[t-1]), so the T levels of one iteration are
-  // independent (T x NP-way ILP instead of a T-long dependency chain); level
-  // t emits row i - 2t + 1 at iteration i.
-  u32 S[2][T][NP], H[2][T][NP], Y[T][NP];
+  // Rolling state per level: H = horizontal sum of the level's previous
+  // input row, S = that of the two previous rows, updated in place (the new
+  // values replace dead ones, so the register allocator renames instead of
+  // copying; a parity-double-buffered form cost 40-64 more VGPRs and one
+  // wave per SIMD).  Levels are SKEWED: level t consumes the row level t-1
+  // emitted in the PREVIOUS iteration (Y[t-1]), so the T levels of one
+  // iteration are independent (T x NP-way ILP instead of a T-long dependency
+  // chain); level t emits row i - 2t + 1 at iteration i.
+  u32 S[T][NP], H[T][NP], Y[T][NP];
 #pragma unroll
   for (int t = 0; t < T; ++t)
 #pragma unroll
-    for (int k = 0; k < NP; ++k) S[0][t][k] = H[0][t][k] = Y[t][k] = 0u;
+    for (int k = 0; k < NP; ++k) S[t][k] = H[t][k] = Y[t][k] = 0u;
   // Input rows are prefetched PF rows ahead (a ring of PF raw rows): one
   // row's T levels are ~T x 6 x NP instructions, far less than a load's
   // latency from HBM.
@@ -420,7 +421,6 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ src,
 
   auto row = [&](auto slot_c, auto safe_c, int i) {
     constexpr int Q = decltype(slot_c)::value;
-    constexpr int P = Q & 1;  // state parity (PF is even, so parity follows the slot)
     constexpr bool SAFE = decltype(safe_c)::value;  // every emitted row inside the image, no edge columns
     u32 X0[NP];
     unpack<NP>(ra[Q], rb[Q], X0);
@@ -436,14 +436,14 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ src,
       const int j = i - 2 * t - 1;  // row emitted by level t + 1
 #pragma unroll
       for (int k = 0; k < NP; ++k) {
-        const u32 Sn = H[P][t][k] + Hn[k];
-        const u32 sum = S[P][t][k] + Sn;
+        const u32 Sn = H[t][k] + Hn[k];
+        const u32 sum = S[t][k] + Sn;
         if constexpr (!ALT)
           X[k] = trunc_sum<0>(sum);
         else  // unrolled: the level parity folds at compile time
           X[k] = ((T - 1 - t) & 1) ? trunc_sum<1>(sum) /* keeps 16 x floor */ : trunc_sum<2>(sum);
-        S[P ^ 1][t][k] = Sn;
-        H[P ^ 1][t][k] = Hn[k];
+        S[t][k] = Sn;
+        H[t][k] = Hn[k];
       }
       if constexpr (!SAFE) {
         if (j < img_lo || j >= img_hi) {
@@ -528,17 +528,18 @@ int alt_mode() {
   return v;
 }
 
-// Off by default: measured slower than the tile kernel on every geometry
-// (16384^2 grey 43.7 vs 37.1 us/rep: ~190 VGPRs leave 2 waves per SIMD and
-// the level chain is latency-bound; docs/PERFORMANCE.md).  PCONV_STREAM=-1
-// lets the tuner time it, =1 forces it (tests).
+// Timed by the tuner against the tile kernel (where its segments are long
+// enough).  At 8 levels it lost everywhere (~190 VGPRs, 2 waves per SIMD;
+// docs/PERFORMANCE.md); at 6 levels (~150 VGPRs) it wins on frames beyond the
+// Infinity Cache: 32768^2 grey 128.8 vs 135.9 us/rep (profiles/r02/).
+// PCONV_STREAM=0 keeps it out of the tuning, =1 forces it (tests / A-B).
 std::atomic<int> g_stream_mode{-2};  // -2: PCONV_STREAM on first use; -1 tune, 0 off, 1 forced
 
 int stream_mode() {
   int v = g_stream_mode.load(std::memory_order_relaxed);
   if (v == -2) {
     const char* e = std::getenv("PCONV_STREAM");
-    v = !e ? 0 : e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
+    v = !e ? -1 : e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
     g_stream_mode.store(v, std::memory_order_relaxed);
   }
   return v;

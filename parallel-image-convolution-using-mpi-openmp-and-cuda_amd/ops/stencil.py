@@ -26,7 +26,6 @@ from ..models.filters import get_filter
 from .reference import numpy_convolve
 
 _CHANNELS = {1: "grey", 3: "rgb", 4: "rgba"}
-_DEFAULT_FUSE = 8
 
 
 def image_geometry(shape) -> Tuple[int, int, str]:
@@ -51,7 +50,7 @@ class Engine:
         self.filter = get_filter(filter)
         nf = self.filter.to_native()
         if fuse is None:
-            fuse = _DEFAULT_FUSE if n.supports_fusion(nf, variant) else 1
+            fuse = n.auto_fuse(nf, variant, int(width) * int(height) * {"grey": 1, "rgb": 3, "rgba": 4}[channels])
         self.width, self.height, self.channels = int(width), int(height), channels
         self.device = int(device)
         self._eng = n.BandEngine(self.width, self.height, channels, nf, 0, 1, self.device, halo=int(fuse),

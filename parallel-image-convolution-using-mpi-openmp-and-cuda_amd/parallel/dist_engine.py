@@ -21,7 +21,6 @@ from .._native import require_native
 from ..models.filters import get_filter
 from .bootstrap import env_context, make_rccl_comm
 
-DEFAULT_FUSE = 8
 AUTO_HALO_CAP = 64
 
 
@@ -68,7 +67,8 @@ class DistributedBlur:
         self.width, self.height, self.channels = int(width), int(height), channels
         nf = get_filter(filter).to_native()
         if fuse is None:
-            fuse = DEFAULT_FUSE if n.supports_fusion(nf, variant) else 1
+            ch = {"grey": 1, "rgb": 3, "rgba": 4}[channels]
+            fuse = n.auto_fuse(nf, variant, self.width * ch * (self.height // max(1, self.world)))
         if halo is None:
             halo = auto_halo(self.height, self.world, reps, fuse, preload=bool(preload_halo) and not slot_exchange)
         kw = dict(halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant, slots=int(slots),

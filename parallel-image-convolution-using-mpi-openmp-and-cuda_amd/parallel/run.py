@@ -84,10 +84,11 @@ class _HipBand:
 
     def __init__(self, a, rank, world, device):
         n = require_native()
-        from .dist_engine import DEFAULT_FUSE, auto_halo
+        from .dist_engine import auto_halo
 
         nf = get_filter(a.filter).to_native()
-        fuse = a.fuse if a.fuse is not None else (DEFAULT_FUSE if n.supports_fusion(nf, "auto") else 1)
+        frame = a.width * _CH[a.channels] * (a.height // max(1, world))
+        fuse = a.fuse if a.fuse is not None else n.auto_fuse(nf, "auto", frame)
         halo = a.halo if a.halo is not None else auto_halo(a.height, world, a.reps, fuse)
         self.eng = n.BandEngine(a.width, a.height, a.channels, nf, rank, world, device, halo=int(halo),
                                 fuse=int(fuse), overlap=not a.no_overlap)
