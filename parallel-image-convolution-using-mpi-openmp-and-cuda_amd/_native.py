@@ -38,3 +38,11 @@ def require_native():
             f"Original error: {_ERR}"
         )
     return native
+
+
+def conv_binary() -> str:
+    """Path of the in-tree `conv` CLI binary (built with the extension)."""
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bin", "conv")
+    if not os.path.exists(p):
+        raise FileNotFoundError(f"conv binary not built: {p} (run __graft_entry__.build())")
+    return p

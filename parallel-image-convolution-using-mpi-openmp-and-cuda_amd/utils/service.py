@@ -1,0 +1,115 @@
+"""Python client of the resident convolution service (``conv --serve``).
+
+The server (``csrc/src/service.cpp``) keeps one GPU context, cached engines,
+pinned staging and tuned kernels between jobs; a job is a ``conv`` argv.
+This module speaks its wire format (u32 argc, then u32 length + bytes per
+argument; reply u32 length + JSON) and starts servers for scripts and tests:
+
+    from pconv.utils.service import start_server, ServiceClient
+    srv = start_server("/tmp/pconv.sock", device=0)
+    c = ServiceClient("/tmp/pconv.sock")
+    meta = c.run("image.raw", 1920, 2520, 40, "rgb")   # -> blur_image.raw, report dict
+    c.shutdown(); srv.wait()
+
+The reference has no service: its CUDA program pays context creation in
+every run (``cuda/main.c:20-49``).
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import struct
+import subprocess
+import time
+from typing import Dict, List, Optional
+
+from .._native import conv_binary
+
+
+class ServiceError(RuntimeError):
+    pass
+
+
+class ServiceClient:
+    def __init__(self, socket_path: str, timeout: float = 600.0):
+        self.socket_path = socket_path
+        self.timeout = float(timeout)
+
+    def request(self, *args: str) -> Dict:
+        """Send one argv (args[0] is the program name or a control word)."""
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.settimeout(self.timeout)
+        try:
+            s.connect(self.socket_path)
+            msg = [struct.pack("I", len(args))]
+            for a in args:
+                b = str(a).encode()
+                msg.append(struct.pack("I", len(b)) + b)
+            s.sendall(b"".join(msg))
+            n = struct.unpack("I", _recv_exact(s, 4))[0]
+            return json.loads(_recv_exact(s, n))
+        finally:
+            s.close()
+
+    def ping(self) -> Dict:
+        return self.request("__ping__")
+
+    def shutdown(self) -> Dict:
+        return self.request("__shutdown__")
+
+    def run(self, image: str, width: int, height: int, reps: int, channels: str = "grey",
+            out: Optional[str] = None, **flags) -> Dict:
+        """One job with the CLI's contract; keyword flags map to `--flag value`
+        (`check=True` -> `--check`).  Paths are resolved here, as the server's
+        working directory is its own.  Raises ServiceError on a failed job."""
+        synthetic = flags.get("synthetic") is not None
+        argv: List[str] = ["conv", image if synthetic else os.path.abspath(image), str(width), str(height),
+                           str(reps), channels]
+        from .raw_io import output_path_for
+
+        argv += ["--out", os.path.abspath(out if out is not None else output_path_for(image))]
+        for k, v in flags.items():
+            if v is None or v is False:
+                continue
+            argv.append("--" + k.replace("_", "-"))
+            if v is not True:
+                argv.append(str(v))
+        argv.append("--json")
+        meta = self.request(*argv)
+        if "error" in meta:
+            raise ServiceError(meta["error"])
+        return meta
+
+
+def _recv_exact(s: socket.socket, n: int) -> bytes:
+    buf = b""
+    while len(buf) < n:
+        chunk = s.recv(n - len(buf))
+        if not chunk:
+            raise ServiceError("server closed the connection")
+        buf += chunk
+    return buf
+
+
+def start_server(socket_path: str, device: int = 0, idle_timeout: float = 0.0, max_engines: int = 8,
+                 wait_s: float = 120.0) -> subprocess.Popen:
+    """Start `conv --serve` as a child process and wait until it listens
+    (device -1: a CPU-only server for the cpu / omp backends)."""
+    if os.path.exists(socket_path):
+        os.unlink(socket_path)
+    p = subprocess.Popen([conv_binary(), "--serve", socket_path, "--device", str(device), "--idle-timeout",
+                          str(idle_timeout), "--max-engines", str(max_engines)], stderr=subprocess.PIPE, text=True)
+    t0 = time.time()
+    while time.time() - t0 < wait_s:
+        if os.path.exists(socket_path):
+            try:
+                ServiceClient(socket_path, timeout=10).ping()
+                return p
+            except (OSError, ServiceError):
+                pass
+        if p.poll() is not None:
+            raise ServiceError(f"server exited: {p.stderr.read()}")
+        time.sleep(0.05)
+    p.kill()
+    raise ServiceError("server did not start listening")

@@ -107,3 +107,29 @@ def test_service_gpu_jobs_reuse_engines(pconv_mod, server, tmp_path, rng):
         out = pconv_mod.read_raw(str(tmp_path / f"blur_j{i}.raw"), w, h, ch)
         assert np.array_equal(out, pconv_mod.numpy_convolve(img, reps))
     assert _request(server, "__ping__")["jobs"] == len(jobs)
+
+
+def test_python_service_client(pconv_mod, tmp_path, rng):
+    """pconv.utils.service: start a (CPU-only) server, run jobs through the
+    Python client, errors raise ServiceError, shutdown stops the process."""
+    from pconv.utils.service import ServiceClient, ServiceError, start_server
+
+    sock = str(tmp_path / "py.sock")
+    p = start_server(sock, device=-1, idle_timeout=120)
+    try:
+        c = ServiceClient(sock)
+        img = rng.integers(0, 256, size=(29, 31), dtype=np.uint8)
+        pconv_mod.write_raw(str(tmp_path / "g.raw"), img)
+        meta = c.run(str(tmp_path / "g.raw"), 31, 29, 6, "grey", backend="omp", check=True)
+        assert meta["mismatches"] == 0 and meta["output"].endswith("blur_g.raw")
+        out = pconv_mod.read_raw(str(tmp_path / "blur_g.raw"), 31, 29, "grey")
+        assert np.array_equal(out, pconv_mod.numpy_convolve(img, 6))
+        meta = c.run("x.raw", 16, 16, 2, "rgb", out=str(tmp_path / "s.raw"), backend="cpu", synthetic=5)
+        assert meta["mismatches"] == -1 and os.path.getsize(tmp_path / "s.raw") == 16 * 16 * 3
+        with pytest.raises(ServiceError):
+            c.run(str(tmp_path / "missing.raw"), 8, 8, 1, "grey", backend="cpu")
+        assert c.ping()["jobs"] == 2
+    finally:
+        ServiceClient(sock).shutdown()
+        p.wait(timeout=60)
+    assert p.returncode == 0 and not os.path.exists(sock)
