@@ -87,6 +87,7 @@ class BandEngine {
   const EngineOptions& options() const { return opt_; }
   static constexpr size_t kMaxCachedGraphs = 64;
   size_t cached_graphs() const { return graphs_.size() + step_graphs_.size(); }
+  size_t cached_step_graphs() const { return step_graphs_.size(); }
   hipStream_t compute_stream() const { return cs_; }
   hipStream_t comm_stream() const { return ms_; }
 

@@ -74,12 +74,19 @@ BandEngine::~BandEngine() {
 }
 
 void BandEngine::trim_graph_caches() {
-  if (graphs_.size() < kMaxCachedGraphs && step_graphs_.size() < kMaxCachedGraphs) return;
+  // Only the cache that reached its bound is emptied (the other keeps its
+  // still-valid graphs).
+  const bool g = graphs_.size() >= kMaxCachedGraphs, sg = step_graphs_.size() >= kMaxCachedGraphs;
+  if (!g && !sg) return;
   PCONV_HIP_CHECK(hipStreamSynchronize(cs_));  // no cached graph may still be running
-  for (auto& kv : graphs_) PCONV_HIP_CHECK(hipGraphExecDestroy(kv.second));
-  for (auto& kv : step_graphs_) PCONV_HIP_CHECK(hipGraphExecDestroy(kv.second.exec));
-  graphs_.clear();
-  step_graphs_.clear();
+  if (g) {
+    for (auto& kv : graphs_) PCONV_HIP_CHECK(hipGraphExecDestroy(kv.second));
+    graphs_.clear();
+  }
+  if (sg) {
+    for (auto& kv : step_graphs_) PCONV_HIP_CHECK(hipGraphExecDestroy(kv.second.exec));
+    step_graphs_.clear();
+  }
 }
 
 void BandEngine::clear() {

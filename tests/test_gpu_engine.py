@@ -261,3 +261,29 @@ def test_device_pci_id_and_numa_bind(pconv_mod):
             assert kept == len(after) and after <= (device_local_cpus(0) or set())
     finally:
         os.sched_setaffinity(0, before)
+
+
+def test_step_graph_cache_bounded_across_host_buffers(pconv_mod, rng):
+    """Whole-step graphs are keyed on the host buffers: cycling more distinct
+    pinned (in, out) pairs than the cache holds evicts and re-captures, every
+    result stays exact, and the repetition-loop graph cache is untouched."""
+    n = pconv_mod.native
+    w, h, reps = 45, 23, 9
+    eng = n.BandEngine(w, h, "rgb", "gaussian", 0, 1, 0, halo=8, fuse=8, graph=True)
+    cap = eng.max_cached_graphs
+    img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+    ref = pconv_mod.numpy_convolve(img, reps)
+    # one loop graph first (run() with graph=True), it must survive the step-graph evictions
+    eng.upload(img.reshape(-1), 0, h)
+    eng.run(reps)
+    eng.synchronize()
+    loop_graphs = eng.cached_graphs - eng.cached_step_graphs
+    assert loop_graphs == 1
+    bufs = [(n.PinnedBuffer(img.size), n.PinnedBuffer(img.size)) for _ in range(cap + 6)]
+    for k, (bi, bo) in enumerate(bufs):
+        np.asarray(bi)[:] = img.reshape(-1)
+        eng.process_graph(bi.ptr, 0, h, bo.ptr, reps)
+        eng.synchronize()
+        assert eng.cached_step_graphs <= cap
+        assert np.array_equal(np.asarray(bo).reshape(h, w, 3), ref), k
+    assert eng.cached_graphs - eng.cached_step_graphs == loop_graphs

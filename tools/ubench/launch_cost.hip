@@ -64,6 +64,35 @@ __global__ __launch_bounds__(512) void k_tile_io(const uint8_t* __restrict__ src
   }
 }
 
+// Same bytes as k_tile_io, 16 B per lane: a wave instruction covers two
+// tile rows x both strips (4 x 256 B) instead of one row of one strip.
+__global__ __launch_bounds__(512) void k_tile_io16(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst) {
+  __shared__ int lds[8192];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tile = blockIdx.x, col = tile / kRowTiles, rt = tile - col * kRowTiles;
+  const int q = lane >> 4, l16 = lane & 15;  // quarter: (row parity, strip), 16 lanes x 16 B = 256 B
+  const int strip = q & 1 ? col + kPairs : col;
+  const int x = strip * kVbytes - kHalo * 4 + l16 * 16;
+  const int r0 = rt * kVrows - 8 + w * kM;
+  uint4 v[kM / 2];
+#pragma unroll
+  for (int i = 0; i < kM / 2; ++i) {
+    const int r = r0 + 2 * i + (q >> 1);
+    const bool ok = r >= 0 && r < kRows && x >= 0 && x + 16 <= kRowBytes;
+    v[i] = ok ? *reinterpret_cast<const uint4*>(src + r * kPitch + x) : make_uint4(0, 0, 0, 0);
+  }
+  if (threadIdx.x == 0) lds[w] = static_cast<int>(v[0].x);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kM / 2; ++i) {
+    const int r = r0 + 2 * i + (q >> 1);
+    if (r < rt * kVrows || r >= (rt + 1) * kVrows || r >= kRows || x < 0 || x + 16 > kRowBytes) continue;
+    uint4 o = v[i];
+    o.x += lds[0] * 0;
+    *reinterpret_cast<uint4*>(dst + r * kPitch + x) = o;
+  }
+}
+
 int main() {
   const size_t bytes = static_cast<size_t>(kPitch) * (kRows + 16);
   uint8_t *s = nullptr, *d = nullptr;
@@ -94,8 +123,15 @@ int main() {
     CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&ms, e0, e1));
     const float io_us = ms * 1e3f / iters;
-    std::printf("{\"round\": %d, \"grid\": %u, \"block\": %u, \"empty_launch_us\": %.2f, \"tile_io_launch_us\": %.2f}\n",
-                round, grid.x, block.x, empty_us, io_us);
+    CK(hipEventRecord(e0, st));
+    for (int i = 0; i < iters; ++i) k_tile_io16<<<grid, block, 0, st>>>(i & 1 ? d + 8 * kPitch : s + 8 * kPitch,
+                                                                      i & 1 ? s + 8 * kPitch : d + 8 * kPitch);
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const float io16_us = ms * 1e3f / iters;
+    std::printf("{\"round\": %d, \"grid\": %u, \"block\": %u, \"empty_launch_us\": %.2f, \"tile_io_launch_us\": %.2f, "
+                "\"tile_io16_launch_us\": %.2f}\n", round, grid.x, block.x, empty_us, io_us, io16_us);
   }
   return 0;
 }
