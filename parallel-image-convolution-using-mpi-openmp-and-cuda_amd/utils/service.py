@@ -113,3 +113,80 @@ def start_server(socket_path: str, device: int = 0, idle_timeout: float = 0.0, m
         time.sleep(0.05)
     p.kill()
     raise ServiceError("server did not start listening")
+
+
+class ServicePool:
+    """Data-parallel serving over several resident servers (one per GPU):
+    independent images go to the servers round-robin by availability, each
+    job whole on one GPU — no halos, so N servers give N x the image
+    throughput of one (the row-band decomposition instead splits ONE image
+    over N GPUs, trading halo work for latency; docs/ARCHITECTURE.md §5).
+
+        pool = ServicePool.start(8, "/tmp/pconv")      # /tmp/pconv.0.sock ... .7.sock
+        metas = pool.map([dict(image=p, width=1920, height=2520, reps=40, channels="rgb") for p in paths])
+        pool.close()
+    """
+
+    def __init__(self, sockets: List[str], procs: Optional[List[subprocess.Popen]] = None, timeout: float = 600.0):
+        if not sockets:
+            raise ValueError("ServicePool needs at least one server socket")
+        self.clients = [ServiceClient(s, timeout) for s in sockets]
+        self.procs = list(procs or [])
+
+    @classmethod
+    def start(cls, devices, prefix: str, idle_timeout: float = 0.0) -> "ServicePool":
+        """Start one server per device (an int n means devices 0..n-1)."""
+        devs = list(range(devices)) if isinstance(devices, int) else list(devices)
+        socks = [f"{prefix}.{i}.sock" for i in range(len(devs))]
+        procs = []
+        try:
+            for d, s in zip(devs, socks):
+                procs.append(start_server(s, device=d, idle_timeout=idle_timeout))
+        except Exception:
+            for p in procs:
+                p.kill()
+            raise
+        return cls(socks, procs)
+
+    def map(self, jobs: List[Dict]) -> List[Dict]:
+        """Run every job (ServiceClient.run keyword arguments); results in job
+        order.  Each server runs one job at a time; a free server takes the
+        next job.  The first failing job's ServiceError is raised after all
+        jobs finish."""
+        import queue
+        import threading
+
+        todo: "queue.Queue" = queue.Queue()
+        for i, j in enumerate(jobs):
+            todo.put((i, j))
+        out: List[Optional[Dict]] = [None] * len(jobs)
+        errs: List[BaseException] = []
+
+        def worker(c: ServiceClient):
+            while True:
+                try:
+                    i, j = todo.get_nowait()
+                except queue.Empty:
+                    return
+                try:
+                    out[i] = c.run(**j)
+                except BaseException as e:  # reported after the pool drains
+                    errs.append(e)
+
+        ts = [threading.Thread(target=worker, args=(c,)) for c in self.clients]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise errs[0]
+        return out  # type: ignore[return-value]
+
+    def close(self) -> None:
+        for c in self.clients:
+            try:
+                c.shutdown()
+            except (OSError, ServiceError):
+                pass
+        for p in self.procs:
+            p.wait(timeout=60)

@@ -133,3 +133,26 @@ def test_python_service_client(pconv_mod, tmp_path, rng):
         ServiceClient(sock).shutdown()
         p.wait(timeout=60)
     assert p.returncode == 0 and not os.path.exists(sock)
+
+
+def test_service_pool_distributes_jobs(pconv_mod, tmp_path, rng):
+    """ServicePool over two CPU-only servers: every job exact, all jobs served."""
+    from pconv.utils.service import ServicePool
+
+    pool = ServicePool.start([-1, -1], str(tmp_path / "pool"), idle_timeout=120)
+    try:
+        jobs, imgs = [], []
+        for k in range(6):
+            img = rng.integers(0, 256, size=(21, 17, 3), dtype=np.uint8)
+            pconv_mod.write_raw(str(tmp_path / f"p{k}.raw"), img)
+            imgs.append(img)
+            jobs.append(dict(image=str(tmp_path / f"p{k}.raw"), width=17, height=21, reps=k + 1, channels="rgb",
+                             backend="omp"))
+        metas = pool.map(jobs)
+        for k, (m, img) in enumerate(zip(metas, imgs)):
+            out = pconv_mod.read_raw(m["output"], 17, 21, "rgb")
+            assert np.array_equal(out, pconv_mod.numpy_convolve(img, k + 1)), k
+        served = [c.ping()["jobs"] for c in pool.clients]
+        assert sum(served) == 6
+    finally:
+        pool.close()
