@@ -924,8 +924,9 @@ bool capturing(hipStream_t s) {
   return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
 }
 
-constexpr int kTuneCandidates = 5;
+constexpr int kTuneCandidates = 6;
 constexpr int kTuneRepeats = 3;
+constexpr int kTunePasses = 2;
 
 SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream, bool may_measure) {
   const int c = channel_count(ch);
@@ -988,20 +989,23 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   }
   SwarChoice best = cands.front();
   if (cands.size() > 1) {
+    // Two interleaved passes, each candidate's best kept: a single pass in a
+    // fixed order mis-ranked large launches (the first candidates ran while
+    // clocks and caches were still settling; 32768^2 grey picked a shape 7 %
+    // slower than the best).
     Event e0 = Event::create(true), e1 = Event::create(true);
-    float best_ms = 1e30f;
-    for (const auto& cand : cands) {
-      launch_choice(a, ch, stream, cand);  // warm (code object, caches)
-      e0.record(stream);
-      for (int r = 0; r < kTuneRepeats; ++r) launch_choice(a, ch, stream, cand);
-      e1.record(stream);
-      PCONV_HIP_CHECK(hipEventSynchronize(e1.get()));
-      const float ms = Event::elapsed_ms(e0, e1);
-      if (ms < best_ms) {
-        best_ms = ms;
-        best = cand;
+    std::vector<float> t(cands.size(), 1e30f);
+    for (int pass = 0; pass < kTunePasses; ++pass) {
+      for (size_t i = 0; i < cands.size(); ++i) {
+        if (pass == 0) launch_choice(a, ch, stream, cands[i]);  // warm (code object, caches)
+        e0.record(stream);
+        for (int r = 0; r < kTuneRepeats; ++r) launch_choice(a, ch, stream, cands[i]);
+        e1.record(stream);
+        PCONV_HIP_CHECK(hipEventSynchronize(e1.get()));
+        t[i] = std::min(t[i], Event::elapsed_ms(e0, e1));
       }
     }
+    best = cands[std::min_element(t.begin(), t.end()) - t.begin()];
   }
   std::lock_guard<std::mutex> lk(g_tune_mu);
   g_tuned.emplace(key, best);

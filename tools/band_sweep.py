@@ -66,7 +66,7 @@ def main():
                     best = min(best, (time.perf_counter() - t0) / a.iters)
                 res[sh] = best
             n.set_swar_shape(0, 0, 0)
-            tuned = [list(k) for k, _ in n.swar_tuned() if k[1] == f and k[2] == b.rows + 0]
+            tuned = [list(k) + list(sh) for k, sh in n.swar_tuned() if k[1] == f and k[2] == b.rows + 0]
             for sh, t in res.items():
                 print(json.dumps({"world": world, "band_rows": b.rows, "halo": halo, "fuse": f, "ch": a.channels,
                                   "shape": "auto" if sh is None else "%d,%d,%d" % sh,
