@@ -71,10 +71,10 @@ void prepare_stencil(const Filter& f, Channels ch, const StencilLaunch& a, hipSt
 bool supports_fusion(const Filter& f, KernelVariant v);
 
 // Default repetitions per launch for a band frame of `frame_bytes`: 1 without
-// fusion; 8 for frames the Infinity Cache holds (launch overhead dominates);
-// 6 beyond 256 MB, where the tuner's 6-level row-streaming kernel (no
-// trapezoid) beats the 8-step tile kernel (32768^2 grey: 128.8 vs 135.9
-// us/rep, profiles/r02/stream_sweep.md).
+// fusion, else 8.  Measured per frame (profiles/r02/tile_shapes.md): with the
+// taller-wave tiles 8 wins or ties everywhere — 32768^2 grey 121 us/rep at 8
+// ({4,16,8}) vs 129 at 6 (6-level streaming kernel), 1920x2520 RGB 3.5 vs
+// 4.0; 8192^2 RGB is within 2 % either way.
 int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes);
 
 // Row copy by the CUs: `rows` rows of `row_bytes` from src (row pitch sp) to

@@ -477,8 +477,8 @@ bool supports_fusion(const Filter& f, KernelVariant v) {
 }
 
 int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes) {
-  if (!supports_fusion(f, v)) return 1;
-  return frame_bytes > (int64_t(256) << 20) ? 6 : 8;
+  (void)frame_bytes;  // measured: 8 wins or ties on every BASELINE frame (profiles/r02/tile_shapes.md)
+  return supports_fusion(f, v) ? 8 : 1;
 }
 
 

@@ -531,9 +531,10 @@ int alt_mode() {
 
 // Timed by the tuner against the tile kernel (where its segments are long
 // enough).  At 8 levels it lost everywhere (~190 VGPRs, 2 waves per SIMD;
-// docs/PERFORMANCE.md); at 6 levels (~150 VGPRs) it wins on frames beyond the
-// Infinity Cache: 32768^2 grey 128.8 vs 135.9 us/rep (profiles/r02/).
-// PCONV_STREAM=0 keeps it out of the tuning, =1 forces it (tests / A-B).
+// docs/PERFORMANCE.md); at 6 levels (~150 VGPRs) it beats the 6-step tile
+// launches of frames beyond the Infinity Cache (32768^2 grey 128.8 vs 158
+// us/rep) but not the taller 8-step tiles (121).  PCONV_STREAM=0 keeps it
+// out of the tuning, =1 forces it (tests / A-B).
 std::atomic<int> g_stream_mode{-2};  // -2: PCONV_STREAM on first use; -1 tune, 0 off, 1 forced
 
 int stream_mode() {
