@@ -503,6 +503,7 @@ constexpr SwarShape kShapes[] = {
     {4, 8, 8}, {4, 6, 8}, {4, 5, 8}, {4, 4, 8}, {4, 3, 8}, {4, 4, 16},  // 4-byte lanes: small bands
     {4, 2, 16}, {4, 3, 16}, {8, 2, 16}, {8, 4, 16},                     // 16 waves: latency-bound bands
     {4, 16, 4}, {4, 12, 4}, {4, 16, 8}, {4, 12, 8},                     // tall waves: fewer halo rows per tile
+    {4, 20, 8},
 };
 
 std::atomic<int> g_xcd_swizzle{-1};  // -1: from PCONV_XCD_SWIZZLE on first use (default on)
@@ -602,6 +603,7 @@ void launch_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh, bool alt) {
   PCONV_SWAR(4, 12, 4)
   PCONV_SWAR(4, 16, 8)
   PCONV_SWAR(4, 12, 8)
+  PCONV_SWAR(4, 20, 8)
 #undef PCONV_SWAR
   PCONV_FAIL("swar temporal kernel: unsupported tile shape");
 }
@@ -775,6 +777,7 @@ KernelRes query_res(SwarShape sh, bool alt) {
   PCONV_SWAR(4, 12, 4)
   PCONV_SWAR(4, 16, 8)
   PCONV_SWAR(4, 12, 8)
+  PCONV_SWAR(4, 20, 8)
 #undef PCONV_SWAR
   KernelRes r;
   if (e == hipSuccess && at.numRegs > 0) {
