@@ -81,7 +81,11 @@ def parse():
     p.add_argument("--loop-steps", type=int, default=None, help="timed device-resident loops (default = --steps)")
     p.add_argument("--variant", default="auto")
     p.add_argument("--seed", type=int, default=1234)
-    p.add_argument("--slots", type=int, default=3, help="images in flight (H2D/compute/D2H overlap)")
+    p.add_argument("--slots", type=int, default=None,
+                   help="images in flight (default 3; 4 engines with --pipeline split)")
+    p.add_argument("--pipeline", choices=["slots", "split"], default="slots",
+                   help="slots: each image's H2D + reps + D2H is one graph on its slot's stream; split: H2D + reps "
+                        "on one of slots/2 compute streams, the D2H on a shared copy stream")
     p.add_argument("--concurrent", choices=["auto", "on", "off"], default="off",
                    help="one compute stream per image in flight (default: one shared compute stream)")
     p.add_argument("--transport", choices=["rccl", "gloo-host"], default="rccl",
@@ -236,6 +240,8 @@ def copy_floor_ms(in_bytes: int, out_bytes: int, device: int, iters: int = 8):
 
 def main():
     a = parse()
+    if a.slots is None:
+        a.slots = 4 if a.pipeline == "split" else 3
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not a.emulate:
         sys.exit(spawn_ranks(a))
     # One hardware queue per stream of the serving pipeline (H2D, D2H, comm and
@@ -280,7 +286,8 @@ def main():
                            preload_halo=a.preload_halo, slots=a.slots, variant=a.variant,
                            transport=head_transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
                            step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
-                           zero_copy_out=a.zero_copy_out == "on", graph_capture=a.graph_capture == "on")
+                           zero_copy_out=a.zero_copy_out == "on", graph_capture=a.graph_capture == "on",
+                           split_d2h=a.pipeline == "split")
     blur.load_synthetic(a.seed)
     # --emulate-rccl: hold a (1-rank) RCCL communicator through the timed
     # region, as every real N>1 rank of the exchange path does.
@@ -389,6 +396,7 @@ def main():
                 "concurrent_images": bool(blur.pipe.concurrent),
                 "slot_streams": bool(blur.pipe.graphs),
                 "step_graphs": bool(blur.pipe.step_graphs),
+                "split_d2h": bool(blur.pipe.split_d2h),
                 "zero_copy_out": bool(blur.pipe.graphs) and a.zero_copy_out == "on",
                 "halo_depth": int(blur.engine.halo),
                 "fuse": int(blur.engine.fuse),

@@ -212,8 +212,16 @@ class BandPipeline {
   // stream-ordered, no cross-stream events) — slots overlap each other; needs
   // exchange-free images.  step_graphs: each such image is one cached hipGraph
   // (one host call), otherwise its copies and launches are issued directly.
+  // split_d2h (needs slot_streams + step_graphs; `slots` engines, an even
+  // number): each image's graph holds only its H2D and repetitions, on one of
+  // slots/2 compute streams (two engines alternate on each); its D2H runs on
+  // a shared copy stream after an event.  A compute stream then uploads and
+  // computes the next image while the previous one still downloads — the
+  // per-stream serial chain is H2D + reps instead of H2D + reps + D2H, with
+  // one more busy queue (slots/2 + 1 in total).  Engine reuse waits for that
+  // engine's previous download (events), so no frame is overwritten early.
   BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt, int slots,
-               int concurrent = -1, bool slot_streams = false, bool step_graphs = true);
+               int concurrent = -1, bool slot_streams = false, bool step_graphs = true, bool split_d2h = false);
   ~BandPipeline();
   int slots() const { return static_cast<int>(slots_.size()); }
   BandEngine& slot(int i) { return *slots_.at(i); }
@@ -232,6 +240,7 @@ class BandPipeline {
   bool concurrent() const { return concurrent_; }
   bool graphs() const { return graphs_; }
   bool step_graphs() const { return graphs_ && step_graphs_; }
+  bool split_d2h() const { return split_d2h_; }
   // Stage timeline of the next `images` submits (not with captured step
   // graphs): per image {slot, H2D start, H2D end, reps end, D2H end} in ms
   // from the first image's H2D start, read after drain().  Timing events
@@ -246,6 +255,8 @@ class BandPipeline {
   bool concurrent_ = false;
   bool graphs_ = false;  // slot-stream mode
   bool step_graphs_ = true;
+  bool split_d2h_ = false;
+  std::vector<Event> ev_done_split_, ev_freed_;  // per engine: graph done / its D2H done
   std::vector<std::unique_ptr<BandEngine>> slots_;
   std::vector<Event> ev_up_, ev_done_, ev_free_, ev_halo_;
   std::vector<bool> used_;

@@ -335,7 +335,7 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     hipGraph_t g = nullptr;
     // Zero-copy output: the last launch must produce exactly the owned rows
     // with the SWAR kernel (gaussian) into a 4-byte-aligned packed row pitch.
-    const bool zc = opt_.zero_copy_out && !ph.empty() && ph.back().launches.size() == 1 &&
+    const bool zc = host_out && opt_.zero_copy_out && !ph.empty() && ph.back().launches.size() == 1 &&
                     ph.back().launches[0].lo == 0 && ph.back().launches[0].hi == band_.rows && filter_.binomial121 &&
                     (opt_.variant == KernelVariant::Auto || opt_.variant == KernelVariant::Temporal) && rb % 4 == 0 &&
                     reinterpret_cast<uintptr_t>(host_out) % 16 == 0;
@@ -346,9 +346,9 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     if (zc) {
       launch(ph.back().launches[0], cs_, host_out, rb);
       cur_ ^= 1;  // frame state as after the phase (its rows now live on the host)
-    } else {
+    } else if (host_out) {
       download_rows(host_out, rb, 0, band_.rows, cs_);
-    }
+    }  // host_out == nullptr: the caller downloads the result frame itself
     PCONV_HIP_CHECK(hipStreamEndCapture(cs_, &g));
     StepGraph sg;
     sg.zero_copy = zc;
@@ -390,9 +390,34 @@ void BandEngine::synchronize() {
 // --------------------------------------------------------------- BandPipeline
 
 BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt,
-                           int slots, int concurrent, bool graphs, bool step_graphs) {
+                           int slots, int concurrent, bool graphs, bool step_graphs, bool split_d2h) {
   PCONV_CHECK(slots >= 1 && slots <= 8, "pipeline slots must be in [1, 8]");
   set_device(opt.device);
+  if (split_d2h) {
+    PCONV_CHECK(graphs && step_graphs, "split_d2h needs whole-step graphs on slot streams");
+    PCONV_CHECK(slots >= 2 && slots % 2 == 0, "split_d2h needs an even number of engines (two per stream)");
+    graphs_ = true;
+    step_graphs_ = true;
+    split_d2h_ = true;
+    concurrent_ = true;
+    EngineOptions o = opt;
+    o.use_graph = false;
+    o.timing = false;
+    o.overlap = false;
+    for (int i = 0; i < slots / 2; ++i) computes_.push_back(Stream::create(0));
+    d2h_ = Stream::create(0);
+    for (int i = 0; i < slots; ++i) {
+      // engines 2j and 2j+1 share compute stream j: consecutive images
+      // alternate streams, and each stream alternates its two engines
+      o.compute_stream = computes_[static_cast<size_t>(i % (slots / 2))].get();
+      o.comm_stream = o.compute_stream;
+      slots_.push_back(std::make_unique<BandEngine>(geom, band, filter, o));
+      ev_done_split_.push_back(Event::create());
+      ev_freed_.push_back(Event::create());
+    }
+    used_.assign(slots, false);
+    return;
+  }
   if (graphs) {
     // One stream per slot carries that slot's whole image (H2D, reps, D2H) as
     // one graph: slots overlap each other without cross-stream events.
@@ -479,6 +504,20 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
     trace_mark(2, cs);
     e.download_rows(host_out, e.layout().row_bytes, 0, e.band().rows);
     trace_mark(3, cs);
+    used_[k] = true;
+    ++count_;
+    return;
+  }
+  if (split_d2h_) {
+    PCONV_CHECK(trace_ev_.empty(), "pipeline trace needs directly issued images (graph capture off)");
+    hipStream_t cs = e.compute_stream();
+    // This engine's frames may still be read by its previous image's D2H.
+    if (used_[k]) ev_freed_[k].wait_on(cs);
+    e.process_graph(host_in, in_r0, in_r1, nullptr, reps);  // H2D + repetitions only
+    ev_done_split_[k].record(cs);
+    ev_done_split_[k].wait_on(d2h_.get());
+    e.download_rows(host_out, e.layout().row_bytes, 0, e.band().rows, d2h_.get());
+    ev_freed_[k].record(d2h_.get());
     used_[k] = true;
     ++count_;
     return;

@@ -534,7 +534,7 @@ PYBIND11_MODULE(_pconv_native, m) {
   py::class_<BandPipeline>(m, "BandPipeline")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
-                       int concurrent, bool graphs, bool zero_copy_out, bool step_graphs) {
+                       int concurrent, bool graphs, bool zero_copy_out, bool step_graphs, bool split_d2h) {
              EngineOptions o;
              o.zero_copy_out = zero_copy_out;
              o.device = device;
@@ -544,12 +544,13 @@ PYBIND11_MODULE(_pconv_native, m) {
              o.variant = parse_variant(variant);
              const ImageGeom g = make_geom(w, h, ch);
              return std::make_unique<BandPipeline>(g, row_band(h, world, rank), make_filter(filter), o, slots,
-                                                   concurrent, graphs, step_graphs);
+                                                   concurrent, graphs, step_graphs, split_d2h);
            }),
            py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
            py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
            py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1,
-           py::arg("graphs") = false, py::arg("zero_copy_out") = false, py::arg("step_graphs") = true)
+           py::arg("graphs") = false, py::arg("zero_copy_out") = false, py::arg("step_graphs") = true,
+           py::arg("split_d2h") = false)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -577,6 +578,7 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_property_readonly("concurrent", &BandPipeline::concurrent)
       .def_property_readonly("graphs", &BandPipeline::graphs)
       .def_property_readonly("step_graphs", &BandPipeline::step_graphs)
+      .def_property_readonly("split_d2h", &BandPipeline::split_d2h)
       .def("enable_trace", &BandPipeline::enable_trace, py::arg("images"),
            "Time the stages of the next `images` submits (directly issued pipelines only)")
       .def("trace", &BandPipeline::trace, py::call_guard<py::gil_scoped_release>(),

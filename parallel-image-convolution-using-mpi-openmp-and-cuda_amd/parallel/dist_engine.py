@@ -58,7 +58,7 @@ class DistributedBlur:
                  overlap: bool = True, preload_halo: bool = False, comm=None, slots: int = 2,
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
                  step_graphs: Optional[bool] = None, zero_copy_out: bool = False, graph_capture: bool = True,
-                 slot_exchange: bool = False):
+                 slot_exchange: bool = False, split_d2h: bool = False):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -92,11 +92,17 @@ class DistributedBlur:
         self.slot_exchange = bool(slot_exchange) and self.world > 1
         if self.slot_exchange:
             graph_capture = False
-        if self.slot_exchange or (free if step_graphs is None else bool(step_graphs)):
+        # split_d2h: each image's graph = H2D + repetitions on one of slots/2
+        # compute streams (two engines alternate on each), its D2H on a shared
+        # copy stream — exchange-free images only.
+        split = bool(split_d2h) and free and not self.slot_exchange
+        if split and (slots < 2 or slots % 2):
+            raise ValueError("split_d2h needs an even number of slots (two engines per compute stream)")
+        if self.slot_exchange or split or (free if step_graphs is None else bool(step_graphs)):
             del self.pipe
             self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
                                        graphs=True, zero_copy_out=bool(zero_copy_out),
-                                       step_graphs=bool(graph_capture), **kw)
+                                       step_graphs=bool(graph_capture) or split, split_d2h=split, **kw)
         self.engine = self.pipe.slot(0)
         self.band = self.engine.band
         self.row_bytes = self.engine.row_bytes

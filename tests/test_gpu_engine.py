@@ -287,3 +287,29 @@ def test_step_graph_cache_bounded_across_host_buffers(pconv_mod, rng):
         assert eng.cached_step_graphs <= cap
         assert np.array_equal(np.asarray(bo).reshape(h, w, 3), ref), k
     assert eng.cached_graphs - eng.cached_step_graphs == loop_graphs
+
+
+@pytest.mark.parametrize("slots,reps,world,rank", [(2, 9, 1, 0), (4, 13, 1, 0), (4, 40, 8, 3), (6, 7, 3, 1)])
+def test_pipeline_split_d2h(pconv_mod, rng, slots, reps, world, rank):
+    """Split pipeline (graph = H2D + reps on slots/2 compute streams, D2H on a
+    shared copy stream).  Three rings of images over the same slot inputs with
+    no host synchronisation in between: an engine reused before its previous
+    download finished would have its result frame overwritten by the next
+    upload (the raw input would come back), so every output must equal the
+    oracle of its slot's input."""
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    w, h = 83, 120
+    blur = DistributedBlur(w, h, "rgb", "gaussian", reps, rank=rank, world=world, device=0, slots=slots,
+                           preload_halo=True, transport="none", split_d2h=True)
+    assert blur.pipe.split_d2h
+    b = blur.band
+    imgs = [rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for _ in range(slots)]
+    for k, img in enumerate(imgs):
+        blur.load_image(img, slot=k)
+    for _ in range(3 * slots):
+        blur.submit(reps)
+    blur.drain()
+    for k, img in enumerate(imgs):
+        ref = pconv_mod.numpy_convolve(img, reps).reshape(h, -1)[b.y0:b.y0 + b.rows]
+        assert np.array_equal(blur.outputs[k], ref), k
