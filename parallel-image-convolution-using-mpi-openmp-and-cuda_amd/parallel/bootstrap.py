@@ -66,11 +66,24 @@ def broadcast_bytes(data: Optional[bytes], src: int = 0, group=None) -> bytes:
     return obj[0]
 
 
+def single_node(world: int) -> bool:
+    """All `world` ranks on this host (torchrun exports LOCAL_WORLD_SIZE)."""
+    return int(os.environ.get("LOCAL_WORLD_SIZE", world)) >= world
+
+
 def make_rccl_comm(device: int, group=None):
-    """Create the native RCCL communicator for this rank (collective)."""
+    """Create the native RCCL communicator for this rank (collective).
+
+    On one node the communicator's bootstrap sockets go over loopback
+    (NCCL_SOCKET_IFNAME=lo unless the user set it): the data moves over
+    xGMI / P2P anyway, and a host whose only interfaces are loopback or
+    unreachable container bridges then cannot stall the first RCCL call.
+    librccl is loaded on that first call, so the variable is still unread."""
     n = require_native()
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if single_node(world):
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     uid = n.rccl_unique_id() if rank == 0 else None
     uid = broadcast_bytes(uid, 0, group)
     return n.RcclComm(uid, rank, world, device)
