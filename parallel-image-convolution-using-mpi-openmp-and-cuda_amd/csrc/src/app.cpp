@@ -463,6 +463,9 @@ AppReport run_multi(const CliConfig& c) {
   PCONV_CHECK(c.gpus <= kMaxRanks, "too many ranks");
   PCONV_CHECK(g.height >= c.gpus, "image has fewer rows than ranks");
   if (!c.synthetic) validate_input_file(c.image, g);
+  // One node by construction: RCCL's bootstrap sockets over loopback (the
+  // halo data itself goes over xGMI), unless the user chose an interface.
+  if (c.transport == "rccl") ::setenv("NCCL_SOCKET_IFNAME", "lo", 0);
   create_output(out_path(c), g);  // sized + truncated once, ranks pwrite their bands
   if (c.checkpoint_every > 0)
     for (int d = c.checkpoint_every; d < c.reps; d += c.checkpoint_every)
