@@ -243,11 +243,17 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   // One-shot process: CU copies skip the SDMA / blit first-use set-up; a
   // resident server has paid it once and keeps SDMA.
   o.kernel_copies = c.copies < 0 ? cache == nullptr : c.copies == 1;
+  Stream own_stream;  // declared before the engine: outlives it
   std::unique_ptr<BandEngine> own_eng;
   bool fresh = true;
   if (cache) {
     (void)cache->engine(g, f, o, c.filter, &fresh);
   } else {
+    // The process's first stream = its first hardware queue (~20 ms of
+    // runtime set-up), timed apart from the frames and the first kernel.
+    own_stream = Stream::create(0);
+    o.compute_stream = own_stream.get();
+    pc.mark("queue");
     own_eng = std::make_unique<BandEngine>(g, row_band(g.height, 1, 0), f, o);
   }
   BandEngine& eng = cache ? *cache->engines.front().second : *own_eng;

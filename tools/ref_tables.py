@@ -132,6 +132,8 @@ def cmd_cuda(a):
             for i, reps in enumerate(REPS):
                 runs = []
                 for _ in range(a.runs):
+                    if a.gap > 0:  # let the previous process's KFD teardown finish (tools/ubench/hsa_cost.cpp)
+                        time.sleep(a.gap)
                     m = run_conv([img, "1920", str(h), str(reps), ch, "--json", "--quiet",
                                   "--out", os.path.join(d, "out.raw")] + extra)
                     if srv:  # the client's clock (after its argument parsing -> answer), IPC included
@@ -139,7 +141,8 @@ def cmd_cuda(a):
                     runs.append(m)
                 runs.sort(key=lambda m: m["e2e_s"])
                 med = runs[len(runs) // 2]
-                emit(a.out, {"table": "cuda-service" if srv else "cuda", "channels": ch, "height": h, "reps": reps,
+                table = "cuda-service" if srv else ("cuda-idle" if a.gap > 0 else "cuda")
+                emit(a.out, {"table": table, "gap_s": a.gap, "channels": ch, "height": h, "reps": reps,
                              "ref_s": CUDA_REF[(ch, h)][i],
                              "e2e_s": med["e2e_s"], "e2e_all_s": [m["e2e_s"] for m in runs],
                              "loop_s": med["loop_s"], "process_wall_s": med["process_wall_s"],
@@ -249,7 +252,9 @@ def cmd_report(a):
     recs = _load(a.inputs)
     out = []
     for table, title in (("cuda", "### CUDA table semantics: `conv` end-to-end (s), cold process, one MI355X vs "
-                                   "GTX 970\n"),
+                                   "GTX 970, processes back to back\n"),
+                         ("cuda-idle", "### CUDA table semantics: `conv` end-to-end (s), one cold process on an idle GPU "
+                                       "(idle gap before each process), one MI355X vs GTX 970\n"),
                          ("cuda-service", "### CUDA table semantics through the resident service: `conv --server` "
                                           "end-to-end (s, client clock), one MI355X vs GTX 970\n")):
         _cuda_table(recs, table, title, out)
@@ -304,6 +309,9 @@ def main():
         if name == "cuda":
             s.add_argument("--service", action="store_true",
                            help="run every job through one resident `conv --serve` (warm GPU context)")
+            s.add_argument("--gap", type=float, default=0.0,
+                           help="idle seconds before each fresh process: a process started right after another "
+                                "waits 85-206 ms in open(/dev/kfd) for the previous one's driver teardown")
             s.add_argument("--extra", nargs=argparse.REMAINDER, default=[])
         if name == "mpi-cpu":
             s.add_argument("--backends", default="cpu,omp")
