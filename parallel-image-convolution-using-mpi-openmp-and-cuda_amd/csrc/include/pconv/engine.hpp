@@ -232,7 +232,8 @@ class BandPipeline {
   void set_slot_transport(int k, std::shared_ptr<HaloTransport> t);
   // Enqueue one image: host_in holds frame rows [in_r0, in_r1) (ghost rows
   // allowed), host_out receives the owned rows.  Host buffers must be pinned
-  // and must stay untouched until drain() (or until S later submits).
+  // and must stay untouched until drain(): submit() never blocks the host, so
+  // later submits say nothing about when this image's copies have run.
   void submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps);
   void drain();
   int64_t submitted() const { return count_; }
