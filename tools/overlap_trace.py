@@ -74,7 +74,7 @@ def analyse(a):
     for k in ks:
         name = k["Kernel_Name"]
         s, e, st = int(k["Start_Timestamp"]), int(k["End_Timestamp"]), k["Stream_Id"]
-        if "rccl" in name.lower() or "ncclkernel" in name.lower():
+        if any(t in name.lower() for t in ("rccl", "ncclkernel", "nccldevkernel")):
             if a.kinds == "rccl":
                 halo.append((s, e, "rccl:" + name.split("(")[0].replace("void ", "")[:30], st))
         elif "k_swar" in name or "k_binomial" in name or "k_stream" in name:
