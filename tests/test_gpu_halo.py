@@ -165,7 +165,7 @@ def test_cli_gpu1_phase_breakdown(pconv_mod, tmp_path):
     assert r.returncode == 0, r.stderr
     meta = json.loads(r.stdout.strip().splitlines()[-1])
     ph = meta["phases_s"]
-    for k in ("hip_init", "pinned_alloc", "synthesize", "device_alloc", "h2d", "loop", "d2h", "write"):
+    for k in ("hip_init", "pinned_alloc", "synthesize", "queue", "device_alloc", "h2d", "loop", "d2h", "write"):
         assert k in ph and ph[k] >= 0
     assert sum(ph.values()) <= meta["e2e_s"] + 1e-3
     assert meta["since_exec_s"] >= meta["e2e_s"] - 0.02
