@@ -87,5 +87,8 @@ void launch_copy_rows(const uint8_t* src, int64_t sp, uint8_t* dst, int64_t dp, 
                       hipStream_t stream);
 // Zero `bytes` (a multiple of 16, 16-byte aligned) with a kernel of this module.
 void launch_fill_zero(uint8_t* p, int64_t bytes, hipStream_t stream);
+// Load the code object of the temporal / copy kernels now (a one-shot process
+// calls it from a helper thread while it creates its first hardware queue).
+void preload_kernel_module();
 
 }  // namespace pconv

@@ -1089,6 +1089,13 @@ void launch_fill_zero(uint8_t* p, int64_t bytes, hipStream_t stream) {
   PCONV_HIP_CHECK(hipGetLastError());
 }
 
+void preload_kernel_module() {
+  // Any attribute query of a kernel makes the runtime load the code object of
+  // its translation unit (all of this file's kernels); no GPU work is issued.
+  hipFuncAttributes at{};
+  if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_fill_zero)) != hipSuccess) (void)hipGetLastError();
+}
+
 void prepare_swar(const StencilLaunch& a, Channels ch, hipStream_t stream) { (void)tuned_choice(a, ch, stream, true); }
 
 void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream) {

@@ -21,6 +21,7 @@
 #include "pconv/cpu_stencil.hpp"
 #include "pconv/device.hpp"
 #include "pconv/engine.hpp"
+#include "pconv/kernels.hpp"
 #include "pconv/raw_io.hpp"
 #include "pconv/rccl_comm.hpp"
 #include "pconv/service.hpp"
@@ -224,10 +225,25 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   const Filter f = Filter::by_name(c.filter);
   const int device = cache ? cache->device : 0;
   set_device(device);
+  std::thread preload;  // joined before the engine's first kernel
   if (!cache) {
     PCONV_HIP_CHECK(hipFree(nullptr));  // the runtime + device context (cudaMalloc's hidden cost in the reference)
     pc.mark("hip_init");
+    // The kernels' code object (~6 ms to load on first use) loads on a helper
+    // thread while this one allocates staging, reads the image and creates
+    // the first hardware queue (~20 ms).  PCONV_PRELOAD=0 disables (A/B).
+    const char* pe = std::getenv("PCONV_PRELOAD");
+    if (!(pe && pe[0] == '0'))
+      preload = std::thread([device] {
+        if (hipSetDevice(device) == hipSuccess) preload_kernel_module();
+      });
   }
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } join_preload{preload};
   PinnedBuffer own_host;
   uint8_t* host = nullptr;
   if (cache) {
@@ -254,6 +270,7 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
     own_stream = Stream::create(0);
     o.compute_stream = own_stream.get();
     pc.mark("queue");
+    if (preload.joinable()) preload.join();
     own_eng = std::make_unique<BandEngine>(g, row_band(g.height, 1, 0), f, o);
   }
   BandEngine& eng = cache ? *cache->engines.front().second : *own_eng;
