@@ -90,5 +90,9 @@ void launch_fill_zero(uint8_t* p, int64_t bytes, hipStream_t stream);
 // Load the code object of the temporal / copy kernels now (a one-shot process
 // calls it from a helper thread while it creates its first hardware queue).
 void preload_kernel_module();
+// Empirical tile-shape tuning on / off (off: the latency model's pick);
+// returns the previous setting.  A one-shot process turns it off: timing a
+// dozen candidates costs more than the loop they would speed up.
+bool set_shape_tuning(bool on);
 
 }  // namespace pconv

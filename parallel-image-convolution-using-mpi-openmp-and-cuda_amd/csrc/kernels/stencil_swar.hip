@@ -1019,6 +1019,11 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
 }  // namespace
 
 void set_autotune(bool on) { g_autotune.store(on ? 1 : 0, std::memory_order_relaxed); }
+bool set_shape_tuning(bool on) {
+  const bool prev = autotune_enabled();
+  set_autotune(on);
+  return prev;
+}
 
 void clear_swar_tuning() {
   std::lock_guard<std::mutex> lk(g_tune_mu);

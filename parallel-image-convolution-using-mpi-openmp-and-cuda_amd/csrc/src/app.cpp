@@ -244,6 +244,19 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
       if (t.joinable()) t.join();
     }
   } join_preload{preload};
+  // One-shot process: the model's tile shape, no timing of candidates (2-4 ms
+  // of tuning launches against a 0.03-0.7 ms loop; profiles/r02/raw/startup/
+  // cli_modes.jsonl).  PCONV_AUTOTUNE in the environment keeps its setting.
+  struct TuneScope {
+    bool active = false, prev = true;
+    ~TuneScope() {
+      if (active) (void)set_shape_tuning(prev);
+    }
+  } tune_scope;
+  if (!cache && !std::getenv("PCONV_AUTOTUNE")) {
+    tune_scope.active = true;
+    tune_scope.prev = set_shape_tuning(false);
+  }
   PinnedBuffer own_host;
   uint8_t* host = nullptr;
   if (cache) {
