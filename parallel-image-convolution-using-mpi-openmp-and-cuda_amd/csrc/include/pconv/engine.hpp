@@ -61,6 +61,13 @@ struct EngineOptions {
   // the pinned host output (zero-copy D2H fused into the producing kernel)
   // instead of a separate D2H copy — when the filter / row size allow it.
   bool zero_copy_out = false;
+  // process_graph() without zero-copy: the image's last launch stores its
+  // rows PACKED (pitch = row bytes) into a device staging buffer and the D2H
+  // is one contiguous copy.  For boxes whose pitched (2-D) D2H is slow
+  // (12-35 GB/s against 45-54 contiguous on one measured box); on a box
+  // without that problem it measured slower (N=1 0.41-0.42 vs 0.33-0.38 ms,
+  // 8-way rank 0.069 vs 0.059 ms: profiles/r02/raw/packed_d2h/), so off.
+  bool packed_out = false;
   // Host <-> frame copies (upload_rows / download_rows) and the initial frame
   // zeroing by kernels of this library instead of SDMA / the runtime's blit
   // programs: a one-shot process (the `conv` CLI) skips their first-use
@@ -188,7 +195,9 @@ class BandEngine {
     int end_cur = 0;
     int launches = 0;
     bool zero_copy = false;
+    bool packed = false;
   };
+  DeviceBuffer stage_;  // packed_out: the last launch's packed rows
   // (reps, start buffer, in, in_r0, in_r1, out) -> whole-step graph.  Keyed
   // on host pointers, so both caches are bounded: past kMaxCachedGraphs
   // entries the stream is drained and the cache is emptied.

@@ -335,23 +335,35 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     hipGraph_t g = nullptr;
     // Zero-copy output: the last launch must produce exactly the owned rows
     // with the SWAR kernel (gaussian) into a 4-byte-aligned packed row pitch.
-    const bool zc = host_out && opt_.zero_copy_out && !ph.empty() && ph.back().launches.size() == 1 &&
-                    ph.back().launches[0].lo == 0 && ph.back().launches[0].hi == band_.rows && filter_.binomial121 &&
-                    (opt_.variant == KernelVariant::Auto || opt_.variant == KernelVariant::Temporal) && rb % 4 == 0 &&
-                    reinterpret_cast<uintptr_t>(host_out) % 16 == 0;
+    // The last launch can store its rows straight to another pointer (the
+    // SWAR kernel takes a destination pitch) when it alone produces exactly
+    // the owned rows.
+    const bool last_whole = host_out && !ph.empty() && ph.back().exchange_depth == 0 &&
+                            ph.back().launches.size() == 1 && ph.back().launches[0].lo == 0 &&
+                            ph.back().launches[0].hi == band_.rows && filter_.binomial121 &&
+                            (opt_.variant == KernelVariant::Auto || opt_.variant == KernelVariant::Temporal) &&
+                            rb % 4 == 0;
+    const bool zc = last_whole && opt_.zero_copy_out && reinterpret_cast<uintptr_t>(host_out) % 16 == 0;
+    const bool packed = last_whole && !zc && opt_.packed_out;
+    if (packed && stage_.size() < static_cast<size_t>(rb * band_.rows))
+      stage_ = DeviceBuffer(static_cast<size_t>(rb * band_.rows));
     prepare(ph);  // tile-shape tuning cannot run inside the capture
     PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
     upload_rows(host_in, rb, in_r0, in_r1, cs_);
-    for (size_t i = 0; i + (zc ? 1 : 0) < ph.size(); ++i) enqueue_phase(ph[i]);
-    if (zc) {
-      launch(ph.back().launches[0], cs_, host_out, rb);
-      cur_ ^= 1;  // frame state as after the phase (its rows now live on the host)
+    for (size_t i = 0; i + (zc || packed ? 1 : 0) < ph.size(); ++i) enqueue_phase(ph[i]);
+    if (zc || packed) {
+      launch(ph.back().launches[0], cs_, zc ? host_out : stage_.data(), rb);
+      cur_ ^= 1;  // frame state as after the phase (its rows now live outside the frames)
+      if (packed)
+        PCONV_HIP_CHECK(hipMemcpyAsync(host_out, stage_.data(), static_cast<size_t>(rb * band_.rows),
+                                       hipMemcpyDeviceToHost, cs_));
     } else if (host_out) {
       download_rows(host_out, rb, 0, band_.rows, cs_);
     }  // host_out == nullptr: the caller downloads the result frame itself
     PCONV_HIP_CHECK(hipStreamEndCapture(cs_, &g));
     StepGraph sg;
     sg.zero_copy = zc;
+    sg.packed = packed;
     PCONV_HIP_CHECK(hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0));
     PCONV_HIP_CHECK(hipGraphDestroy(g));
     sg.end_cur = cur_;

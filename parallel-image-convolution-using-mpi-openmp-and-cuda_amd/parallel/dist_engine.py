@@ -58,7 +58,7 @@ class DistributedBlur:
                  overlap: bool = True, preload_halo: bool = False, comm=None, slots: int = 2,
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
                  step_graphs: Optional[bool] = None, zero_copy_out: bool = False, graph_capture: bool = True,
-                 slot_exchange: bool = False, split_d2h: bool = False):
+                 slot_exchange: bool = False, split_d2h: bool = False, packed_out: bool = False):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -101,7 +101,7 @@ class DistributedBlur:
         if self.slot_exchange or split or (free if step_graphs is None else bool(step_graphs)):
             del self.pipe
             self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
-                                       graphs=True, zero_copy_out=bool(zero_copy_out),
+                                       graphs=True, zero_copy_out=bool(zero_copy_out), packed_out=bool(packed_out),
                                        step_graphs=bool(graph_capture) or split, split_d2h=split, **kw)
         self.engine = self.pipe.slot(0)
         self.band = self.engine.band

@@ -4,8 +4,11 @@
 // build: hipcc --offload-arch=gfx950 -O3 tools/ubench/copy_bw.hip -o tools/ubench/copy_bw
 #include <hip/hip_runtime.h>
 
+#include <sys/mman.h>
+
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CHECK(x)                                                        \
@@ -35,8 +38,25 @@ int main(int argc, char** argv) {
   const size_t H = argc > 1 ? static_cast<size_t>(atol(argv[1])) : 2520;
   const size_t bytes = W * H;
   void *h_in, *h_out, *d_a, *d_b;
-  CHECK(hipHostMalloc(&h_in, bytes, 0));
-  CHECK(hipHostMalloc(&h_out, bytes, 0));
+  // argv[3] = "thp": host buffers from 2 MB-aligned anonymous memory with
+  // transparent huge pages requested, then registered (hipHostRegister) —
+  // fewer IOMMU / page-table entries per DMA than hipHostMalloc's pages.
+  const bool thp = argc > 3 && std::strcmp(argv[3], "thp") == 0;
+  if (thp) {
+    const size_t span = (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+    for (void** hp : {&h_in, &h_out}) {
+      void* m = mmap(nullptr, span + (size_t(2) << 20), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (m == MAP_FAILED) return 1;
+      void* a = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(m) + (size_t(2) << 20) - 1) & ~((uintptr_t(2) << 20) - 1));
+      (void)madvise(a, span, MADV_HUGEPAGE);
+      std::memset(a, 1, span);
+      CHECK(hipHostRegister(a, span, hipHostRegisterDefault));
+      *hp = a;
+    }
+  } else {
+    CHECK(hipHostMalloc(&h_in, bytes, 0));
+    CHECK(hipHostMalloc(&h_out, bytes, 0));
+  }
   CHECK(hipMalloc(&d_a, P * (H + 16)));
   CHECK(hipMalloc(&d_b, P * (H + 16)));
   hipStream_t s1, s2;
@@ -46,7 +66,7 @@ int main(int argc, char** argv) {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   const int iters = argc > 2 ? atoi(argv[2]) : 20;
-  printf("rows %zu, %.2f MB per copy, %d iterations\n", H, W * H / 1e6, iters);
+  printf("rows %zu, %.2f MB per copy, %d iterations, host memory: %s\n", H, W * H / 1e6, iters, thp ? "THP + hipHostRegister" : "hipHostMalloc");
   auto report = [&](const char* name, float ms, double gb) {
     printf("%-34s %8.3f ms/iter  %6.1f GB/s\n", name, ms / iters, gb * iters / (ms * 1e-3));
   };
@@ -167,6 +187,29 @@ int main(int argc, char** argv) {
     CHECK(hipEventSynchronize(e1));
     CHECK(hipEventElapsedTime(&ms, e0, e1));
     report("SDMA H2D + zero-copy D2H", ms, 2 * bytes / 1e9);
+    // the same copies as hipGraph memcpy nodes (the serving step graphs
+    // capture their H2D / D2H this way): 1-D vs 2-D (pitched) D2H node
+    for (int two_d = 0; two_d <= 1; ++two_d) {
+      hipGraph_t g;
+      hipGraphExec_t ge;
+      CHECK(hipStreamBeginCapture(s1, hipStreamCaptureModeRelaxed));
+      if (two_d)
+        CHECK(hipMemcpy2DAsync(h_out, W, (char*)d_b + 16, P, W, H, hipMemcpyDeviceToHost, s1));
+      else
+        CHECK(hipMemcpyAsync(h_out, d_b, bytes, hipMemcpyDeviceToHost, s1));
+      CHECK(hipStreamEndCapture(s1, &g));
+      CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+      CHECK(hipGraphLaunch(ge, s1));
+      CHECK(hipStreamSynchronize(s1));
+      CHECK(hipEventRecord(e0, s1));
+      for (int i = 0; i < iters; ++i) CHECK(hipGraphLaunch(ge, s1));
+      CHECK(hipEventRecord(e1, s1));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      report(two_d ? "D2H graph node, pitched (2D)" : "D2H graph node, contiguous", ms, bytes / 1e9);
+      CHECK(hipGraphExecDestroy(ge));
+      CHECK(hipGraphDestroy(g));
+    }
     // each direction split in halves on two streams (4 SDMA queues busy)
     {
       static hipStream_t s3 = nullptr, s4 = nullptr;
