@@ -73,6 +73,11 @@ struct EngineOptions {
   // programs: a one-shot process (the `conv` CLI) skips their first-use
   // set-up; the serving pipeline keeps SDMA (faster per byte, frees the CUs).
   bool kernel_copies = false;
+  // run() of a single-band gaussian frame small enough for one workgroup per
+  // CU: all repetitions in ONE register-resident launch (halo rings exchanged
+  // between workgroups every `fuse` steps; kernels/stencil_resident.hip).
+  // Needs the whole device: never with other kernels running concurrently.
+  bool resident = false;
 };
 
 struct RunStats {
@@ -198,6 +203,14 @@ class BandEngine {
     bool packed = false;
   };
   DeviceBuffer stage_;  // packed_out: the last launch's packed rows
+  // resident run(): plan (once), per-workgroup flags, epoch, error word
+  bool run_resident(int reps);
+  bool rplan_done_ = false;
+  ResidentPlan rplan_;
+  DeviceBuffer rflags_;
+  PinnedBuffer rerr_;
+  uint32_t repoch_ = 1;
+  bool resident_pending_ = false;
   // (reps, start buffer, in, in_r0, in_r1, out) -> whole-step graph.  Keyed
   // on host pointers, so both caches are bounded: past kMaxCachedGraphs
   // entries the stream is drained and the cache is emptied.

@@ -1,6 +1,8 @@
 // BandEngine / LocalCluster (see engine.hpp).
 #include "pconv/engine.hpp"
 
+#include <cstring>
+
 #include "pconv/trace.hpp"
 
 #include <algorithm>
@@ -278,6 +280,14 @@ void BandEngine::run(int reps) {
   pre_exchanges_ = 0;
   wall_t0_ = wall_seconds();
   if (opt_.timing) ev_t0_.record(cs_);
+  if (opt_.resident && run_resident(reps)) {
+    if (opt_.timing) {
+      ev_t1_.record(cs_);
+      timing_pending_ = true;
+    }
+    halo_valid_ = false;
+    return;
+  }
   bool graph = opt_.use_graph && !ph.empty();
   for (const auto& p : ph) graph = graph && p.exchange_depth == 0;
   if (graph) {
@@ -309,6 +319,44 @@ void BandEngine::run(int reps) {
     timing_pending_ = true;
   }
   halo_valid_ = false;
+}
+
+bool BandEngine::run_resident(int reps) {
+  if (reps < 1 || band_.up >= 0 || band_.down >= 0 || !filter_.binomial121 ||
+      !(opt_.variant == KernelVariant::Auto || opt_.variant == KernelVariant::Temporal))
+    return false;
+  if (!rplan_done_) {
+    rplan_ = plan_resident(geom_.channels, band_.rows, lay_.row_bytes, std::max(1, opt_.fuse));
+    rplan_done_ = true;
+    if (rplan_.ok) {
+      rflags_ = DeviceBuffer(static_cast<size_t>(round_up(rplan_.grid, 4)) * 4);
+      PCONV_HIP_CHECK(hipMemsetAsync(rflags_.data(), 0, rflags_.size(), cs_));
+      rerr_ = PinnedBuffer(64);
+      std::memset(rerr_.data(), 0, 64);
+    }
+  }
+  if (!rplan_.ok) return false;
+  const int K = std::max(1, opt_.fuse);
+  const int phases = (reps + K - 1) / K;
+  ResidentLaunch a;
+  a.f0 = frame_at(cur_);
+  a.f1 = frame_at(cur_ ^ 1);
+  a.pitch = lay_.pitch;
+  a.row_bytes = lay_.row_bytes;
+  a.height = band_.rows;
+  a.reps = reps;
+  a.K = K;
+  a.flags = reinterpret_cast<uint32_t*>(rflags_.data());
+  a.epoch = repoch_;
+  a.err = reinterpret_cast<uint32_t*>(rerr_.data());
+  const char* fa = std::getenv("PCONV_RESIDENT_ACQUIRE");  // A/B: keep the acquire at one workgroup per CU
+  a.force_acquire = fa && fa[0] == '1';
+  repoch_ += static_cast<uint32_t>(phases) + 1;
+  launch_resident(a, geom_.channels, rplan_, cs_);
+  ++stats_.launches;
+  if (phases & 1) cur_ ^= 1;
+  resident_pending_ = true;
+  return true;
 }
 
 bool BandEngine::exchange_free(int reps, bool halo_preloaded) const {
@@ -392,6 +440,15 @@ void BandEngine::exec_compute(const Phase& p) {
 void BandEngine::synchronize() {
   PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
   if (ms_ != cs_) PCONV_HIP_CHECK(hipStreamSynchronize(ms_));
+  if (resident_pending_) {
+    resident_pending_ = false;
+    volatile uint32_t* e = reinterpret_cast<volatile uint32_t*>(rerr_.data());
+    if (*e != 0) {
+      *e = 0;
+      PCONV_FAIL("resident kernel: a workgroup timed out waiting for its neighbours (grid not co-resident: "
+                 "another kernel on the device?); the frames hold garbage");
+    }
+  }
   if (timing_pending_) {
     stats_.loop_ms = Event::elapsed_ms(ev_t0_, ev_t1_);
     stats_.wall_ms = (wall_seconds() - wall_t0_) * 1e3;

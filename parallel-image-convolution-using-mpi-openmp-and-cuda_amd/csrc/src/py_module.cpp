@@ -396,9 +396,10 @@ PYBIND11_MODULE(_pconv_native, m) {
   py::class_<BandEngine>(m, "BandEngine")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, bool graph, const std::string& variant,
-                       bool kernel_copies) {
+                       bool kernel_copies, bool resident) {
              EngineOptions o;
              o.kernel_copies = kernel_copies;
+             o.resident = resident;
              o.device = device;
              o.halo_depth = halo;
              o.fuse = fuse;
@@ -411,7 +412,7 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
            py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
            py::arg("overlap") = true, py::arg("graph") = false, py::arg("variant") = "auto",
-           py::arg("kernel_copies") = false)
+           py::arg("kernel_copies") = false, py::arg("resident") = false)
       .def_property_readonly("band", &BandEngine::band)
       .def_property_readonly("halo", [](const BandEngine& e) { return e.layout().halo; })
       .def_property_readonly("fuse", [](const BandEngine& e) { return e.options().fuse; })
