@@ -351,6 +351,7 @@ bool BandEngine::run_resident(int reps) {
   a.err = reinterpret_cast<uint32_t*>(rerr_.data());
   const char* fa = std::getenv("PCONV_RESIDENT_ACQUIRE");  // A/B: keep the acquire at one workgroup per CU
   a.force_acquire = fa && fa[0] == '1';
+  if (const char* ts = std::getenv("PCONV_RESIDENT_TIMEOUT_S")) a.timeout_s = std::atof(ts);  // tests: abort path
   repoch_ += static_cast<uint32_t>(phases) + 1;
   launch_resident(a, geom_.channels, rplan_, cs_);
   ++stats_.launches;

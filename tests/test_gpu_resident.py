@@ -75,3 +75,22 @@ def test_resident_matches_tile_kernel_bytes(pconv_mod):
              img, w, h, reps)
     b = _run(n, n.BandEngine(w, h, ch, "gaussian", 0, 1, 0, halo=8, fuse=8, variant="temporal"), img, w, h, reps)
     assert np.array_equal(a, b)
+
+
+def test_resident_wait_timeout_aborts_cleanly(pconv_mod, monkeypatch):
+    """A wait that times out sets the error word, every workgroup exits (no
+    hang) and synchronize() raises; the next launch on the same engine (new
+    flag epoch) is exact again."""
+    n = pconv_mod.native
+    w, h, ch, reps = 1920, 2520, "rgb", 40
+    img = pconv_mod.synthetic_image(w, h, ch, seed=4)
+    ref = _oracle(n, img, w, h, ch, reps)
+    e = n.BandEngine(w, h, ch, "gaussian", 0, 1, 0, halo=8, fuse=8, variant="temporal", resident=True)
+    e.upload(img.reshape(-1), 0, h)
+    e.synchronize()
+    monkeypatch.setenv("PCONV_RESIDENT_TIMEOUT_S", "1e-8")  # one clock tick: a wait that is not met at once
+    e.run(reps)
+    with pytest.raises(RuntimeError, match="timed out"):
+        e.synchronize()
+    monkeypatch.delenv("PCONV_RESIDENT_TIMEOUT_S")
+    assert np.array_equal(_run(n, e, img, w, h, reps), ref)
