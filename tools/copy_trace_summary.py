@@ -37,6 +37,9 @@ def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("trace_dir")
     ap.add_argument("--images", type=int, default=20)
+    ap.add_argument("--skip-images", type=int, default=None,
+                    help="images to skip on the slot streams (bench.py: its --warmup count, so that the window is "
+                         "exactly the timed images); default: take the last --images images of the trace")
     ap.add_argument("--bytes", type=int, default=1920 * 2520 * 3)
     ap.add_argument("--md", default=None)
     a = ap.parse_args()
@@ -51,12 +54,19 @@ def main():
         if t == "c":
             copies.append((s, e, "D2H" if last.get(st) == "k" else "H2D", st, lab))
         last[st] = t
-    copies = copies[-2 * a.images:]
+    # only the copies of streams that also ran stencil launches (the pipeline's
+    # slot streams; bench.py's copy-floor probe runs on another stream)
+    slot_streams = {st for _, _, t, st, _ in ev if t == "k"}
+    copies = [c for c in copies if c[3] in slot_streams]
+    if a.skip_images is not None:
+        copies = copies[2 * a.skip_images:2 * (a.skip_images + a.images)]
+    else:
+        copies = copies[-2 * a.images:]
     t0, t1 = min(c[0] for c in copies), max(c[1] for c in copies)
     win = (t1 - t0) / 1e3
     out = [f"# Copy trace of the serving pipeline: {a.trace_dir}", "",
            f"Labels in the trace: {sorted({c[4] for c in copies})} (direction recovered from stream order).", "",
-           f"Window of the last {a.images} images: {win:.0f} us = {win / a.images / 1e3:.3f} ms per image.", "",
+           f"Window of {a.images} images{' after ' + str(a.skip_images) + ' skipped' if a.skip_images is not None else ' (the last)'}: {win:.0f} us = {win / a.images / 1e3:.3f} ms per image.", "",
            "| direction | copies | busy % of window | mean us | min us | max us | mean GB/s | same-direction overlaps |",
            "|---|---|---|---|---|---|---|---|"]
     for d in ("H2D", "D2H"):
