@@ -112,7 +112,16 @@ int serve_main(const ServeOptions& o) {
   Fd ls(::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0));
   PCONV_CHECK(ls.fd >= 0, std::string("service: socket: ") + std::strerror(errno));
   const sockaddr_un addr = address(o.socket_path);
-  ::unlink(o.socket_path.c_str());  // a stale socket of a dead server
+  // A leftover socket of a dead server is replaced; anything else at that
+  // path (a regular file, a live server) is refused, never deleted.
+  struct stat st{};
+  if (::lstat(o.socket_path.c_str(), &st) == 0) {
+    PCONV_CHECK(S_ISSOCK(st.st_mode), "service: " + o.socket_path + " exists and is not a socket");
+    Fd probe(::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0));
+    PCONV_CHECK(probe.fd >= 0 && ::connect(probe.fd, reinterpret_cast<const sockaddr*>(&addr), sizeof(addr)) != 0,
+                "service: a server is already listening on " + o.socket_path);
+    ::unlink(o.socket_path.c_str());
+  }
   const mode_t old = ::umask(077);  // owner-only socket
   const int br = ::bind(ls.fd, reinterpret_cast<const sockaddr*>(&addr), sizeof(addr));
   ::umask(old);
@@ -172,7 +181,7 @@ int serve_main(const ServeOptions& o) {
     }
     last = wall_seconds();
   }
-  ::unlink(o.socket_path.c_str());
+  if (::lstat(o.socket_path.c_str(), &st) == 0 && S_ISSOCK(st.st_mode)) ::unlink(o.socket_path.c_str());
   return 0;
 }
 

@@ -95,9 +95,9 @@ def _recv_exact(s: socket.socket, n: int) -> bytes:
 def start_server(socket_path: str, device: int = 0, idle_timeout: float = 0.0, max_engines: int = 8,
                  wait_s: float = 120.0) -> subprocess.Popen:
     """Start `conv --serve` as a child process and wait until it listens
-    (device -1: a CPU-only server for the cpu / omp backends)."""
-    if os.path.exists(socket_path):
-        os.unlink(socket_path)
+    (device -1: a CPU-only server for the cpu / omp backends).  The server
+    replaces a leftover socket of a dead server and refuses any other file
+    or a live server at that path."""
     p = subprocess.Popen([conv_binary(), "--serve", socket_path, "--device", str(device), "--idle-timeout",
                           str(idle_timeout), "--max-engines", str(max_engines)], stderr=subprocess.PIPE, text=True)
     t0 = time.time()

@@ -156,3 +156,34 @@ def test_service_pool_distributes_jobs(pconv_mod, tmp_path, rng):
         assert sum(served) == 6
     finally:
         pool.close()
+
+
+def test_serve_socket_path_safety(server, tmp_path):
+    """`conv --serve PATH` never deletes a non-socket file at PATH, refuses a
+    path a live server listens on, and replaces a dead server's socket."""
+    regular = tmp_path / "not_a_socket"
+    regular.write_text("keep me")
+    r = subprocess.run([CONV_BIN, "--serve", str(regular), "--device", "-1"], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode != 0 and "not a socket" in r.stderr
+    assert regular.read_text() == "keep me"
+    r = subprocess.run([CONV_BIN, "--serve", server, "--device", "-1"], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "already listening" in r.stderr
+    assert _request(server, "__ping__")["ok"]  # the live server is untouched
+    stale = str(tmp_path / "stale.sock")
+    s = socket.socket(socket.AF_UNIX)
+    s.bind(stale)
+    s.close()  # a socket file nobody listens on
+    p = subprocess.Popen([CONV_BIN, "--serve", stale, "--device", "-1", "--idle-timeout", "60"],
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        for _ in range(600):
+            try:
+                if _request(stale, "__ping__")["ok"]:
+                    break
+            except OSError:
+                time.sleep(0.05)
+        assert _request(stale, "__shutdown__")["ok"]
+    finally:
+        p.wait(timeout=60)
+    assert not os.path.exists(stale)
