@@ -34,14 +34,16 @@ __global__ void k_copy_rows(const uint8_t* __restrict__ src, size_t sp, uint8_t*
 int main(int argc, char** argv) {
   // 1920x2520 RGB row bytes, frame pitch; optional argv[1] = rows (e.g. 395:
   // one rank's band + ghost rows of the 8-way split), argv[2] = iterations.
-  const size_t W = 5760, P = 5888;
+  // argv[4] / argv[5]: row bytes / frame pitch (default: the RGB headline frame)
+  const size_t W = argc > 4 ? static_cast<size_t>(atol(argv[4])) : 5760;
+  const size_t P = argc > 5 ? static_cast<size_t>(atol(argv[5])) : 5888;
   const size_t H = argc > 1 ? static_cast<size_t>(atol(argv[1])) : 2520;
   const size_t bytes = W * H;
   void *h_in, *h_out, *d_a, *d_b;
   // argv[3] = "thp": host buffers from 2 MB-aligned anonymous memory with
   // transparent huge pages requested, then registered (hipHostRegister) —
   // fewer IOMMU / page-table entries per DMA than hipHostMalloc's pages.
-  const bool thp = argc > 3 && std::strcmp(argv[3], "thp") == 0;
+  const bool thp = argc > 3 && std::strcmp(argv[3], "thp") == 0;  // any other word: hipHostMalloc
   if (thp) {
     const size_t span = (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
     for (void** hp : {&h_in, &h_out}) {
