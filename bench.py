@@ -101,6 +101,8 @@ def parse():
                    help="step graphs: the last fused launch stores packed rows into a device staging buffer and the "
                         "D2H is one contiguous copy (default off: a pitched 2-D copy from the frame; packed measured "
                         "slower on a box whose 2-D D2H runs at full rate, profiles/r02/raw/packed_d2h/)")
+    p.add_argument("--d2h", choices=["sdma", "kernel"], default="sdma",
+                   help="step graphs: the D2H by SDMA (pitched copy) or by a CU copy kernel")
     p.add_argument("--emulate", default=None, metavar="WORLD:RANK",
                    help="time ONE rank of a WORLD-way split on this GPU (pre-loaded halos, no peers): a "
                         "single-GPU proxy of the per-rank step; reported as emulated, never as the headline")
@@ -291,7 +293,8 @@ def main():
                            transport=head_transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
                            step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
                            zero_copy_out=a.zero_copy_out == "on", graph_capture=a.graph_capture == "on",
-                           split_d2h=a.pipeline == "split", packed_out=a.packed_d2h == "on")
+                           split_d2h=a.pipeline == "split", packed_out=a.packed_d2h == "on",
+                           kernel_d2h=a.d2h == "kernel")
     blur.load_synthetic(a.seed)
     # --emulate-rccl: hold a (1-rank) RCCL communicator through the timed
     # region, as every real N>1 rank of the exchange path does.
@@ -403,6 +406,7 @@ def main():
                 "split_d2h": bool(blur.pipe.split_d2h),
                 "zero_copy_out": bool(blur.pipe.graphs) and a.zero_copy_out == "on",
                 "packed_d2h": bool(blur.pipe.step_graphs) and a.packed_d2h == "on" and a.zero_copy_out != "on",
+                "d2h": a.d2h,
                 "halo_depth": int(blur.engine.halo),
                 "fuse": int(blur.engine.fuse),
                 "preload_halo": bool(blur.preload_halo),

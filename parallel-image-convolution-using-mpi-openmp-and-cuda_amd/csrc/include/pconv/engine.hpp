@@ -73,6 +73,10 @@ struct EngineOptions {
   // programs: a one-shot process (the `conv` CLI) skips their first-use
   // set-up; the serving pipeline keeps SDMA (faster per byte, frees the CUs).
   bool kernel_copies = false;
+  // D2H only by a CU copy kernel (H2D stays on SDMA): an SDMA H2D beside a
+  // kernel D2H keeps both directions at full rate even on boxes whose pitched
+  // SDMA D2H is slow (tools/ubench/copy_bw.hip "SDMA H2D + zero-copy D2H").
+  bool kernel_d2h = false;
   // run() of a single-band gaussian frame small enough for one workgroup per
   // CU: all repetitions in ONE register-resident launch (halo rings exchanged
   // between workgroups every `fuse` steps; kernels/stencil_resident.hip).

@@ -128,7 +128,7 @@ void BandEngine::download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begi
                                hipStream_t stream) {
   PCONV_CHECK(r_begin >= 0 && r_end <= lay_.rows && r_begin <= r_end, "download_rows: rows outside band");
   if (r_end == r_begin) return;
-  if (opt_.kernel_copies) {
+  if (opt_.kernel_copies || opt_.kernel_d2h) {
     launch_copy_rows(src_frame() + r_begin * lay_.pitch, lay_.pitch, host, host_pitch, lay_.row_bytes, r_end - r_begin,
                      stream ? stream : cs_);
     return;

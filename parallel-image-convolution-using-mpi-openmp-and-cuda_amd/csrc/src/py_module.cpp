@@ -536,10 +536,11 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
                        int concurrent, bool graphs, bool zero_copy_out, bool step_graphs, bool split_d2h,
-                       bool packed_out) {
+                       bool packed_out, bool kernel_d2h) {
              EngineOptions o;
              o.zero_copy_out = zero_copy_out;
              o.packed_out = packed_out;
+             o.kernel_d2h = kernel_d2h;
              o.device = device;
              o.halo_depth = halo;
              o.fuse = fuse;
@@ -553,7 +554,7 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
            py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1,
            py::arg("graphs") = false, py::arg("zero_copy_out") = false, py::arg("step_graphs") = true,
-           py::arg("split_d2h") = false, py::arg("packed_out") = false)
+           py::arg("split_d2h") = false, py::arg("packed_out") = false, py::arg("kernel_d2h") = false)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",

@@ -58,7 +58,8 @@ class DistributedBlur:
                  overlap: bool = True, preload_halo: bool = False, comm=None, slots: int = 2,
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
                  step_graphs: Optional[bool] = None, zero_copy_out: bool = False, graph_capture: bool = True,
-                 slot_exchange: bool = False, split_d2h: bool = False, packed_out: bool = False):
+                 slot_exchange: bool = False, split_d2h: bool = False, packed_out: bool = False,
+                 kernel_d2h: bool = False):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -102,6 +103,7 @@ class DistributedBlur:
             del self.pipe
             self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
                                        graphs=True, zero_copy_out=bool(zero_copy_out), packed_out=bool(packed_out),
+                                       kernel_d2h=bool(kernel_d2h),
                                        step_graphs=bool(graph_capture) or split, split_d2h=split, **kw)
         self.engine = self.pipe.slot(0)
         self.band = self.engine.band
