@@ -171,18 +171,20 @@ def test_pipeline_step_graphs_preloaded_band(pconv_mod, rng):
 
 @pytest.mark.parametrize("w,h,ch,reps,fuse", [(67, 45, "rgb", 9, 8), (64, 33, "grey", 13, 8), (40, 50, "rgba", 8, 4),
                                               (61, 20, "rgb", 3, 8), (1920, 64, "rgb", 40, 8)])
-@pytest.mark.parametrize("mode", ["zero_copy", "packed"])
+@pytest.mark.parametrize("mode", ["zero_copy", "packed", "kernel_d2h"])
 def test_pipeline_zero_copy_out(pconv_mod, rng, w, h, ch, reps, fuse, mode):
     """The last fused launch writes packed rows straight into pinned host
     memory (zero_copy) or into a device staging buffer followed by one
-    contiguous D2H (packed): every byte rewritten (pre-filled with 0xAB) and
+    contiguous D2H (packed), or a CU copy kernel does the D2H (kernel_d2h):
+    every byte rewritten (pre-filled with 0xAB) and
     exact — a partial last chunk spilling into the next packed row would show
     as a mismatch."""
     from pconv.parallel.dist_engine import DistributedBlur
 
     c = {"grey": 1, "rgb": 3, "rgba": 4}[ch]
     blur = DistributedBlur(w, h, ch, "gaussian", reps, rank=0, world=1, device=0, fuse=fuse, slots=2,
-                           step_graphs=True, zero_copy_out=mode == "zero_copy", packed_out=mode == "packed")
+                           step_graphs=True, zero_copy_out=mode == "zero_copy", packed_out=mode == "packed",
+                           kernel_d2h=mode == "kernel_d2h")
     for rnd in range(2):
         img = rng.integers(0, 256, size=(h, w, c), dtype=np.uint8)
         blur.load_image(img)
