@@ -121,6 +121,7 @@ class DistributedBlur:
         self.outputs = [np.asarray(x).reshape(b.rows, self.row_bytes) for x in self._out]
         self.input, self.output = self.inputs[0], self.outputs[0]
         self._next = 0
+        self._pending = False  # submitted images not yet drained
         self.comm = None
         self.transport = None
         self.slot_comms = []
@@ -158,13 +159,21 @@ class DistributedBlur:
         """Global rows [first, last) held by the pinned input buffers."""
         return self.band.y0 - self.above, self.band.y0 + self.band.rows + self.below
 
+    def _quiesce(self) -> None:
+        # Images in flight read the pinned inputs asynchronously: never
+        # rewrite an input buffer under them.
+        if self._pending:
+            self.drain()
+
     def load_image(self, image: np.ndarray, slot: Optional[int] = None) -> None:
+        self._quiesce()
         a, b = self.input_rows
         rows = np.ascontiguousarray(image, dtype=np.uint8).reshape(self.height, self.row_bytes)[a:b]
         for i in ([slot] if slot is not None else range(self.slots)):
             self.inputs[i][:] = rows
 
     def load_file(self, path: str) -> None:
+        self._quiesce()
         a, b = self.input_rows
         require_native().read_raw_rows(path, self.inputs[0].reshape(-1), self.width, self.height, self.channels, a,
                                        b - a)
@@ -172,6 +181,7 @@ class DistributedBlur:
             self.inputs[i][:] = self.inputs[0]
 
     def load_synthetic(self, seed: int = 0) -> None:
+        self._quiesce()
         a, b = self.input_rows
         require_native().synth_rows(self.inputs[0].reshape(-1), self.width, self.height, self.channels, int(seed),
                                     a, b - a)
@@ -185,6 +195,7 @@ class DistributedBlur:
         k = self._next
         self.pipe.submit(self._in[k].ptr, -self.above, self.band.rows + self.below, self._out[k].ptr, int(reps))
         self._next = (k + 1) % self.slots
+        self._pending = True
         return k
 
     def drain(self, timeout_s: Optional[float] = None) -> None:
@@ -195,6 +206,7 @@ class DistributedBlur:
             for k, c in enumerate(self.slot_comms):
                 c.wait(self.pipe.slot(k).compute_stream, float(timeout_s))
         self.pipe.drain()
+        self._pending = False
 
     def step(self, reps: int) -> np.ndarray:
         """Synchronous: one image through H2D + reps + D2H; returns its rows."""
