@@ -26,8 +26,11 @@ constexpr int ITERS = 4096;
 template <int OP>
 __global__ __launch_bounds__(256) void k(u32* out, u32 seed, u32 two_bits) {
   u32 a[8];
+  uint64_t b[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) a[i] = seed * (threadIdx.x + 7 * i + 1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b[i] = (uint64_t(a[i]) << 32) | a[(i + 1) & 7];
   const u16x2 two = __builtin_bit_cast(u16x2, two_bits);
   for (int it = 0; it < ITERS; ++it) {
 #pragma unroll
@@ -52,12 +55,20 @@ __global__ __launch_bounds__(256) void k(u32* out, u32 seed, u32 two_bits) {
         a[i] = __builtin_amdgcn_ds_swizzle(a[i], 0x041F) + 1;
       } else if constexpr (OP == 9) {  // v_permlane32_swap-free alternative: __shfl_up via ds_bpermute
         a[i] = __shfl_up(a[i], 1) + 1;
+      } else if constexpr (OP == 10) {  // v_lshl_add_u64 (shift 0): 64-bit add, four 16-bit SWAR fields
+        b[i] = b[i] + b[(i + 1) & 7];
+      } else if constexpr (OP == 11) {  // v_lshl_add_u64 (shift 1): b + 2c
+        b[i] = (b[(i + 3) & 7] << 1) + b[i];
+      } else if constexpr (OP == 12) {  // v_lshrrev_b64
+        b[i] = (b[i] >> 4) ^ b[(i + 2) & 7];
+      } else if constexpr (OP == 13) {  // v_add3_u32
+        a[i] = a[i] + a[(i + 1) & 7] + a[(i + 5) & 7];
       }
     }
   }
   u32 s = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s ^= a[i];
+  for (int i = 0; i < 8; ++i) s ^= a[i] ^ u32(b[i]) ^ u32(b[i] >> 32);
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
@@ -100,6 +111,10 @@ int main() {
     run<5>("dpp row_shr:1 (+add)", b);
     run<8>("ds_swizzle (+add)", b);
     run<9>("shfl_up/bpermute(+add)", b);
+    run<10>("v_lshl_add_u64 (add)", b);
+    run<11>("v_lshl_add_u64 (<<1)", b);
+    run<12>("v_lshrrev_b64 (+xor)", b);
+    run<13>("v_add3_u32", b);
   }
   return 0;
 }
