@@ -8,7 +8,9 @@
 // Why SWAR-32: measured on gfx950 (tools/ubench/isa_rates.hip), packed
 // 16-bit VOP3P ops (v_pk_add_u16, v_pk_mad_u16, v_pk_lshrrev_b16) and
 // v_perm_b32 issue at HALF the rate of plain 32-bit VALU ops, while
-// v_add_u32 / v_add3_u32 / v_lshlrev_b32 / v_and_b32 run at full rate.  Two
+// v_add_u32 / v_lshlrev_b32 / v_and_b32 run at full rate (v_add3_u32 at half
+// rate: one v_add3 costs what two v_add_u32 do; 64-bit adds and shifts at half
+// to a third, profiles/r02/raw/isa/isa_rates_u64.txt).  Two
 // 16-bit fields in a u32 never carry into each other here (every sum stays
 // below 4080 < 2^16), so plain 32-bit adds do the packed work at twice the
 // throughput.
@@ -146,6 +148,139 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
           store_bytes<NP>(rowq + xB, b, validB);
       }
     }
+  }
+}
+
+// Buffer-op form of k_swar (4-byte lanes), optionally persistent.
+//   Every row load and store is a raw buffer op; rows and lanes outside the
+// frame get an offset past the descriptor's range, so the hardware returns
+// zeros / drops the store instead of the branches k_swar takes around each
+// chunk, and every wave issues exactly 2M loads and 2M stores per tile.  One
+// workgroup per tile is the form the tuner times against k_swar (2-6 %
+// faster on RGB frames, e.g. the headline 3.45 -> 3.26 us/rep; slower on
+// grey ones, where its ALT form needs far more VGPRs:
+// profiles/r02/prefetch_kernel.md).
+//   Persistent form (opt-in, set_prefetch_mode(mode, cap != 0)): a resident
+// grid in which each workgroup walks a run of tiles and issues the NEXT
+// tile's row loads before the current tile's steps (the steps' barriers wait
+// on LDS only, s_waitcnt lgkmcnt), the loop rotated so the next tile is
+// unpacked right after this tile's stores (the compiler's wait there is
+// vmcnt(2M): the loads, not the stores still draining; gfx950 counts both in
+// vmcnt, in issue order).  Tiles are dealt to the 8 XCDs in contiguous runs
+// (workgroup b runs on XCD b % 8).  Measured 10-40 % SLOWER than relaunching
+// k_swar on 32768^2 grey (one workgroup per CU at the prefetch's VGPR cost
+// leaves the per-step barrier bubbles unhidden), so the tuner never picks it.
+//   Contract (checked at launch): row_bytes % 4 == 0, source and destination
+// ranges under 2 GiB.
+template <int CH, int M, int NW, bool ALT>
+__global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                     int pitch, int dst_pitch, int row_bytes, int r0, int r1,
+                                                     int steps, int g_row0, int height, int nstrips, int pair_stride,
+                                                     int row_tiles) {
+  constexpr int LW = 4, NP = 4, NQ = 1;
+  constexpr u32 kOut = 0x80000000u;  // offset past every descriptor's range
+  __shared__ uint4 lds[2][NW][2][NQ][64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hl = (steps * CH + LW - 1) / LW;
+  const int vbytes = (64 - 2 * hl) * LW;
+  const int vrows = NW * M - 2 * steps;
+  // Source rows [lo_ok, hi_ok) are readable; destination rows [r0, st_end).
+  const int lo_ok = max(r0 - steps, -g_row0), hi_ok = min(r1 + steps, height - g_row0);
+  const int st_end = min(r1, height - g_row0);
+  const auto srsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(src) + static_cast<int64_t>(lo_ok) * pitch, 0, max(hi_ok - lo_ok, 0) * pitch, 0x00020000);
+  const auto drsrc = __builtin_amdgcn_make_buffer_rsrc(dst + static_cast<int64_t>(r0) * dst_pitch, 0,
+                                                       max(st_end - r0, 0) * dst_pitch, 0x00020000);
+
+  const int ntiles = pair_stride * row_tiles;
+  const int nwg = static_cast<int>(gridDim.x), b = static_cast<int>(blockIdx.x);
+  // With fewer than 8 workgroups only XCDs 0..nwg-1 hold one: the tiles are
+  // split over those.
+  const int nx = min(nwg, 8);
+  const int xcd = b & 7, local = b >> 3;
+  const int t_step = (nwg - xcd + 7) >> 3;  // workgroups on this XCD
+  const int t_end = static_cast<int>((int64_t(xcd) + 1) * ntiles / nx);
+  int tile = static_cast<int>(int64_t(xcd) * ntiles / nx) + local;
+  if (tile >= t_end) return;  // whole workgroup (uniform)
+
+  // Per tile: lane byte offsets of strips A / B (or kOut), first frame row of
+  // this wave, and whether edge columns need masking.
+  int xA, xB, row_base;
+  bool needs_mask;
+  auto geo = [&](int t, int& ga, int& gb, int& grow, bool& gmask) {
+    const int col = t / row_tiles, rtile = t - col * row_tiles;
+    const int sB = col + pair_stride;
+    const int baseA = col * vbytes - hl * LW, baseB = sB * vbytes - hl * LW;
+    const int pa = baseA + lane * LW, pb = baseB + lane * LW;
+    ga = (pa >= 0 && pa < row_bytes) ? pa : -1;
+    gb = (sB < nstrips && pb >= 0 && pb < row_bytes) ? pb : -1;
+    gmask = baseA < 0 || baseA + 64 * LW > row_bytes || sB >= nstrips || baseB + 64 * LW > row_bytes;
+    grow = r0 + rtile * vrows - steps + w * M;
+  };
+  u32 pa[M], pb[M];
+  auto fetch = [&](int ga, int gb, int grow) {
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const int fr = grow + i;
+      const bool rok = fr >= lo_ok && fr < hi_ok;
+      const u32 ro = static_cast<u32>(fr - lo_ok) * static_cast<u32>(pitch);
+      pa[i] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, (rok && ga >= 0) ? ro + ga : kOut, 0, 0);
+      pb[i] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, (rok && gb >= 0) ? ro + gb : kOut, 0, 0);
+    }
+  };
+  geo(tile, xA, xB, row_base, needs_mask);
+  fetch(xA, xB, row_base);
+  u32 D[M][NP];
+#pragma unroll
+  for (int i = 0; i < M; ++i) unpack<NP>(pa[i], pb[i], D[i]);
+  while (true) {
+    const int next = tile + t_step;
+    const bool more = next < t_end;
+    int nA, nB, nrow;
+    bool nmask;
+    geo(more ? next : tile, nA, nB, nrow, nmask);
+    fetch(more ? nA : -1, more ? nB : -1, nrow);  // in flight during this tile's steps (all-zero past the end)
+    u32 cm[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+      cm[k] = (xA >= 0 && xA + k < row_bytes ? 0xffffu : 0u) | (xB >= 0 && xB + k < row_bytes ? 0xffff0000u : 0u);
+    const int out_top = min(max(-g_row0 - row_base, 0), M);
+    const int out_bot = min(max(height - g_row0 - row_base, 0), M);
+    if constexpr (ALT) {
+      int s = 0;
+      for (; s + 2 <= steps; s += 2) {
+        swar_step<CH, NP, M, NW, 1>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+        swar_step<CH, NP, M, NW, 2>(D, lds, 1, w, lane, needs_mask, cm, out_top, out_bot);
+      }
+      if (s < steps) swar_step<CH, NP, M, NW, 0>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+    } else {
+      for (int s = 0; s < steps; ++s) swar_step<CH, NP, M, NW, 0>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
+    }
+    const bool lane_in = lane >= hl && lane < 64 - hl;
+    const int tile_r0 = row_base + steps - w * M;
+    const int st_lo = max(tile_r0, r0), st_hi = min(tile_r0 + vrows, st_end);
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const int fr = row_base + i;
+      const bool rst = fr >= st_lo && fr < st_hi;
+      const u32 ro = static_cast<u32>(fr - r0) * static_cast<u32>(dst_pitch);
+      u32 a, bb;
+      pack<NP>(D[i], a, bb);
+      __builtin_amdgcn_raw_buffer_store_b32(a, drsrc, (rst && lane_in && xA >= 0) ? ro + xA : kOut, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(bb, drsrc, (rst && lane_in && xB >= 0) ? ro + xB : kOut, 0, 0);
+    }
+    if (!more) break;
+    tile = next;
+    xA = nA;
+    xB = nB;
+    row_base = nrow;
+    needs_mask = nmask;
+#pragma unroll
+    for (int i = 0; i < M; ++i) unpack<NP>(pa[i], pb[i], D[i]);
+    // The next tile's first step overwrites LDS parity 0, which the slowest
+    // wave of this tile may still be reading (its last step's boundary rows).
+    __syncthreads();
   }
 }
 
@@ -418,6 +553,122 @@ void launch_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh, bool alt) {
   PCONV_FAIL("swar temporal kernel: unsupported tile shape");
 }
 
+// Persistent prefetching launches (k_swar_pf): shapes instantiated, and the
+// grid = resident workgroups (occupancy x CUs), never more than the tiles.
+constexpr SwarShape kPfShapes[] = {
+    {4, 8, 8}, {4, 12, 4}, {4, 16, 4}, {4, 12, 8}, {4, 16, 8}, {4, 20, 8},
+};
+
+bool known_pf_shape(const SwarShape& s) {
+  for (const auto& k : kPfShapes)
+    if (k.lw == s.lw && k.m == s.m && k.nw == s.nw) return true;
+  return false;
+}
+
+std::atomic<int> g_pf_mode{-2};  // -2: PCONV_PREFETCH on first use; -1 tune, 0 off, 1 forced
+// 0: one workgroup per tile (the tuned form); < 0: persistent, the resident
+// workgroup count (A/B); > 0: persistent, at most this many (tests: many
+// tiles per workgroup)
+std::atomic<int> g_pf_grid_cap{0};
+
+int pf_mode() {
+  int v = g_pf_mode.load(std::memory_order_relaxed);
+  if (v == -2) {
+    const char* e = std::getenv("PCONV_PREFETCH");
+    v = !e ? -1 : e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
+    g_pf_mode.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+
+template <int CH, int M, int NW>
+const void* pf_fn(bool alt) {
+  return alt ? reinterpret_cast<const void*>(&k_swar_pf<CH, M, NW, true>)
+             : reinterpret_cast<const void*>(&k_swar_pf<CH, M, NW, false>);
+}
+
+int cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 256;
+  }
+  return n > 0 ? n : 256;
+}
+
+int pf_resident_wgs(const void* fn, int threads) {
+  static std::mutex mu;
+  static std::map<const void*, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(fn);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0;
+  PCONV_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0));
+  const int n = std::max(1, per_cu) * cu_count();
+  cache.emplace(fn, n);
+  return n;
+}
+
+// Launches the prefetch kernel can take: 4-byte lanes, whole dwords per row,
+// source and destination ranges under 2 GiB (32-bit buffer offsets).
+bool pf_launch_ok(const StencilLaunch& a, int steps) {
+  const int64_t src_rows = (a.r1 + steps) - (a.r0 - steps), dp = a.dst_pitch ? a.dst_pitch : a.pitch;
+  return a.row_bytes % 4 == 0 && src_rows * a.pitch < (int64_t(1) << 31) && (a.r1 - a.r0) * dp < (int64_t(1) << 31);
+}
+
+template <int CH, int M, int NW>
+void launch_pf_one(const StencilLaunch& a, hipStream_t s, bool alt) {
+  const int steps = a.steps;
+  const int hl = (steps * CH + 3) / 4;
+  const int vbytes = (64 - 2 * hl) * 4;
+  const int vrows = M * NW - 2 * steps;
+  PCONV_CHECK(vbytes > 0 && vrows > 0, "swar prefetch kernel: steps too large for the tile");
+  PCONV_CHECK(pf_launch_ok(a, steps), "swar prefetch kernel: needs whole dwords per row and < 2 GiB ranges");
+  const int nstrips = static_cast<int>(ceil_div<int64_t>(a.row_bytes, vbytes));
+  const int pair_stride = (nstrips + 1) / 2;
+  const int row_tiles = ceil_div(static_cast<int>(a.r1 - a.r0), vrows);
+  const int64_t ntiles = int64_t(pair_stride) * row_tiles;
+  PCONV_CHECK(ntiles < (int64_t(1) << 31), "swar prefetch kernel: too many tiles");
+  const int cap = g_pf_grid_cap.load(std::memory_order_relaxed);
+  int64_t wgs = ntiles;
+  if (cap != 0) {
+    wgs = pf_resident_wgs(pf_fn<CH, M, NW>(alt), 64 * NW);
+    if (cap > 0) wgs = std::min<int64_t>(wgs, cap);
+  }
+  const int grid = static_cast<int>(std::min<int64_t>(ntiles, wgs));
+  const int hmax = static_cast<int>(std::min<int64_t>(a.height, int64_t(1) << 30));
+  const int dp = static_cast<int>(a.dst_pitch ? a.dst_pitch : a.pitch);
+  if (alt)
+    k_swar_pf<CH, M, NW, true><<<dim3(grid), dim3(64 * NW), 0, s>>>(
+        a.src, a.dst, static_cast<int>(a.pitch), dp, static_cast<int>(a.row_bytes), static_cast<int>(a.r0),
+        static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), hmax, nstrips, pair_stride, row_tiles);
+  else
+    k_swar_pf<CH, M, NW, false><<<dim3(grid), dim3(64 * NW), 0, s>>>(
+        a.src, a.dst, static_cast<int>(a.pitch), dp, static_cast<int>(a.row_bytes), static_cast<int>(a.r0),
+        static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), hmax, nstrips, pair_stride, row_tiles);
+}
+
+// Tiles of a launch and the workgroups the prefetch kernel keeps resident.
+int64_t pf_tiles(SwarShape sh, int ch, int steps, int64_t rows, int64_t row_bytes) {
+  const int hl = (steps * ch + sh.lw - 1) / sh.lw;
+  const int vbytes = (64 - 2 * hl) * sh.lw;
+  const int vrows = sh.m * sh.nw - 2 * steps;
+  if (vbytes <= 0 || vrows <= 0 || sh.lw < ch || rows <= 0) return 0;
+  return ((ceil_div<int64_t>(row_bytes, vbytes) + 1) / 2) * ceil_div<int64_t>(rows, vrows);
+}
+
+template <int CH>
+void launch_pf_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh, bool alt) {
+#define PCONV_PF(LW_, M_, NW_)                       \
+  if (sh.lw == LW_ && sh.m == M_ && sh.nw == NW_) {  \
+    launch_pf_one<CH, M_, NW_>(a, s, alt);           \
+    return;                                          \
+  }
+  PCONV_PF(4, 8, 8) PCONV_PF(4, 12, 4) PCONV_PF(4, 16, 4) PCONV_PF(4, 12, 8) PCONV_PF(4, 16, 8) PCONV_PF(4, 20, 8)
+#undef PCONV_PF
+  PCONV_FAIL("swar prefetch kernel: unsupported tile shape");
+}
+
 // Row-streaming launches: (NP, T) instantiations, T = the launch's steps.
 struct StreamCfg {
   int np = 0;    // 0: tile kernel
@@ -634,6 +885,11 @@ KernelRes kernel_res(SwarShape sh, int ch, bool alt) {
 void set_xcd_swizzle(bool on) { g_xcd_swizzle.store(on ? 1 : 0, std::memory_order_relaxed); }
 void set_swar_alt(int mode) { g_alt_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
 void set_stream_mode(int mode) { g_stream_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
+void set_prefetch_mode(int mode, int grid_cap) {
+  g_pf_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed);
+  g_pf_grid_cap.store(grid_cap, std::memory_order_relaxed);
+}
+std::vector<SwarShape> swar_prefetch_shapes() { return std::vector<SwarShape>(std::begin(kPfShapes), std::end(kPfShapes)); }
 
 SwarResources swar_resources(SwarShape s, int ch) {
   const KernelRes r = kernel_res(s, ch, default_alt());
@@ -689,9 +945,18 @@ struct SwarChoice {
   SwarShape shape;
   bool alt = true;
   StreamCfg stream;  // np > 0: row-streaming kernel instead of the tile kernel
+  bool pf = false;   // persistent prefetching tile kernel (k_swar_pf)
 };
 
 void launch_choice(const StencilLaunch& a, Channels ch, hipStream_t stream, SwarChoice c) {
+  if (c.pf) {
+    switch (ch) {
+      case Channels::Grey: launch_pf_ch<1>(a, stream, c.shape, c.alt); break;
+      case Channels::Rgb: launch_pf_ch<3>(a, stream, c.shape, c.alt); break;
+      case Channels::Rgba: launch_pf_ch<4>(a, stream, c.shape, c.alt); break;
+    }
+    return;
+  }
   if (c.stream.np > 0) {
     switch (ch) {
       case Channels::Grey: launch_stream_ch<1>(a, stream, c.stream, c.alt); break;
@@ -753,6 +1018,25 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
     fallback.stream = StreamCfg{4, 1};  // forced streaming kernel, untuned
     return fallback;
   }
+  if (pf_mode() == 1 && pf_launch_ok(a, a.steps) && (override_shape(fallback.shape) || !autotune_enabled())) {
+    // forced prefetch kernel, untuned: the overridden shape if it has a
+    // prefetch instantiation, else the first prefetch shape that runs
+    if (!override_shape(fallback.shape) || !known_pf_shape(fallback.shape) ||
+        pf_tiles(fallback.shape, c, a.steps, rows, a.row_bytes) == 0) {
+      fallback.shape = SwarShape{0, 0, 0};
+      for (const auto& p : kPfShapes)
+        if (pf_tiles(p, c, a.steps, rows, a.row_bytes) > 0) {
+          fallback.shape = p;
+          break;
+        }
+    }
+    if (fallback.shape.m > 0) {
+      fallback.pf = true;
+      return fallback;
+    }
+    fallback.shape = pick_swar_shape(a.steps, c, rows, a.row_bytes);
+    return fallback;
+  }
   if (override_shape(fallback.shape) || !autotune_enabled()) {
     if (!override_shape(fallback.shape)) fallback.shape = pick_swar_shape(a.steps, c, rows, a.row_bytes);
     return fallback;
@@ -780,10 +1064,23 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   std::vector<SwarChoice> cands;
   for (const auto& r : ranked)
     for (int alt = 0; alt <= 1; ++alt)
-      if (mode < 0 || mode == alt) cands.push_back(SwarChoice{r.second, alt == 1, StreamCfg{}});
+      if (mode < 0 || mode == alt) cands.push_back(SwarChoice{r.second, alt == 1, StreamCfg{}, false});
   // Row-streaming candidates where the segments stay long against their
   // 2T-row run-in (large frames / bands): 8 segments' worth of rows per
   // strip pair at least.
+  // Buffer-op tile kernel (k_swar_pf, one workgroup per tile) for the
+  // model's candidate shapes it instantiates: hardware zero-fill of rows and
+  // lanes outside the frame instead of branches (measured 2-6 % faster on RGB
+  // frames, slower on grey ones: profiles/r02/prefetch_kernel.md).
+  if (pf_mode() != 0 && pf_launch_ok(a, a.steps)) {
+    std::vector<SwarChoice> pfs;
+    for (const auto& r : ranked)
+      if (known_pf_shape(r.second))
+        for (int alt = 0; alt <= 1; ++alt)
+          if (mode < 0 || mode == alt) pfs.push_back(SwarChoice{r.second, alt == 1, StreamCfg{}, true});
+    if (pf_mode() == 1 && !pfs.empty()) cands.clear();  // forced: only these candidates
+    cands.insert(cands.end(), pfs.begin(), pfs.end());
+  }
   if (stream_mode() != 0) {
     for (int np : {4}) {
       if (!stream_supported(c, np, a.steps)) continue;
@@ -791,7 +1088,7 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
         const StreamGrid g = stream_grid(c, np, a.steps, rows, a.row_bytes, 4, segf);
         if (g.nwaves == 0 || (stream_mode() != 1 && g.seg_rows < 8 * a.steps)) continue;
         for (int alt = 0; alt <= 1; ++alt)
-          if (mode < 0 || mode == alt) cands.push_back(SwarChoice{fallback.shape, alt == 1, StreamCfg{np, segf}});
+          if (mode < 0 || mode == alt) cands.push_back(SwarChoice{fallback.shape, alt == 1, StreamCfg{np, segf}, false});
       }
     }
     if (stream_mode() == 1) {  // forced: only streaming candidates (tests / A-B)
@@ -845,7 +1142,7 @@ std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned() {
   std::vector<std::pair<std::vector<int64_t>, SwarShape>> out;
   for (const auto& kv : g_tuned)
     out.push_back({{kv.first.ch, kv.first.steps, kv.first.rows, kv.first.row_bytes, kv.second.alt ? 1 : 0,
-                    kv.second.stream.np, kv.second.stream.segf},
+                    kv.second.stream.np, kv.second.stream.segf, kv.second.pf ? 1 : 0},
                    kv.second.shape});
   return out;
 }

@@ -338,6 +338,15 @@ PYBIND11_MODULE(_pconv_native, m) {
   m.def("set_stream_mode", &set_stream_mode, py::arg("mode"),
         "Row-streaming temporal kernel: -1 tuned against the tile kernel, 0 never (default), 1 forced where it "
         "applies (8-step launches)");
+  m.def("set_prefetch_mode", &set_prefetch_mode, py::arg("mode"), py::arg("grid_cap") = 0,
+        "Buffer-op tile kernel: -1 tuned against the others (default), 0 never, 1 forced (with a set_swar_shape "
+        "shape it instantiates, that shape); grid_cap 0: one workgroup per tile, < 0: persistent resident "
+        "workgroups prefetching the next tile, > 0: persistent, at most that many workgroups (tests)");
+  m.def("swar_prefetch_shapes", []() {
+    py::list out;
+    for (const auto& s : swar_prefetch_shapes()) out.append(py::make_tuple(s.lw, s.m, s.nw));
+    return out;
+  });
   m.def("set_swar_alt", &set_swar_alt, py::arg("mode"),
         "SWAR step form: -1 tuned (default), 0 truncate every step, 1 pairs of steps with a x16 intermediate.");
   m.def("set_xcd_swizzle", &set_xcd_swizzle, py::arg("on"),

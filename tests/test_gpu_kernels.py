@@ -193,6 +193,60 @@ def test_every_swar_shape_bit_exact(native, rng, form):
         native.set_swar_alt(-1)
 
 
+@pytest.mark.parametrize("cap", [0, 13])
+@pytest.mark.parametrize("form", [0, 1])
+def test_prefetch_kernel_every_shape_bit_exact(native, rng, form, cap):
+    """The buffer-op tile kernel (k_swar_pf), forced in each shape and step
+    form: whole images and band regions with ghost rows and image edges,
+    guard-band canaries, untouched rows outside [r0, r1).  cap 0: one
+    workgroup per tile (the tuned form); cap 13: persistent, 13 workgroups
+    (not a multiple of the 8 XCDs) each walking many tiles — the prefetch of
+    the next tile, the rotated loop and the per-XCD tile runs."""
+    try:
+        native.set_swar_alt(form)
+        native.set_prefetch_mode(1, cap)
+        for (lw, m, nw) in native.swar_prefetch_shapes():
+            native.set_swar_shape(lw, m, nw)
+            for channels, steps in (("grey", 3), ("rgb", 4), ("rgba", 2), ("rgb", 8), ("grey", 8), ("rgb", 1)):
+                if m * nw <= 2 * steps:
+                    continue
+                c = CH[channels]
+                w = 300 if c == 1 else 100  # row bytes multiple of 4 (the kernel's contract)
+                img = rng.integers(0, 256, size=(131, w, c) if c > 1 else (131, w), dtype=np.uint8)
+                gpu, cpu = _run_fused(native, img, steps, 0, 131, steps, 0, 131, variant="temporal")
+                assert np.array_equal(gpu, cpu), (lw, m, nw, channels, steps)
+                gpu, cpu = _run_fused(native, img[:40], steps, -5, 45, 16, 30, 200, variant="temporal")
+                assert np.array_equal(gpu[11:61], cpu[11:61]), (lw, m, nw, channels, steps, "band")
+    finally:
+        native.set_prefetch_mode(-1, 0)
+        native.set_swar_shape(0, 0, 0)
+        native.set_swar_alt(-1)
+        native.clear_swar_tuning()
+
+
+def test_prefetch_kernel_tuned_large_frame(native, rng):
+    """Tuned (default) choice on a frame with many tiles per resident
+    workgroup, with the prefetch kernel among the candidates, against the CPU
+    fused reference; and the prefetch kernel forced at its full grid."""
+    import torch
+
+    h, w = 1536, 4096
+    img = rng.integers(0, 256, size=(h, w), dtype=np.uint8)
+    try:
+        native.clear_swar_tuning()
+        gpu, cpu = _run_fused(native, img, 8, 0, h, 8, 0, h, variant="temporal")
+        assert np.array_equal(gpu, cpu)
+        native.set_prefetch_mode(1, -1)  # persistent, full resident grid
+        native.set_swar_shape(4, 16, 8)
+        gpu, cpu = _run_fused(native, img, 8, 0, h, 8, 0, h, variant="temporal")
+        assert np.array_equal(gpu, cpu)
+    finally:
+        native.set_prefetch_mode(-1, 0)
+        native.set_swar_shape(0, 0, 0)
+        native.clear_swar_tuning()
+        torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("steps", [4, 6, 8])
 @pytest.mark.parametrize("form", [0, 1])
 def test_row_streaming_kernel_bit_exact(native, rng, form, steps):
