@@ -75,7 +75,7 @@ bool supports_fusion(const Filter& f, KernelVariant v);
 // taller-wave tiles 8 wins or ties everywhere — 32768^2 grey 121 us/rep at 8
 // ({4,16,8}) vs 129 at 6 (6-level streaming kernel), 1920x2520 RGB 3.5 vs
 // 4.0; 8192^2 RGB is within 2 % either way.
-int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes);
+int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes, int channels = 0);
 
 // Row copy by the CUs: `rows` rows of `row_bytes` from src (row pitch sp) to
 // dst (row pitch dp); either side may be pinned host memory (the CUs move the

@@ -476,9 +476,15 @@ bool supports_fusion(const Filter& f, KernelVariant v) {
          (v == KernelVariant::Auto || v == KernelVariant::Temporal || v == KernelVariant::TemporalPk);
 }
 
-int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes) {
-  (void)frame_bytes;  // measured: 8 wins or ties on every BASELINE frame (profiles/r02/tile_shapes.md)
-  return supports_fusion(f, v) ? 8 : 1;
+int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes, int channels) {
+  if (!supports_fusion(f, v)) return 1;
+  // Grey frames far beyond the Infinity Cache: 12 repetitions per launch
+  // measured 2-6 % faster than 8 in every run (32768^2: 113.2-116.2 vs
+  // 116.9-121.1 us/rep over four boxes; 16384^2: 30.6 vs 32.2;
+  // profiles/r02/tile_shapes.md, prefetch_kernel.md).  RGB's horizontal halo
+  // is 3x wider and deeper fusion makes it slower: 8 everywhere else.
+  if (channels == 1 && frame_bytes >= (int64_t(256) << 20)) return 12;
+  return 8;
 }
 
 

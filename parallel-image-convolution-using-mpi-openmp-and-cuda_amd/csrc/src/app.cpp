@@ -60,7 +60,7 @@ EngineOptions engine_options(const CliConfig& c, const ImageGeom& g, int world, 
   o.overlap = c.overlap;
   o.use_graph = c.graph && world == 1;
   const bool fusable = supports_fusion(f, c.variant);
-  o.fuse = c.fuse > 0 ? c.fuse : auto_fuse(f, c.variant, g.row_bytes() * (g.height / std::max(1, world)));
+  o.fuse = c.fuse > 0 ? c.fuse : auto_fuse(f, c.variant, g.row_bytes() * (g.height / std::max(1, world)), g.ch());
   if (!fusable) o.fuse = 1;
   o.fuse = std::max(1, std::min(o.fuse, std::max(1, c.reps)));
   if (c.halo > 0) {

@@ -366,11 +366,11 @@ PYBIND11_MODULE(_pconv_native, m) {
       },
       py::arg("steps"), py::arg("channels"), py::arg("rows"), py::arg("row_bytes"));
   m.def("auto_fuse",
-        [](py::object filter, const std::string& v, int64_t frame_bytes) {
-          return auto_fuse(make_filter(filter), parse_variant(v), frame_bytes);
+        [](py::object filter, const std::string& v, int64_t frame_bytes, int channels) {
+          return auto_fuse(make_filter(filter), parse_variant(v), frame_bytes, channels);
         },
-        py::arg("filter"), py::arg("variant"), py::arg("frame_bytes"),
-        "Default repetitions per launch for a band frame of `frame_bytes`");
+        py::arg("filter"), py::arg("variant"), py::arg("frame_bytes"), py::arg("channels") = 0,
+        "Default repetitions per launch for a band frame of `frame_bytes` with `channels` bytes per pixel");
   m.def("supports_fusion",
         [](py::object filter, const std::string& v) { return supports_fusion(make_filter(filter), parse_variant(v)); },
         py::arg("filter"), py::arg("variant") = "auto");

@@ -50,7 +50,8 @@ class Engine:
         self.filter = get_filter(filter)
         nf = self.filter.to_native()
         if fuse is None:
-            fuse = n.auto_fuse(nf, variant, int(width) * int(height) * {"grey": 1, "rgb": 3, "rgba": 4}[channels])
+            ch = {"grey": 1, "rgb": 3, "rgba": 4}[channels]
+            fuse = n.auto_fuse(nf, variant, int(width) * int(height) * ch, ch)
         self.width, self.height, self.channels = int(width), int(height), channels
         self.device = int(device)
         self._eng = n.BandEngine(self.width, self.height, channels, nf, 0, 1, self.device, halo=int(fuse),

@@ -69,7 +69,7 @@ class DistributedBlur:
         nf = get_filter(filter).to_native()
         if fuse is None:
             ch = {"grey": 1, "rgb": 3, "rgba": 4}[channels]
-            fuse = n.auto_fuse(nf, variant, self.width * ch * (self.height // max(1, self.world)))
+            fuse = n.auto_fuse(nf, variant, self.width * ch * (self.height // max(1, self.world)), ch)
         if halo is None:
             halo = auto_halo(self.height, self.world, reps, fuse, preload=bool(preload_halo) and not slot_exchange)
         kw = dict(halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant, slots=int(slots),

@@ -88,7 +88,7 @@ class _HipBand:
 
         nf = get_filter(a.filter).to_native()
         frame = a.width * _CH[a.channels] * (a.height // max(1, world))
-        fuse = a.fuse if a.fuse is not None else n.auto_fuse(nf, "auto", frame)
+        fuse = a.fuse if a.fuse is not None else n.auto_fuse(nf, "auto", frame, _CH[a.channels])
         halo = a.halo if a.halo is not None else auto_halo(a.height, world, a.reps, fuse)
         self.eng = n.BandEngine(a.width, a.height, a.channels, nf, rank, world, device, halo=int(halo),
                                 fuse=int(fuse), overlap=not a.no_overlap)

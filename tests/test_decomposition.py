@@ -139,3 +139,20 @@ def test_cpu_fused_launch_matches_repeated_steps(native, rng):
         ref = numpy_convolve(img, steps)
         got = dst.reshape(h + 2 * halo, lay["pitch"])[halo + 3 : halo + 15, 16 : 16 + w]
         assert np.array_equal(got, ref[3:15])
+
+
+def test_auto_fuse_policy(native, pconv_mod):
+    """Repetitions per launch: 12 for grey frames far beyond the Infinity
+    Cache (measured faster there), 8 for every other fusable frame, 1 for
+    filters the fused kernel does not implement."""
+    from pconv.models.filters import get_filter
+
+    g = get_filter("gaussian").to_native()
+    assert native.auto_fuse(g, "auto", 32768 * 32768, 1) == 12
+    assert native.auto_fuse(g, "auto", 16384 * 16384, 1) == 12
+    assert native.auto_fuse(g, "auto", 8192 * 8192 * 3, 3) == 8
+    assert native.auto_fuse(g, "auto", 1920 * 2520 * 3, 3) == 8
+    assert native.auto_fuse(g, "auto", 1920 * 2520, 1) == 8
+    assert native.auto_fuse(g, "auto", 32768 * 4096, 1) == 8  # 8-way band of 32768^2
+    assert native.auto_fuse(g, "auto", 32768 * 32768) == 8  # channels unknown
+    assert native.auto_fuse(get_filter("box").to_native(), "auto", 32768 * 32768, 1) == 1
