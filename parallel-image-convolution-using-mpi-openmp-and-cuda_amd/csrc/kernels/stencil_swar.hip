@@ -156,8 +156,8 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
 // frame get an offset past the descriptor's range, so the hardware returns
 // zeros / drops the store instead of the branches k_swar takes around each
 // chunk, and every wave issues exactly 2M loads and 2M stores per tile.  One
-// workgroup per tile is the form the tuner times against k_swar (2-6 %
-// faster on RGB frames, e.g. the headline 3.45 -> 3.26 us/rep; slower on
+// workgroup per tile is the form the tuner times against k_swar (4-8 %
+// faster on RGB frames, e.g. the headline 3.47 -> 3.19 us/rep; slower on
 // grey ones, where its ALT form needs far more VGPRs:
 // profiles/r02/prefetch_kernel.md).
 //   Persistent form (opt-in, set_prefetch_mode(mode, cap != 0)): a resident
@@ -237,10 +237,12 @@ __global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__
   while (true) {
     const int next = tile + t_step;
     const bool more = next < t_end;
-    int nA, nB, nrow;
-    bool nmask;
-    geo(more ? next : tile, nA, nB, nrow, nmask);
-    fetch(more ? nA : -1, more ? nB : -1, nrow);  // in flight during this tile's steps (all-zero past the end)
+    int nA = -1, nB = -1, nrow = 0;
+    bool nmask = false;
+    if (more) {  // wave-uniform; never taken with one workgroup per tile
+      geo(next, nA, nB, nrow, nmask);
+      fetch(nA, nB, nrow);  // in flight during this tile's steps
+    }
     u32 cm[NP];
 #pragma unroll
     for (int k = 0; k < NP; ++k)
