@@ -71,7 +71,8 @@ def test_multiprocess_bands_one_gpu(pconv_mod, world, halo, fuse, preload, slots
 
 
 @pytest.mark.parametrize("world,extra", [(2, []), (3, ["--halo-mode", "exchange"]), (4, []),
-                                         (2, ["--slots", "1", "--no-overlap", "--halo-mode", "exchange"])])
+                                         (2, ["--slots", "1", "--no-overlap", "--halo-mode", "exchange"]),
+                                         (2, ["--halo-select", "exchange"])])
 def test_bench_torchrun_rehearsal(world, extra):
     """bench.py under torch.distributed.run with `world` ranks sharing the one
     GPU (gloo-host halos): the driver's N-GPU launch path, checked bit-exact."""
@@ -93,6 +94,13 @@ def test_bench_torchrun_rehearsal(world, extra):
     hx = meta["halo_exchange"]  # secondary run: ghost rows exchanged, one transport per slot
     assert hx["status"] == "ok", hx
     assert hx["mismatches_vs_headline"] == 0 and hx["exchanges_per_step"] >= 1
+    sel = meta["halo_select"]
+    if "--halo-select" in extra:  # forced adoption: the headline is K timed steps of the exchange pipeline
+        assert sel["mode"] == "exchange" and sel["preload_ms_per_step"] > 0
+        assert meta["headline_transport"] == "gloo-host" and meta["config"]["exchanges_per_step"] >= 1
+        assert meta["config"]["preload_halo"] is False
+    elif "--halo-mode" not in extra:
+        assert sel["mode"] in ("preload", "exchange")
 
 
 def test_bench_exchange_watchdog():
