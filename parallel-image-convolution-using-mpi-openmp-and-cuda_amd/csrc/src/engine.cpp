@@ -495,7 +495,9 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
     step_graphs_ = step_graphs;
     concurrent_ = slots > 1;
     EngineOptions o = opt;
-    o.use_graph = false;
+    // Directly issued images (exchange mode) replay their repetitions as the
+    // engine's cached rep-loop graph whenever no exchange phase remains.
+    o.use_graph = !step_graphs;
     o.timing = false;
     o.overlap = false;  // an image's exchange and launches share its stream: no split launches
     for (int i = 0; i < slots; ++i) {
@@ -569,7 +571,15 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
     trace_mark(0, cs);
     e.upload_rows(host_in, e.layout().row_bytes, in_r0, in_r1);
     trace_mark(1, cs);
-    e.set_halo_valid(preloaded);
+    if (!preloaded && e.exchange_free(reps, true)) {
+      // The ghost zone covers all `reps`: ONE exchange of the whole zone in
+      // stream order, then the repetitions need none and run() launches them
+      // as one cached graph — an image costs the upload, the transport's
+      // calls, one graph launch and the download on the host.
+      e.exchange_now(cs);
+    } else {
+      e.set_halo_valid(preloaded);
+    }
     e.run(reps);
     trace_mark(2, cs);
     e.download_rows(host_out, e.layout().row_bytes, 0, e.band().rows);
