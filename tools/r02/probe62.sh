@@ -1,0 +1,23 @@
+#!/usr/bin/env bash
+# Round-2 probe 62: final-tree evidence after the exchange-mode pipeline change, the buffer-op tile kernel and
+# the grey large-frame fuse policy: full GPU suite, smoke, the driver's bench
+# command, rocprofv3 kernel stats of it, and the BASELINE configs.
+set -euo pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r02/probe62
+mkdir -p "$O"
+rc=0
+timeout -k 10 700 python3 -u -m pytest tests -m gpu -q --timeout 150 --timeout-method thread > "$O/pytest_gpu.log" 2>&1 || rc=$?
+tail -n 3 "$O/pytest_gpu.log"
+if [ "$rc" -gt 1 ]; then exit "$rc"; fi
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
+tail -n 1 "$O/smoke.log"
+timeout -k 10 120 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_n1.json" 2> "$O/bench.err"
+cut -c1-200 "$O/bench_n1.json"
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/prof_bench.json" 2> "$O/prof.err"
+find "$O/prof" -name "*kernel_stats.csv" > "$O/files.txt"
+cat "$O/files.txt"
+timeout -k 10 900 bash tools/baseline_configs.sh > "$O/baseline.txt" 2>&1
+cp gpurun_out/baseline/*.json "$O/" || true
+tail -n 24 "$O/baseline.txt" | cut -c1-240
+exit $rc
