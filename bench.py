@@ -510,7 +510,10 @@ def main():
                     adopted["vs_baseline"] = round(adopted["value"] / BASELINE_MPIX, 2)
                 adopted["config"] = dict(out["config"], preload_halo=False, halo_depth=int(xb.engine.halo),
                                          launches_per_step=int(st.launches), exchanges_per_step=int(st.exchanges),
-                                         images_in_flight=a.slots)
+                                         images_in_flight=a.slots, slot_streams=bool(xb.pipe.graphs),
+                                         step_graphs=bool(xb.pipe.step_graphs),
+                                         concurrent_images=bool(xb.pipe.concurrent), zero_copy_out=False,
+                                         packed_d2h=False, split_d2h=False)
                 adopted["halo_select"] = {"mode": "exchange", "preload_ms_per_step": out["ms_per_step"],
                                           "preload_value": out["value"]}
                 out = adopted
