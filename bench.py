@@ -475,6 +475,7 @@ def main():
                 print(json.dumps(line), flush=True)
                 emitted.append(True)
 
+    dog = None
     if world > 1 and not a.emulate and (a.exchange_check == "on" or (a.exchange_check == "auto" and world > 1)):
         # Secondary measurement after the headline is final.  A watchdog on
         # every rank bounds it (communicator set-up included): on expiry rank
@@ -498,8 +499,14 @@ def main():
             halo_exchange.get("mismatches_vs_headline") == 0 and head_transport == "none"
         adopt = ok and (a.halo_select == "exchange" or
                         (a.halo_select == "auto" and halo_exchange["ms_per_step"] < 0.97 * head_ms))
+        x_elapsed = None
         if adopt:
-            x_elapsed = timed_steps(xb, a.steps, a.reps, a.exchange_timeout)
+            try:
+                x_elapsed = timed_steps(xb, a.steps, a.reps, a.exchange_timeout)
+            except Exception as e:  # the pre-loaded headline stands
+                if out is not None:
+                    out["halo_select"] = {"mode": "preload", "reason": f"exchange re-time failed: {e}"[:300]}
+        if x_elapsed is not None:
             if out is not None:
                 st = xb.stats
                 adopted = dict(out)
@@ -517,15 +524,18 @@ def main():
                 adopted["halo_select"] = {"mode": "exchange", "preload_ms_per_step": out["ms_per_step"],
                                           "preload_value": out["value"]}
                 out = adopted
-        elif out is not None:
+        elif out is not None and not adopt:
             why = "headline exchanges halos" if head_transport != "none" else \
                 "exchange not faster" if ok else "exchange check failed"
             out["halo_select"] = {"mode": "preload" if head_transport == "none" else "exchange", "reason": why}
-        dog.cancel()
         if out is not None:
             out["halo_exchange"] = halo_exchange
     emit(out)
+    # The watchdog (N>1) stays armed through the process-group shutdown: a
+    # peer stuck in the exchange can then never keep this rank alive.
     shutdown(ctx)
+    if dog is not None:
+        dog.cancel()
 
 
 if __name__ == "__main__":
