@@ -46,6 +46,9 @@ constexpr T round_up(T a, T b) { return ceil_div(a, b) * b; }
 // whose gettimeofday call sat inside assert() and vanished under NDEBUG).
 double wall_seconds();
 
+// Escape a free-form string (paths, error text) for a JSON string literal.
+std::string json_escape(const std::string& s);
+
 }  // namespace pconv
 
 #define PCONV_FAIL(msg) ::pconv::raise_error(__FILE__, __LINE__, (msg))

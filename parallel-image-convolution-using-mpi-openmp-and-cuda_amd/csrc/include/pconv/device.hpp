@@ -30,6 +30,17 @@ void set_device(int device);
 std::string device_name(int device);
 // PCI address of a device, lower case ("0000:75:00.0").
 std::string device_pci_bus_id(int device);
+// The HIP runtime this process runs on (which may differ from the one the
+// code was compiled against: torch processes load torch's bundled runtime):
+// runtime and driver versions from the API, the runtime library's path, and
+// the compile-time HIP version.
+struct HipRuntimeInfo {
+  int runtime_version = 0;
+  int driver_version = 0;
+  std::string runtime_path;
+  std::string compiled_version;
+};
+HipRuntimeInfo hip_runtime_info();
 // Restrict the calling process to the CPUs local to `device` (sysfs
 // local_cpulist of its PCI function, intersected with the current affinity);
 // PCONV_NUMA_BIND=0 disables.  Returns the CPUs kept, 0 if nothing changed.

@@ -71,10 +71,12 @@ void prepare_stencil(const Filter& f, Channels ch, const StencilLaunch& a, hipSt
 bool supports_fusion(const Filter& f, KernelVariant v);
 
 // Default repetitions per launch for a band frame of `frame_bytes`: 1 without
-// fusion, else 8.  Measured per frame (profiles/r02/tile_shapes.md): with the
-// taller-wave tiles 8 wins or ties everywhere — 32768^2 grey 121 us/rep at 8
-// ({4,16,8}) vs 129 at 6 (6-level streaming kernel), 1920x2520 RGB 3.5 vs
-// 4.0; 8192^2 RGB is within 2 % either way.
+// fusion; 12 for grey frames of 256 MiB and more (far beyond the Infinity
+// Cache: 32768^2 grey 113.2-116.2 us/rep at 12 vs 116.9-121.1 at 8 over four
+// boxes, 16384^2 30.6 vs 32.2; profiles/r02/tile_shapes.md,
+// prefetch_kernel.md); 8 everywhere else (RGB's 3x wider horizontal halo makes
+// deeper fusion slower; 1920x2520 RGB 3.5 us/rep at 8 vs 4.0 at 6, 8192^2 RGB
+// within 2 % either way).
 int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes, int channels = 0);
 
 // Row copy by the CUs: `rows` rows of `row_bytes` from src (row pitch sp) to

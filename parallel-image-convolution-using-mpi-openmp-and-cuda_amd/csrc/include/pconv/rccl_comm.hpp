@@ -32,6 +32,10 @@ std::string rccl_version();
 // True once librccl is mapped into this process (it is dlopen'ed on the first
 // RCCL call, never at start-up).
 bool rccl_loaded();
+// Path of the librccl this process mapped ("" while none is mapped): in a
+// torch process `librccl.so.1` resolves to torch's bundled copy, in the `conv`
+// CLI to ROCm's.
+std::string rccl_library_path();
 
 class RcclComm {
  public:

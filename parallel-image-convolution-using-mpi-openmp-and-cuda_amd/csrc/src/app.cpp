@@ -606,8 +606,15 @@ std::string report_json(const CliConfig& c, const AppReport& r) {
      << ", \"fuse\": " << r.fuse << ", \"launches\": " << r.launches << ", \"exchanges\": " << r.exchanges
      << ", \"loop_s\": " << r.loop_s << ", \"e2e_s\": " << r.e2e_s << ", \"loop_mpix_per_s\": " << r.mpix_per_s
      << ", \"e2e_mpix_per_s\": " << (r.e2e_s > 0 ? px / r.e2e_s / 1e6 : 0.0)
-     << ", \"mismatches\": " << r.mismatches << ", \"output\": \"" << r.output << "\""
+     << ", \"mismatches\": " << r.mismatches << ", \"output\": \"" << json_escape(r.output) << "\""
      << ", \"rccl_loaded\": " << (rccl_loaded() ? "true" : "false");
+  if (rccl_loaded()) os << ", \"rccl_version\": \"" << rccl_version() << "\", \"rccl_path\": \""
+                        << json_escape(rccl_library_path()) << "\"";
+  if (c.backend == Backend::Hip && c.gpus <= 1) {  // (the --gpus N launcher process never touches HIP)
+    const HipRuntimeInfo h = hip_runtime_info();
+    os << ", \"hip_runtime_version\": " << h.runtime_version << ", \"hip_runtime_path\": \""
+       << json_escape(h.runtime_path) << "\"";
+  }
   if (!r.copies.empty()) os << ", \"copies\": \"" << r.copies << "\"";
   if (!r.phases.empty()) {
     os << ", \"phases_s\": {";

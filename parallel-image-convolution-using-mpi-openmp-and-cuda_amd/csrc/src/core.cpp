@@ -31,6 +31,19 @@ void raise_error(const char* file, int line, const std::string& msg) {
   throw Error(os.str());
 }
 
+std::string json_escape(const std::string& s) {
+  std::string o;
+  for (char ch : s) {
+    if (ch == '"' || ch == '\\') o += '\\';
+    if (static_cast<unsigned char>(ch) < 0x20) {
+      o += ' ';
+      continue;
+    }
+    o += ch;
+  }
+  return o;
+}
+
 double wall_seconds() {
   using clk = std::chrono::steady_clock;
   return std::chrono::duration<double>(clk::now().time_since_epoch()).count();

@@ -1,6 +1,7 @@
 // HIP runtime RAII wrappers (see device.hpp).
 #include "pconv/device.hpp"
 
+#include <dlfcn.h>
 #include <sched.h>
 
 #include <cctype>
@@ -29,6 +30,23 @@ std::string device_pci_bus_id(int device) {
   std::string id(buf);
   for (auto& c : id) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
   return id;
+}
+
+HipRuntimeInfo hip_runtime_info() {
+  HipRuntimeInfo r;
+  PCONV_HIP_CHECK(hipRuntimeGetVersion(&r.runtime_version));
+  (void)hipDriverGetVersion(&r.driver_version);
+  Dl_info info{};
+  if (dladdr(reinterpret_cast<void*>(&hipRuntimeGetVersion), &info) != 0 && info.dli_fname) {
+    r.runtime_path = info.dli_fname;
+    // the symbol's address may be this library's PLT stub: resolve the real
+    // definition through the global scope instead
+    if (void* real = dlsym(RTLD_DEFAULT, "hipRuntimeGetVersion"))
+      if (dladdr(real, &info) != 0 && info.dli_fname) r.runtime_path = info.dli_fname;
+  }
+  r.compiled_version = std::to_string(HIP_VERSION_MAJOR) + "." + std::to_string(HIP_VERSION_MINOR) + "." +
+                       std::to_string(HIP_VERSION_PATCH);
+  return r;
 }
 
 int bind_to_device_numa(int device) {

@@ -630,6 +630,22 @@ PYBIND11_MODULE(_pconv_native, m) {
   });
   m.def("rccl_version", &rccl_version);
   m.def("rccl_loaded", &rccl_loaded, "True once librccl is mapped (loaded lazily on the first RCCL call)");
+  m.def("rccl_library_path", &rccl_library_path, "path of the mapped librccl ('' while none is mapped)");
+  m.def(
+      "runtime_info",
+      []() {
+        const HipRuntimeInfo h = hip_runtime_info();
+        py::dict d;
+        d["hip_runtime_version"] = h.runtime_version;
+        d["hip_driver_version"] = h.driver_version;
+        d["hip_runtime_path"] = h.runtime_path;
+        d["hip_compiled_version"] = h.compiled_version;
+        const bool loaded = rccl_loaded();
+        d["rccl_version"] = loaded ? py::object(py::str(rccl_version())) : py::object(py::none());
+        d["rccl_path"] = loaded ? py::object(py::str(rccl_library_path())) : py::object(py::none());
+        return d;
+      },
+      "the HIP runtime / RCCL this process actually runs on (versions and library paths)");
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def(py::init([](py::bytes id, int rank, int world, int device) {
              const std::string s = id;

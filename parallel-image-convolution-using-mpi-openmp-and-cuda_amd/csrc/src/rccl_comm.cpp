@@ -84,6 +84,13 @@ bool rccl_loaded() {
   return h != nullptr;
 }
 
+std::string rccl_library_path() {
+  if (!rccl_loaded()) return "";
+  Dl_info info{};
+  if (dladdr(reinterpret_cast<void*>(rccl().GetVersion), &info) == 0 || info.dli_fname == nullptr) return "";
+  return info.dli_fname;
+}
+
 #define PCONV_RCCL_CHECK(expr)                                                                            \
   do {                                                                                                    \
     ncclResult_t _r = (expr);                                                                             \

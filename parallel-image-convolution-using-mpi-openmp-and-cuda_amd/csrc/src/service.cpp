@@ -67,19 +67,6 @@ struct Fd {
   }
 };
 
-std::string json_escape(const std::string& s) {
-  std::string o;
-  for (char ch : s) {
-    if (ch == '"' || ch == '\\') o += '\\';
-    if (static_cast<unsigned char>(ch) < 0x20) {
-      o += ' ';
-      continue;
-    }
-    o += ch;
-  }
-  return o;
-}
-
 }  // namespace
 
 ServeOptions parse_serve_args(const std::vector<std::string>& args) {

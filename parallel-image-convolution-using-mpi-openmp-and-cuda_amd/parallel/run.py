@@ -125,6 +125,7 @@ class _HipBand:
 
     @property
     def counts(self):
+        """(launches, exchanges) of the LAST run() (the caller sums chunks)."""
         s = self.eng.stats
         return int(s.launches), int(s.exchanges)
 
@@ -154,7 +155,9 @@ class _CpuBand:
         self._preloaded = halo_valid
 
     def run(self, reps: int) -> None:
+        before = self.r.exchanges
         self.r.run(reps, halo_preloaded=self._preloaded)
+        self._last_exchanges = self.r.exchanges - before
         self._preloaded = False  # a later run (after a checkpoint) exchanges its ghost rows
 
     def result(self, out: np.ndarray) -> None:
@@ -162,7 +165,8 @@ class _CpuBand:
 
     @property
     def counts(self):
-        return 0, int(self.r.exchanges)
+        """(launches, exchanges) of the LAST run() (the caller sums chunks)."""
+        return 0, int(getattr(self, "_last_exchanges", 0))
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -212,9 +216,13 @@ def main(argv: Optional[List[str]] = None) -> int:
         barrier()  # MPI_Barrier before MPI_Wtime (mpi_convolution.c:151-154)
         t0 = time.perf_counter()
         done = 0
+        launches = exchanges = 0  # summed over checkpoint chunks (each run() reports its own)
         while done < a.reps or (done == 0 and a.reps == 0):
             k = min(ce, a.reps - done) if ce > 0 else a.reps
             runner.run(k)
+            cl, cx = runner.counts
+            launches += cl
+            exchanges += cx
             done += k
             if done in ck:
                 runner.result(res)
@@ -228,7 +236,6 @@ def main(argv: Optional[List[str]] = None) -> int:
         n.write_raw_rows(out_path, res, a.width, a.height, a.channels, b.y0, b.rows)
         t_max = max_over_ranks(loop_s)
         barrier()
-        launches, exchanges = runner.counts
         mismatches = None
         if a.check:
             bad = 0

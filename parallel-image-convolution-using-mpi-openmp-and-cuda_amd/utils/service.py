@@ -92,6 +92,26 @@ def _recv_exact(s: socket.socket, n: int) -> bytes:
     return buf
 
 
+def _drain_stderr(p: subprocess.Popen, keep: int = 40) -> List[str]:
+    """Read the server's stderr on a daemon thread for as long as it runs
+    (served jobs may write to it: --explain plans, reply errors, HIP runtime
+    logs), so a full 64 KiB pipe can never block the server in a write and
+    hang every client.  The first `keep` lines are kept for error messages."""
+    import threading
+
+    head: List[str] = []
+
+    def pump():
+        for line in p.stderr:
+            if len(head) < keep:
+                head.append(line)
+
+    t = threading.Thread(target=pump, name="pconv-serve-stderr", daemon=True)
+    t.start()
+    p._pconv_stderr_thread = t  # type: ignore[attr-defined]
+    return head
+
+
 def start_server(socket_path: str, device: int = 0, idle_timeout: float = 0.0, max_engines: int = 8,
                  wait_s: float = 120.0) -> subprocess.Popen:
     """Start `conv --serve` as a child process and wait until it listens
@@ -100,6 +120,7 @@ def start_server(socket_path: str, device: int = 0, idle_timeout: float = 0.0, m
     or a live server at that path."""
     p = subprocess.Popen([conv_binary(), "--serve", socket_path, "--device", str(device), "--idle-timeout",
                           str(idle_timeout), "--max-engines", str(max_engines)], stderr=subprocess.PIPE, text=True)
+    err_head = _drain_stderr(p)
     t0 = time.time()
     while time.time() - t0 < wait_s:
         if os.path.exists(socket_path):
@@ -109,7 +130,8 @@ def start_server(socket_path: str, device: int = 0, idle_timeout: float = 0.0, m
             except (OSError, ServiceError):
                 pass
         if p.poll() is not None:
-            raise ServiceError(f"server exited: {p.stderr.read()}")
+            p._pconv_stderr_thread.join(timeout=5)  # type: ignore[attr-defined]
+            raise ServiceError(f"server exited: {''.join(err_head)}")
         time.sleep(0.05)
     p.kill()
     raise ServiceError("server did not start listening")

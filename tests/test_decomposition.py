@@ -156,3 +156,50 @@ def test_auto_fuse_policy(native, pconv_mod):
     assert native.auto_fuse(g, "auto", 32768 * 4096, 1) == 8  # 8-way band of 32768^2
     assert native.auto_fuse(g, "auto", 32768 * 32768) == 8  # channels unknown
     assert native.auto_fuse(get_filter("box").to_native(), "auto", 32768 * 32768, 1) == 1
+
+
+def _ext_model(owned, y0, height, plan, halo, reps):
+    """Independent model of a self-neighbour band: the extended array of
+    ghost + owned rows is stepped as a whole (zero outside it and outside the
+    global image); each exchange re-reflects the band's own rows into the
+    ghost zone.  Owned rows must match the frame-level oracle whenever the
+    plan is dependency safe."""
+    from pconv.ops.reference import numpy_convolve
+
+    rows = owned.shape[0]
+    ext = np.zeros((rows + 2 * halo,) + owned.shape[1:], np.uint8)
+    ext[halo:halo + rows] = owned
+    g = np.arange(-halo, rows + halo) + y0
+    outside = (g < 0) | (g >= height)
+    done = 0
+    for ph in plan:
+        d = ph.exchange_depth
+        if d:
+            ext[halo - d:halo] = ext[halo:halo + d]
+            ext[halo + rows:halo + rows + d] = ext[halo + rows - d:halo + rows]
+            ext[:halo - d] = 0  # stale beyond the exchanged depth: never read
+            ext[halo + rows + d:] = 0
+        for _ in range(ph.steps):
+            ext[outside] = 0
+            ext = numpy_convolve(ext, 1)
+        done += ph.steps
+    assert done == reps
+    return ext[halo:halo + rows]
+
+
+@pytest.mark.parametrize("reps,halo,fuse,overlap", [(13, 4, 4, True), (20, 8, 8, False), (5, 1, 1, True),
+                                                    (17, 6, 3, True), (40, 40, 8, True), (24, 12, 8, False)])
+@pytest.mark.parametrize("y0", [0, 9, 37])
+def test_reflected_ghost_oracle_cpu(native, rng, reps, halo, fuse, overlap, y0):
+    """The oracle of the GPU mid-image RCCL self-band tests
+    (tests/test_gpu_halo.py) agrees with an independent model."""
+    from halo_oracle import reflected_ghost_oracle
+
+    rows, w, height = 48, 29, y0 + 48 + 45
+    b = native.Band()
+    b.rank, b.world, b.y0, b.rows, b.up, b.down = 0, 1, y0, rows, 0, 0
+    d, t = native.normalize_plan(halo, fuse, 0)
+    plan = native.plan_band(b, reps, d, t, overlap, False)
+    owned = rng.integers(0, 256, size=(rows, w), dtype=np.uint8)
+    got = reflected_ghost_oracle(native, plan, d, owned, y0, height, "grey")
+    assert np.array_equal(got, _ext_model(owned, y0, height, plan, d, reps))

@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 
 from conftest import ROOT
+from halo_oracle import reflected_ghost_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -74,6 +75,63 @@ def test_rccl_self_band_runs_exact(pconv_mod, rng, overlap, reps, halo, fuse):
     eng.download(out.reshape(-1), 0, h)
     eng.synchronize()
     assert np.array_equal(out, pconv_mod.numpy_convolve(img, reps))
+
+
+def _mid_band(n, y0, rows):
+    """A band in the MIDDLE of a taller image whose up and down neighbour is
+    itself (1-rank communicator): RCCL send/recv-to-self then delivers the
+    band's own top rows as its ghost rows above and its bottom rows as its
+    ghost rows below.  Those ghost rows lie INSIDE the image, so the kernel
+    reads them (no zero boundary there) and the result depends on every byte
+    RCCL delivered, at every exchange phase."""
+    b = n.Band()
+    b.rank, b.world, b.y0, b.rows, b.up, b.down = 0, 1, y0, rows, 0, 0
+    return b
+
+
+@pytest.fixture(scope="module")
+def self_comm(pconv_mod):
+    n = pconv_mod.native
+    return n.RcclComm(n.rccl_unique_id(), 0, 1, 0)
+
+
+@pytest.mark.parametrize("ch,w", [("rgb", 57), ("grey", 1920)])
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("reps,halo,fuse", [(13, 4, 4), (20, 8, 8), (5, 1, 1), (17, 6, 3), (40, 40, 8), (24, 12, 8)])
+def test_rccl_mid_image_band_consumes_exchanged_rows(pconv_mod, rng, self_comm, ch, w, overlap, reps, halo, fuse):
+    """The RCCL-received ghost rows are CONSUMED: a mid-image self-neighbour
+    band (y0 > 0, y0 + rows < height) runs every exchange phase through
+    ncclSend/ncclRecv on the comm stream — with overlap, the interior launch
+    concurrently and the edge launches after ev_halo — and must equal the
+    reflected-ghost oracle byte for byte.  The reference's loop being replaced:
+    Isend/Irecv, inner compute, Wait, edges (mpi/mpi_convolution.c:156-240)."""
+    n = pconv_mod.native
+    c = {"grey": 1, "rgb": 3}[ch]
+    y0, rows, height = 37, 48, 130
+    eng = n.BandEngine.for_band(w, height, ch, "gaussian", _mid_band(n, y0, rows), 0, halo, fuse, overlap, "auto")
+    eng.attach_rccl(self_comm)
+    owned = rng.integers(0, 256, size=(rows, w * c), dtype=np.uint8)
+    plan = eng.plan(reps)
+    n_ex = len([p for p in plan if p.exchange_depth])
+    assert n_ex >= 1
+    if overlap and eng.halo < reps:
+        assert any(len(p.launches) > 1 and any(l.after_halo for l in p.launches) for p in plan if p.exchange_depth)
+    ref = reflected_ghost_oracle(n, plan, eng.halo, owned, y0, height, ch)
+    # the oracle really depends on the exchanged rows: zero ghost rows differ
+    assert not np.array_equal(ref, pconv_mod.numpy_convolve(owned.reshape(rows, w, c) if c > 1 else owned, reps)
+                              .reshape(rows, -1))
+    for _ in range(2):  # twice: the second run starts from the other frame parity
+        eng.upload(owned.reshape(-1), 0, rows)
+        eng.run(reps)
+        self_comm.wait(eng.comm_stream, 60.0)
+        self_comm.wait(eng.compute_stream, 60.0)
+        eng.synchronize()
+        assert eng.stats.exchanges == n_ex
+        out = np.empty_like(owned)
+        eng.download(out.reshape(-1), 0, rows)
+        eng.synchronize()
+        bad = int(np.count_nonzero(out != ref))
+        assert bad == 0, f"{bad} bytes differ from the reflected-ghost oracle"
 
 
 @pytest.mark.parametrize("bands", [2, 3, 5, 8])

@@ -72,10 +72,12 @@ def test_multiprocess_bands_one_gpu(pconv_mod, world, halo, fuse, preload, slots
 
 @pytest.mark.parametrize("world,extra", [(2, []), (3, ["--halo-mode", "exchange"]), (4, []),
                                          (2, ["--slots", "1", "--no-overlap", "--halo-mode", "exchange"]),
-                                         (2, ["--halo-select", "exchange"])])
+                                         (2, ["--halo-select", "exchange"]), (3, ["--halo-select", "overlap"]),
+                                         (2, ["--halo-select", "event"])])
 def test_bench_torchrun_rehearsal(world, extra):
     """bench.py under torch.distributed.run with `world` ranks sharing the one
-    GPU (gloo-host halos): the driver's N-GPU launch path, checked bit-exact."""
+    GPU (gloo-host halos): the driver's N-GPU launch path, checked bit-exact,
+    with every halo mode timed after the headline and 0 bytes different."""
     import json
     import subprocess
     import sys
@@ -91,21 +93,35 @@ def test_bench_torchrun_rehearsal(world, extra):
     meta = json.loads(lines[0])
     assert meta["n_gpus"] == world and meta["mismatches"] == 0
     assert meta["value"] > 0 and meta["config"]["parallelism"] == f"rowband{world}"
-    hx = meta["halo_exchange"]  # secondary run: ghost rows exchanged, one transport per slot
-    assert hx["status"] == "ok", hx
-    assert hx["mismatches_vs_headline"] == 0 and hx["exchanges_per_step"] >= 1
+    assert meta["runtime"]["hip_runtime_version"] > 0 and meta["runtime"]["hip_runtime_path"]
+    modes = meta["halo_modes"]
+    head = "event" if "--halo-mode" in extra else "preload"
+    assert set(modes) == {head, "slot_exchange", "event", "overlap"}, modes
+    for m, r in modes.items():
+        assert r["status"] == "ok", (m, r)
+        assert r["ms_per_step"] > 0
+        if m != head:
+            assert r["mismatches_vs_headline"] == 0 and r["exchanges_per_step"] >= 1, (m, r)
+    # overlap: a T-deep ghost zone, one exchange per fused launch (the reference's per-rep loop, T at a time)
+    assert modes["overlap"]["halo_depth"] == modes["overlap"]["fuse"]
+    assert modes["overlap"]["exchanges_per_step"] >= 40 // modes["overlap"]["fuse"]
     sel = meta["halo_select"]
-    if "--halo-select" in extra:  # forced adoption: the headline is K timed steps of the exchange pipeline
-        assert sel["mode"] == "exchange" and sel["preload_ms_per_step"] > 0
+    assert set(sel["candidates"]) == set(modes)
+    if "--halo-select" in extra:  # forced adoption: the headline is the K timed steps of that mode
+        want = extra[extra.index("--halo-select") + 1]
+        want = "slot_exchange" if want == "exchange" else want
+        assert sel["mode"] == want and meta["config"]["halo_mode"] == want
+        assert meta["ms_per_step"] == modes[want]["ms_per_step"]
         assert meta["headline_transport"] == "gloo-host" and meta["config"]["exchanges_per_step"] >= 1
         assert meta["config"]["preload_halo"] is False
-    elif "--halo-mode" not in extra:
-        assert sel["mode"] in ("preload", "exchange")
+        assert "loop_only" not in meta and "loop_only" in modes["preload"]
+    else:
+        assert sel["mode"] in modes
 
 
 def test_bench_exchange_watchdog():
-    """A peer that never joins the secondary halo_exchange measurement: the
-    watchdog still prints the headline line (exchange marked timed out) and
+    """A peer that never joins the secondary halo-mode measurement: the
+    watchdog still prints the headline line (the mode marked timed out) and
     every rank exits 0, so the driver's N-GPU run always yields its number."""
     import json
     import subprocess
@@ -124,7 +140,7 @@ def test_bench_exchange_watchdog():
     assert len(lines) == 1, r.stdout
     meta = json.loads(lines[0])
     assert meta["n_gpus"] == 2 and meta["value"] > 0
-    assert meta["halo_exchange"]["status"] == "watchdog timeout"
+    assert meta["halo_modes"]["slot_exchange"]["status"] == "watchdog timeout"
     assert meta["headline_transport"] == "none"
     assert time.time() - t0 < 250
 

@@ -99,13 +99,15 @@ def run_conv(args, timeout=120):
 
 def start_server(d):
     sock = os.path.join(d, "pconv.sock")
-    p = subprocess.Popen([CONV, "--serve", sock, "--device", "0", "--idle-timeout", "600"], stderr=subprocess.PIPE,
-                         text=True)
+    # stderr to a file, never an undrained pipe (a full pipe would block the server)
+    log = open(os.path.join(d, "pconv_serve.stderr"), "w+")
+    p = subprocess.Popen([CONV, "--serve", sock, "--device", "0", "--idle-timeout", "600"], stderr=log, text=True)
     for _ in range(1200):
         if os.path.exists(sock):
             return p, sock
         if p.poll() is not None:
-            raise RuntimeError(p.stderr.read())
+            log.seek(0)
+            raise RuntimeError(log.read()[-2000:])
         time.sleep(0.05)
     raise RuntimeError("server did not start")
 
