@@ -3,6 +3,7 @@
 // Buffers cross the boundary either as Python buffer-protocol objects (numpy
 // arrays, host memory) or as raw integer addresses (torch.Tensor.data_ptr()
 // of CUDA tensors or pinned host tensors) — no torch C++ ABI dependency.
+#include <omp.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -183,6 +184,14 @@ PYBIND11_MODULE(_pconv_native, m) {
       py::arg("filter") = "gaussian", py::arg("omp") = false, py::arg("threads") = 0);
   m.def("default_cpu_threads", &default_cpu_threads,
         "OpenMP team size used when none is set: affinity CPUs capped by the cgroup quota, minus one");
+  m.def(
+      "set_cpu_threads",
+      [](int n) {
+        omp_set_num_threads(std::max(1, n));
+        return omp_get_max_threads();
+      },
+      py::arg("n"), "OpenMP team size of this process's CPU stencil (returns the size now in effect)");
+  m.def("cpu_threads", []() { return omp_get_max_threads(); }, "OpenMP team size in effect");
   m.def("configure_cpu_threads", &configure_cpu_threads, py::arg("share") = 1,
         "Size the OpenMP team (unless OMP_NUM_THREADS is set) for `share` processes on this node");
   m.def(

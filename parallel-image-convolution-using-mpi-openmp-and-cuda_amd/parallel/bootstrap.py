@@ -163,3 +163,38 @@ def bind_to_device_numa(device: int) -> Optional[int]:
         return None
     os.sched_setaffinity(0, keep)
     return len(keep)
+
+
+def cpu_rank_slice(local_rank: int, local_world: int, allowed, budget: int) -> list:
+    """Disjoint CPU slice of one CPU rank of the MPI+OpenMP analog.
+
+    The node's CPU budget (the CPUs this process may use, capped by the
+    cgroup quota, one kept back for the launcher and the gloo threads) is
+    split evenly between the ranks of the node; rank r gets the r-th block.
+    More ranks than budget CPUs share (round-robin) rather than fail."""
+    cpus = sorted(allowed)[:max(1, int(budget))]
+    k = max(1, len(cpus) // max(1, int(local_world)))
+    lo = (int(local_rank) * k) % len(cpus)
+    return cpus[lo:lo + k]
+
+
+def bind_cpu_rank(local_rank: int, local_world: int) -> Optional[list]:
+    """Bind this CPU rank to its slice (``cpu_rank_slice``) BEFORE its
+    OpenMP team starts (team threads inherit the affinity of the thread that
+    creates them) and size torch's own pools to one thread, so that the ranks
+    of a node never run more busy threads than the node's CPU budget.
+
+    Why: with unbound teams of ``budget / n`` threads, spinning OpenMP
+    workers of n ranks plus torch and gloo threads exceed a CFS quota (the
+    GPU box grants 16 CPUs of a 256-CPU host) and the whole cgroup is
+    throttled for the rest of the 100 ms period — the hybrid table got slower
+    as ranks were added (reference: one team per rank,
+    open-mp/omp_convolution.c:292,297).  PCONV_CPU_BIND=0 disables."""
+    if os.environ.get("PCONV_CPU_BIND", "1") == "0" or not hasattr(os, "sched_setaffinity"):
+        return None
+    n = require_native()
+    budget = n.default_cpu_threads()
+    mine = cpu_rank_slice(local_rank, local_world, os.sched_getaffinity(0), budget)
+    os.sched_setaffinity(0, mine)
+    torch.set_num_threads(1)
+    return mine

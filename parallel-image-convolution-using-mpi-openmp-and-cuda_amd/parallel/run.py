@@ -62,6 +62,9 @@ def parse(argv: List[str]) -> argparse.Namespace:
     p.add_argument("--fuse", type=int, default=None, help="repetitions per kernel launch (default: auto)")
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--transport", choices=["rccl", "gloo-host"], default="rccl")
+    p.add_argument("--threads", type=int, default=0,
+                   help="--backend omp: OpenMP threads per rank (default: the rank's CPU slice, i.e. the node's "
+                        "CPU budget / ranks on the node)")
     p.add_argument("--exchange-halo", action="store_true", help="read owned rows only; ghost rows from neighbours")
     p.add_argument("--out", default=None)
     p.add_argument("--synthetic", type=int, default=None, metavar="SEED")
@@ -179,6 +182,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     try:
         if a.height < world:
             raise SystemExit(f"image has fewer rows ({a.height}) than ranks ({world})")
+        cpus = None
         if a.backend == "hip":
             device = ctx.local_rank % max(1, n.device_count())
             n.set_device(device)
@@ -186,8 +190,21 @@ def main(argv: Optional[List[str]] = None) -> int:
                 n.bind_to_device_numa(device)
             runner = _HipBand(a, rank, world, device)
         else:
-            if a.backend == "omp":  # the node's CPUs split between the ranks on it (MPI+OpenMP hybrid)
-                n.configure_cpu_threads(int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+            # the node's CPU budget split between the ranks on it (MPI+OpenMP
+            # hybrid): each rank bound to its own slice, its team = the slice
+            from .bootstrap import bind_cpu_rank
+
+            local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+            cpus = bind_cpu_rank(ctx.local_rank, local_world)
+            if a.backend == "omp":
+                # OMP_NUM_THREADS is not a user choice here: torch.distributed.run
+                # exports 1 to every worker of a multi-process launch
+                if a.threads:
+                    n.set_cpu_threads(a.threads)
+                elif cpus is not None:
+                    n.set_cpu_threads(len(cpus))
+                else:
+                    n.set_cpu_threads(max(1, n.default_cpu_threads() // local_world))
             runner = _CpuBand(a, rank, world, omp=a.backend == "omp")
         b = runner.band
         rb = a.width * _CH[a.channels]
@@ -264,6 +281,8 @@ def main(argv: Optional[List[str]] = None) -> int:
                     "fuse": int(runner.fuse), "transport": (a.transport if a.backend == "hip" else "gloo") if world > 1 else None,
                     "preload_halo": preload, "launches": launches, "exchanges": exchanges, "output": out_path,
                     "mismatches": mismatches,
+                    "rank0_cpus": len(cpus) if cpus is not None else None,
+                    "omp_threads": n.cpu_threads() if a.backend == "omp" else None,
                 }), flush=True)
         return 0 if not mismatches else 2
     finally:
