@@ -24,6 +24,7 @@
 #include "pconv/kernels.hpp"
 #include "pconv/raw_io.hpp"
 #include "pconv/rccl_comm.hpp"
+#include "pconv/selftest.hpp"
 #include "pconv/service.hpp"
 #include "pconv/trace.hpp"
 
@@ -704,6 +705,14 @@ int conv_main(int argc, char** argv) {
       std::fputs(help_text(prog).c_str(), stdout);
       return 0;
     }
+  if (args.size() >= 2 && args[1] == "--selftest") {
+    try {
+      return selftest_main(args);
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "%s: %s\n", prog.c_str(), e.what());
+      return EXIT_FAILURE;
+    }
+  }
   if (args.size() >= 2 && args[1] == "--serve") {
     try {
       return serve_main(parse_serve_args(args));

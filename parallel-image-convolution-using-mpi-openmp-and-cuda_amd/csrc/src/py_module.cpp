@@ -15,6 +15,7 @@
 #include "pconv/engine.hpp"
 #include "pconv/kernels.hpp"
 #include "pconv/partition.hpp"
+#include "pconv/selftest.hpp"
 #include "pconv/raw_io.hpp"
 #include "pconv/rccl_comm.hpp"
 #include "pconv/schedule.hpp"
@@ -639,6 +640,15 @@ PYBIND11_MODULE(_pconv_native, m) {
   });
   m.def("rccl_version", &rccl_version);
   m.def("rccl_loaded", &rccl_loaded, "True once librccl is mapped (loaded lazily on the first RCCL call)");
+  m.def("install_crash_handler", &install_crash_handler,
+        "print a native backtrace on SIGSEGV/SIGBUS/SIGILL/SIGFPE/SIGABRT, then chain to the previous handler");
+  m.def("rccl_capture_probe", &rccl_capture_probe, py::arg("op") = "sendrecv", py::arg("mode") = "relaxed",
+        py::arg("bytes") = 4096, py::arg("device") = 0, py::arg("launches") = 3,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("rccl_selftest_exchange", &rccl_selftest_exchange, py::arg("device") = 0,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("rccl_selftest_multicomm", &rccl_selftest_multicomm, py::arg("device") = 0, py::arg("slots") = 3,
+        py::arg("images") = 60, py::arg("timeout_s") = 60.0, py::call_guard<py::gil_scoped_release>());
   m.def("rccl_library_path", &rccl_library_path, "path of the mapped librccl ('' while none is mapped)");
   m.def(
       "runtime_info",

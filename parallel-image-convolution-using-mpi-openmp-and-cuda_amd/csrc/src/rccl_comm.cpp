@@ -5,10 +5,14 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <sstream>
 #include <thread>
+
+#include "pconv/selftest.hpp"
 
 namespace pconv {
 
@@ -191,6 +195,81 @@ void RcclTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream) {
     PCONV_RCCL_CHECK(rccl().Recv(row0 + b.rows * pitch, n, ncclUint8, b.down, comm, stream));  // ghost below
   }
   PCONV_RCCL_CHECK(rccl().GroupEnd());
+}
+
+std::string rccl_capture_probe(const std::string& op, const std::string& mode, int64_t bytes, int device,
+                               int launches) {
+  PCONV_CHECK(op == "sendrecv" || op == "allreduce", "rccl_capture_probe: op must be sendrecv or allreduce");
+  PCONV_CHECK(bytes >= 8 && bytes % 8 == 0, "rccl_capture_probe: bytes must be a positive multiple of 8");
+  hipStreamCaptureMode cm = hipStreamCaptureModeGlobal;
+  const bool capture = mode != "none";
+  if (mode == "thread_local")
+    cm = hipStreamCaptureModeThreadLocal;
+  else if (mode == "relaxed")
+    cm = hipStreamCaptureModeRelaxed;
+  else
+    PCONV_CHECK(mode == "global" || mode == "none", "rccl_capture_probe: mode must be global|thread_local|relaxed|none");
+  auto step = [&](const char* what) {
+    std::fprintf(stderr, "[rccl_capture_probe %s/%s] %s\n", op.c_str(), mode.c_str(), what);
+    std::fflush(stderr);
+  };
+  set_device(device);
+  step("communicator");
+  RcclComm comm(rccl_unique_id(), 0, 1, device);
+  auto c = static_cast<ncclComm_t>(comm.handle());
+  const size_t n = static_cast<size_t>(bytes);
+  DeviceBuffer a(n), b(n);
+  std::vector<uint8_t> pat(n), got(n);
+  for (size_t i = 0; i < n; ++i) pat[i] = static_cast<uint8_t>((i * 131 + 7) & 0x7f);  // no sum overflow
+  PCONV_HIP_CHECK(hipMemcpy(a.data(), pat.data(), n, hipMemcpyHostToDevice));
+  PCONV_HIP_CHECK(hipMemset(b.data(), 0, n));
+  Stream s = Stream::create(0);
+  auto enqueue = [&] {
+    if (op == "sendrecv") {
+      PCONV_RCCL_CHECK(rccl().GroupStart());
+      PCONV_RCCL_CHECK(rccl().Send(a.data(), n, ncclUint8, 0, c, s.get()));
+      PCONV_RCCL_CHECK(rccl().Recv(b.data(), n, ncclUint8, 0, c, s.get()));
+      PCONV_RCCL_CHECK(rccl().GroupEnd());
+    } else {
+      PCONV_RCCL_CHECK(rccl().AllReduce(a.data(), b.data(), n, ncclUint8, ncclSum, c, s.get()));
+    }
+  };
+  hipGraphExec_t ex = nullptr;
+  size_t nodes = 0;
+  if (capture) {
+    step("begin capture");
+    PCONV_HIP_CHECK(hipStreamBeginCapture(s.get(), cm));
+    step("enqueue under capture");
+    enqueue();
+    hipGraph_t g = nullptr;
+    step("end capture");
+    PCONV_HIP_CHECK(hipStreamEndCapture(s.get(), &g));
+    PCONV_HIP_CHECK(hipGraphGetNodes(g, nullptr, &nodes));
+    step("instantiate");
+    PCONV_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    PCONV_HIP_CHECK(hipGraphDestroy(g));
+  }
+  for (int i = 0; i < launches; ++i) {
+    PCONV_HIP_CHECK(hipMemsetAsync(b.data(), 0, n, s.get()));
+    step(capture ? "graph launch" : "direct enqueue");
+    if (capture)
+      PCONV_HIP_CHECK(hipGraphLaunch(ex, s.get()));
+    else
+      enqueue();
+    comm.wait(s.get(), 60.0);
+    PCONV_HIP_CHECK(hipMemcpy(got.data(), b.data(), n, hipMemcpyDeviceToHost));
+    int64_t bad = 0;
+    for (size_t k = 0; k < n; ++k) bad += got[k] != pat[k];
+    PCONV_CHECK(bad == 0, "rccl_capture_probe " + op + "/" + mode + ": " + std::to_string(bad) +
+                              " bytes differ after launch " + std::to_string(i));
+  }
+  if (ex) PCONV_HIP_CHECK(hipGraphExecDestroy(ex));
+  step("ok");
+  std::ostringstream os;
+  os << "{\"probe\": \"rccl_capture\", \"op\": \"" << op << "\", \"mode\": \"" << mode << "\", \"bytes\": " << bytes
+     << ", \"graph_nodes\": " << nodes << ", \"launches\": " << launches << ", \"status\": \"ok\", \"rccl_version\": \""
+     << rccl_version() << "\", \"rccl_path\": \"" << json_escape(rccl_library_path()) << "\"}";
+  return os.str();
 }
 
 }  // namespace pconv

@@ -331,3 +331,32 @@ def test_cli_copies_modes(pconv_mod, tmp_path, rng, copies):
     assert r.returncode == 0, r.stderr
     meta = json.loads(r.stdout.strip().splitlines()[-1])
     assert meta["copies"] == copies and meta["mismatches"] == 0
+
+
+# --------------------------------------------------------------------------
+# The RCCL self-tests on BOTH stacks: this (torch) process runs torch's bundled
+# HIP runtime and librccl; the `conv` CLI runs ROCm's own.  Each compares the
+# bytes RCCL delivered and the kernels consumed with the reflected-ghost model.
+
+def test_rccl_selftests_torch_stack(pconv_mod):
+    n = pconv_mod.native
+    ex = json.loads(n.rccl_selftest_exchange(0))
+    assert ex["status"] == "ok" and ex["cases"] >= 7 and ex["exchanges"] >= 14
+    # three communicators (one per slot stream) in flight together, 60 exchange images per case
+    mc = json.loads(n.rccl_selftest_multicomm(0, 3, 60, 60.0))
+    assert mc["status"] == "ok" and mc["communicators"] == 3 and mc["images_per_case"] == 60
+    info = n.runtime_info()
+    assert info["rccl_path"] and info["rccl_version"] == ex["rccl_version"]
+
+
+@pytest.mark.parametrize("name", ["rccl-exchange", "rccl-multicomm"])
+def test_rccl_selftests_cli_stack(name):
+    from conftest import CONV_BIN
+
+    r = subprocess.run([CONV_BIN, "--selftest", name, "--slots", "3", "--images", "60"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert lines[0]["status"] == "ok" and lines[-1]["status"] == "ok"
+    # the CLI binds ROCm's librccl / HIP runtime, not torch's copies
+    assert "torch" not in lines[0]["rccl_path"] and "torch" not in lines[-1]["hip_runtime_path"]

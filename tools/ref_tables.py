@@ -186,26 +186,35 @@ def cmd_mpi_cpu(a):
         a.cpus = pconv.native.default_cpu_threads() + 1
     ncpu = a.cpus
     for backend in a.backends.split(","):
-        for ch in ("grey", "rgb"):
-            for h in SIZES:
+        for ch in a.channels.split(","):
+            for h in ([int(x) for x in a.sizes.split(",")] if a.sizes else SIZES):
                 img = make_image(d, ch, h)
                 for n in [int(x) for x in a.ranks.split(",")]:
-                    threads = max(1, ncpu // n) if backend == "omp" else 1
-                    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS=str(threads))
+                    if a.unbound:  # round-2 policy (A/B): unbound ranks, team = CPUs // ranks
+                        threads = max(1, ncpu // n) if backend == "omp" else 1
+                        env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS=str(threads), PCONV_CPU_BIND="0")
+                        extra = ["--threads", str(threads)] if backend == "omp" else []
+                    else:  # the runner's own policy: disjoint CPU slices of the budget, team = slice
+                        threads = None
+                        env = dict(os.environ, PYTHONPATH=ROOT)
+                        extra = []
                     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                            "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "pconv.parallel.run",
                            img, "1920", str(h), "20", ch, "--backend", backend, "--json", "--quiet",
-                           "--out", os.path.join(d, f"out_{n}.raw")]
-                    loops = []
+                           "--out", os.path.join(d, f"out_{n}.raw")] + extra
+                    loops, meta = [], {}
                     for _ in range(a.runs):
                         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
                         if r.returncode != 0:
                             raise RuntimeError(r.stderr[-800:])
-                        loops.append(json.loads(r.stdout.strip().splitlines()[-1])["loop_s"])
+                        meta = json.loads(r.stdout.strip().splitlines()[-1])
+                        loops.append(meta["loop_s"])
                     loops.sort()
                     ref = (MPI_REF if backend == "cpu" else OMP_REF)[(ch, h)]
                     emit(a.out, {"table": "mpi-cpu", "backend": backend, "channels": ch, "height": h, "reps": 20,
-                                 "ranks": n, "omp_threads": threads, "loop_s": loops[len(loops) // 2],
+                                 "ranks": n, "omp_threads": meta.get("omp_threads", threads),
+                                 "rank0_cpus": meta.get("rank0_cpus"), "bound": not a.unbound,
+                                 "loop_s": loops[len(loops) // 2],
                                  "loop_all_s": loops, "ref_s": ref[NS.index(n)] if n in NS else None,
                                  "cpus": ncpu})
 
@@ -319,6 +328,10 @@ def main():
             s.add_argument("--backends", default="cpu,omp")
             s.add_argument("--ranks", default="1,2,4,9,16")
             s.add_argument("--cpus", type=int, default=0)
+            s.add_argument("--sizes", default=None, help="comma list of heights (default: all four)")
+            s.add_argument("--channels", default="grey,rgb")
+            s.add_argument("--unbound", action="store_true",
+                           help="A/B: the round-2 policy (no CPU binding, team = CPUs // ranks)")
     s = sub.add_parser("report")
     s.add_argument("inputs", nargs="+")
     s.add_argument("--md", default=None)
