@@ -122,7 +122,7 @@ def parse():
                         "moved GPU-to-GPU) with the same K steps, and compare their bytes with the headline "
                         "result; reported under 'halo_modes' (auto: on for N>1)")
     p.add_argument("--halo-modes", default=",".join(HALO_MODES),
-                   help="comma list of the halo modes timed after the headline at N>1: slot_exchange, event, overlap")
+                   help="comma list of the halo modes timed after the headline at N>1: " + ", ".join(HALO_MODES))
     p.add_argument("--exchange-timeout", type=float, default=60.0, help="seconds before a mode's drain aborts")
     p.add_argument("--halo-select", choices=["auto", "off", "exchange"] + list(HALO_MODES), default="auto",
                    help="N>1: report as the headline the fastest bit-exact halo mode when it is at least 3 %% faster "
@@ -179,7 +179,10 @@ def gather_floats(v: float):
 # steps, barriers and device syncs as the headline):
 #   slot_exchange: each image on its slot's own stream with its own
 #       communicator; one exchange of the whole ghost zone in stream order,
-#       then the repetitions as one cached graph (slots overlap each other);
+#       then the repetitions; with RCCL the whole image (upload, send/recv,
+#       launches, download) is ONE captured hipGraph (slots overlap each other);
+#   slot_exchange_direct: the same, issued directly (upload, the group's
+#       RCCL calls, the repetitions as a cached graph, download);
 #   event: one communicator, shared H2D / compute / D2H / comm streams; the
 #       whole ghost zone of image k+1 is exchanged on the comm stream while
 #       image k computes (event-ordered);
@@ -188,14 +191,15 @@ def gather_floats(v: float):
 #       exchange every fused launch on the comm stream, the interior launch
 #       concurrently on the compute stream, the edge strips after the halo
 #       event.
-HALO_MODES = ("slot_exchange", "event", "overlap")
+HALO_MODES = ("slot_exchange", "slot_exchange_direct", "event", "overlap")
 
 
 def mode_kwargs(a, mode: str, fuse: int) -> dict:
     kw = dict(preload_halo=False, slots=a.slots, variant=a.variant, fuse=a.fuse, overlap=not a.no_overlap,
               halo=a.halo, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent])
-    if mode == "slot_exchange":
+    if mode in ("slot_exchange", "slot_exchange_direct"):
         kw["slot_exchange"] = True
+        kw["graph_capture"] = mode == "slot_exchange"
     elif mode == "overlap":
         kw["halo"] = int(fuse)  # T-deep ghost zone: one exchange per fused launch
         kw["overlap"] = True
@@ -335,6 +339,7 @@ def main():
     from pconv.parallel.bootstrap import barrier, bind_to_device_numa, init_distributed, max_over_ranks, shutdown
     from pconv.parallel.dist_engine import DistributedBlur, preload_is_exchange_free
 
+    pconv.native.install_crash_handler()  # a native crash prints its C++ frames
     ctx = init_distributed("gloo")
     world = ctx.world
     if world != a.gpus:

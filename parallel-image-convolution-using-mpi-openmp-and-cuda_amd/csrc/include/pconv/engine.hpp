@@ -40,6 +40,10 @@ class HaloTransport {
   virtual ~HaloTransport() = default;
   virtual void exchange(BandEngine& e, int64_t depth, hipStream_t stream) = 0;
   virtual const char* name() const = 0;
+  // True when exchange() only enqueues stream-ordered device work (no host
+  // synchronisation), so it can be captured into a hipGraph: then a serving
+  // step that exchanges halos is still ONE graph launch (process_graph).
+  virtual bool capturable() const { return false; }
 };
 
 struct EngineOptions {
@@ -152,9 +156,11 @@ class BandEngine {
   // allowed), `reps` repetitions, D2H of the owned rows — as ONE cached
   // hipGraph launched on the compute stream: one host API call per image
   // instead of ~12 (copies, launches, events; tools/ubench/api_cost.hip).
-  // The schedule must need no halo exchange (single band, or pre-loaded
-  // ghost rows deep enough for all `reps`).  Host buffers must be pinned and
-  // stay valid; the graph is keyed on them.
+  // A schedule that exchanges halos is captured too when the transport is
+  // capturable (RCCL send/recv, D2D copies): when the ghost zone covers all
+  // `reps`, ONE exchange of the whole zone follows the upload; otherwise the
+  // plan's exchange phases are captured in place.  Host buffers must be
+  // pinned and stay valid; the graph is keyed on them.
   void process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps);
   // True when `reps` repetitions with / without pre-loaded ghost rows need no exchange.
   bool exchange_free(int reps, bool halo_preloaded) const;
@@ -203,6 +209,7 @@ class BandEngine {
     hipGraphExec_t exec = nullptr;
     int end_cur = 0;
     int launches = 0;
+    int exchanges = 0;
     bool zero_copy = false;
     bool packed = false;
   };
@@ -325,6 +332,7 @@ class NullTransport : public HaloTransport {
  public:
   void exchange(BandEngine&, int64_t, hipStream_t) override {}
   const char* name() const override { return "null (timing only)"; }
+  bool capturable() const override { return true; }
 };
 
 // Transport used by LocalCluster (neighbour engines live on the same device).
@@ -333,6 +341,7 @@ class LocalTransport : public HaloTransport {
   explicit LocalTransport(std::vector<BandEngine*> peers) : peers_(std::move(peers)) {}
   void exchange(BandEngine& e, int64_t depth, hipStream_t stream) override;
   const char* name() const override { return "local-d2d"; }
+  bool capturable() const override { return true; }
 
  private:
   std::vector<BandEngine*> peers_;

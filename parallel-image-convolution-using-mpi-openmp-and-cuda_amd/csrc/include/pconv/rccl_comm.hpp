@@ -72,6 +72,9 @@ class RcclTransport : public HaloTransport {
   explicit RcclTransport(std::shared_ptr<RcclComm> comm) : comm_(std::move(comm)) {}
   void exchange(BandEngine& e, int64_t depth, hipStream_t stream) override;
   const char* name() const override { return "rccl"; }
+  // ncclSend/ncclRecv in a group only enqueue kernels on `stream`: capturable
+  // (tests/test_gpu_halo.py and `conv --selftest rccl-capture`, both stacks).
+  bool capturable() const override { return true; }
   RcclComm& comm() { return *comm_; }
 
  private:

@@ -55,7 +55,9 @@ std::string rccl_selftest_exchange(int device);
 // BandPipeline, drive `images` exchange images (each slot's exchanges in its
 // own stream order, several communicators in flight at once); every image
 // compared with the oracle; each slot's drain bounded by `timeout_s` with RCCL
-// async-error polling.  JSON result; throws on mismatch or timeout.
+// async-error polling.  Every case runs twice: images issued directly, and
+// images captured as one hipGraph each (RCCL send/recv inside the capture).
+// JSON result; throws on mismatch or timeout.
 std::string rccl_selftest_multicomm(int device, int slots, int images, double timeout_s);
 
 // `conv --selftest {rccl-capture|rccl-exchange|rccl-multicomm|all} [options]`.

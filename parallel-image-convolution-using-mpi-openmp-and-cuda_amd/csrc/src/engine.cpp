@@ -372,9 +372,22 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
   TraceRange tr("pconv.step_graph");
   PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
   halo_valid_ = input_preloaded(in_r0, in_r1);
-  const std::vector<Phase> ph = plan(reps);
-  for (const auto& p : ph)
-    PCONV_CHECK(p.exchange_depth == 0, "process_graph: this schedule needs halo exchanges (pre-load deeper ghost rows)");
+  std::vector<Phase> ph = plan(reps);
+  bool exchanges = false;
+  for (const auto& p : ph) exchanges = exchanges || p.exchange_depth > 0;
+  // Exchange-mode image: one exchange of the whole ghost zone right after the
+  // upload when it covers every repetition, else the plan's exchange phases.
+  const bool zone_first = exchanges && reps > 0 && exchange_free(reps, true);
+  if (exchanges) {
+    PCONV_CHECK(transport_ != nullptr, "band has neighbours but no halo transport is attached");
+    PCONV_CHECK(transport_->capturable(),
+                std::string("process_graph: this schedule needs halo exchanges and the '") + transport_->name() +
+                    "' transport cannot be captured into a graph (pre-load deeper ghost rows or issue directly)");
+  }
+  if (zone_first) {
+    halo_valid_ = true;
+    ph = plan(reps);
+  }
   const auto key = std::make_tuple(reps, cur_, host_in, in_r0, in_r1, host_out);
   auto it = step_graphs_.find(key);
   stats_ = RunStats{};
@@ -399,6 +412,10 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     prepare(ph);  // tile-shape tuning cannot run inside the capture
     PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
     upload_rows(host_in, rb, in_r0, in_r1, cs_);
+    if (zone_first) {
+      transport_->exchange(*this, lay_.halo, cs_);  // stream order: after the upload, before the launches
+      ++stats_.exchanges;
+    }
     for (size_t i = 0; i + (zc || packed ? 1 : 0) < ph.size(); ++i) enqueue_phase(ph[i]);
     if (zc || packed) {
       launch(ph.back().launches[0], cs_, zc ? host_out : stage_.data(), rb);
@@ -417,10 +434,12 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     PCONV_HIP_CHECK(hipGraphDestroy(g));
     sg.end_cur = cur_;
     sg.launches = stats_.launches;
+    sg.exchanges = stats_.exchanges;
     it = step_graphs_.emplace(key, sg).first;
   } else {
     cur_ = it->second.end_cur;
     stats_.launches = it->second.launches;
+    stats_.exchanges = it->second.exchanges;
   }
   PCONV_HIP_CHECK(hipGraphLaunch(it->second.exec, cs_));
   halo_valid_ = false;

@@ -236,12 +236,15 @@ std::string rccl_selftest_multicomm(int device, int slots, int images, double ti
   // graph; halo < reps: exchange phases inside the run (stream-ordered).
   const Case cases[] = {{40, 40, 8}, {20, 8, 4}};
   int checked = 0;
+  // directly issued images, then images captured as ONE graph each (upload,
+  // RCCL exchange(s), launches, download: BandEngine::process_graph)
+  for (const bool captured : {false, true})
   for (const Case& c : cases) {
     EngineOptions o;
     o.device = device;
     o.halo_depth = c.halo;
     o.fuse = c.fuse;
-    BandPipeline pipe(g, self_band(y0, rows), f, o, slots, -1, /*slot_streams=*/true, /*step_graphs=*/false);
+    BandPipeline pipe(g, self_band(y0, rows), f, o, slots, -1, /*slot_streams=*/true, /*step_graphs=*/captured);
     std::vector<std::shared_ptr<RcclComm>> comms;
     for (int k = 0; k < slots; ++k) {
       comms.push_back(std::make_shared<RcclComm>(rccl_unique_id(), 0, 1, device));
@@ -283,7 +286,7 @@ std::string rccl_selftest_multicomm(int device, int slots, int images, double ti
   }
   std::ostringstream os;
   os << "{\"selftest\": \"rccl_multicomm\", \"communicators\": " << slots << ", \"images_per_case\": " << images
-     << ", \"cases\": " << checked << ", \"status\": \"ok\", \"rccl_version\": \"" << rccl_version()
+     << ", \"cases\": " << checked << ", \"captured_cases\": " << checked / 2 << ", \"status\": \"ok\", \"rccl_version\": \"" << rccl_version()
      << "\", \"rccl_path\": \"" << json_escape(rccl_library_path()) << "\"}";
   return os.str();
 }

@@ -91,8 +91,11 @@ class DistributedBlur:
         # exchange in stream order between upload and launches — slots overlap
         # each other instead of the exchange overlapping its own image.
         self.slot_exchange = bool(slot_exchange) and self.world > 1
-        if self.slot_exchange:
-            graph_capture = False
+        if self.slot_exchange and transport != "rccl":
+            graph_capture = False  # host-staged transports synchronise: they cannot be captured
+        # With RCCL, an exchange image is ONE captured graph (upload, ncclSend/
+        # ncclRecv of the ghost zone, launches, download): one host call per
+        # image instead of the transport's group calls + launches + copies.
         # split_d2h: each image's graph = H2D + repetitions on one of slots/2
         # compute streams (two engines alternate on each), its D2H on a shared
         # copy stream — exchange-free images only.

@@ -44,6 +44,7 @@ def pconv_mod():
     import pconv
 
     assert pconv.native_available(), "native extension not built (run __graft_entry__.build())"
+    pconv.native.install_crash_handler()  # a native crash prints its C++ frames before faulthandler's
     return pconv
 
 

@@ -3,7 +3,7 @@ CPU check of the oracle itself)."""
 import numpy as np
 
 
-def reflected_ghost_oracle(n, plan, halo, owned, y0, height, channels, filt="gaussian"):
+def reflected_ghost_oracle(n, plan, halo, owned, y0, height, channels, filt="gaussian", pre_exchange=0):
     """NumPy/CPU model of a band's `plan` on a self-neighbour band: before
     every exchange phase the ghost zone is refreshed with the band's own rows
     (above: rows [0, d); below: rows [rows - d, rows)), exactly what RCCL
@@ -20,9 +20,13 @@ def reflected_ghost_oracle(n, plan, halo, owned, y0, height, channels, filt="gau
 
     view(frames[0], 0, rows)[:] = owned
     cur = 0
-    for ph in plan:
+    # pre_exchange: an exchange of that depth before the plan (a pipeline's
+    # whole-zone exchange right after the upload)
+    for ph in [None] + list(plan):
+        if ph is None and not pre_exchange:
+            continue
         src, dst = frames[cur], frames[cur ^ 1]
-        d = ph.exchange_depth
+        d = pre_exchange if ph is None else ph.exchange_depth
         if d:
             top, bottom = view(src, 0, d).copy(), view(src, rows - d, rows).copy()
             view(src, -d, 0)[:] = top
@@ -32,6 +36,8 @@ def reflected_ghost_oracle(n, plan, halo, owned, y0, height, channels, filt="gau
             a, b = max(-d, -y0), min(rows + d, height - y0)
             view(src, -d, a)[:] = 0
             view(src, b, rows + d)[:] = 0
+        if ph is None:
+            continue
         for l in ph.launches:
             n.cpu_fused_launch(filt, channels, rb, rows, halo, src, dst, l.lo, l.hi, l.steps, y0, height, False)
         cur ^= 1

@@ -360,3 +360,51 @@ def test_rccl_selftests_cli_stack(name):
     assert lines[0]["status"] == "ok" and lines[-1]["status"] == "ok"
     # the CLI binds ROCm's librccl / HIP runtime, not torch's copies
     assert "torch" not in lines[0]["rccl_path"] and "torch" not in lines[-1]["hip_runtime_path"]
+
+
+@pytest.mark.parametrize("captured", [True, False])
+@pytest.mark.parametrize("reps,halo,fuse", [(40, 40, 8), (20, 8, 4), (13, 13, 4)])
+def test_slot_pipeline_rccl_exchange_images(pconv_mod, captured, reps, halo, fuse):
+    """Slot-exchange pipeline on a mid-image self-neighbour band, one 1-rank
+    communicator per slot stream (three in flight together): images issued
+    directly, or each captured as ONE hipGraph (upload, ncclSend/ncclRecv of
+    the ghost zone, launches, download — BandEngine::process_graph).  Every
+    image equals the reflected-ghost oracle."""
+    n = pconv_mod.native
+    w, height, y0, rows, slots = 301, 520, 211, 96, 3
+    pipe = n.BandPipeline(w, height, "rgb", "gaussian", 0, 1, 0, halo=halo, fuse=fuse, slots=slots, graphs=True,
+                          step_graphs=captured, band=_mid_band(n, y0, rows))
+    assert pipe.step_graphs == captured
+    comms = [n.RcclComm(n.rccl_unique_id(), 0, 1, 0) for _ in range(slots)]
+    for k, c in enumerate(comms):
+        pipe.attach_slot_rccl(k, c)
+    e0 = pipe.slot(0)
+    zone = e0.exchange_free(reps, True)
+    e0.set_halo_valid(zone)
+    plan = e0.plan(reps)
+    e0.set_halo_valid(False)
+    rb = e0.row_bytes
+    rng = np.random.default_rng(reps * 100 + halo)
+    ins = [n.PinnedBuffer(rows * rb) for _ in range(slots)]
+    outs = [n.PinnedBuffer(rows * rb) for _ in range(slots)]
+    refs = []
+    for k in range(slots):
+        owned = rng.integers(0, 256, size=(rows, rb), dtype=np.uint8)
+        np.asarray(ins[k])[:] = owned.reshape(-1)
+        refs.append(reflected_ghost_oracle(n, plan, e0.halo, owned, y0, height, "rgb",
+                                           pre_exchange=e0.halo if zone else 0))
+    for rnd in range(4):
+        for k in range(slots):
+            np.asarray(outs[k])[:] = 0
+            pipe.submit(ins[k].ptr, 0, rows, outs[k].ptr, reps)
+        for k, c in enumerate(comms):
+            c.wait(pipe.slot(k).compute_stream, 60.0)
+        pipe.drain()
+        for k in range(slots):
+            got = np.asarray(outs[k]).reshape(rows, rb)
+            bad = int(np.count_nonzero(got != refs[k]))
+            assert bad == 0, (rnd, k, bad)
+    st = pipe.slot(0).stats
+    assert st.exchanges == (1 if zone else len([p for p in plan if p.exchange_depth]))
+    if captured:
+        assert pipe.slot(0).cached_step_graphs >= 1
