@@ -51,6 +51,7 @@ enum class KernelVariant : int {
   Int9 = 3,      // generic int-exact 9-tap
   Float9 = 4,    // generic float32 9-tap (reference rounding)
   TemporalPk = 5,  // packed-u16 (VOP3P) fused gaussian, kept for A/B measurements
+  FloatTemporal = 6,  // any 3x3 filter, float32 reference rounding, `steps` fused in registers
 };
 
 const char* kernel_variant_name(KernelVariant v);
@@ -67,6 +68,10 @@ void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a, hipStr
 void prepare_stencil(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream,
                      KernelVariant v = KernelVariant::Auto);
 
+// `steps` repetitions of ANY 3x3 filter in the reference's float32 semantics
+// in one launch (kernels/stencil_float.hip): box/9, edge/28, custom filters.
+void launch_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream);
+
 // Whether `v` (or Auto) can fuse `steps` > 1 for this filter.
 bool supports_fusion(const Filter& f, KernelVariant v);
 
@@ -76,7 +81,7 @@ bool supports_fusion(const Filter& f, KernelVariant v);
 // boxes, 16384^2 30.6 vs 32.2; profiles/r02/tile_shapes.md,
 // prefetch_kernel.md); 8 everywhere else (RGB's 3x wider horizontal halo makes
 // deeper fusion slower; 1920x2520 RGB 3.5 us/rep at 8 vs 4.0 at 6, 8192^2 RGB
-// within 2 % either way).
+// within 2 % either way).  Other filters (float temporal kernel): 4.
 int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes, int channels = 0);
 
 // Row copy by the CUs: `rows` rows of `row_bytes` from src (row pitch sp) to

@@ -467,17 +467,21 @@ const char* kernel_variant_name(KernelVariant v) {
     case KernelVariant::Int9: return "int9";
     case KernelVariant::Float9: return "float9";
     case KernelVariant::TemporalPk: return "temporal_pk";
+    case KernelVariant::FloatTemporal: return "float_temporal";
   }
   return "?";
 }
 
 bool supports_fusion(const Filter& f, KernelVariant v) {
-  return f.binomial121 &&
-         (v == KernelVariant::Auto || v == KernelVariant::Temporal || v == KernelVariant::TemporalPk);
+  if (f.binomial121)
+    return v == KernelVariant::Auto || v == KernelVariant::Temporal || v == KernelVariant::TemporalPk;
+  // any other filter: the float temporal kernel (reference float32 semantics)
+  return v == KernelVariant::Auto || v == KernelVariant::FloatTemporal;
 }
 
 int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes, int channels) {
   if (!supports_fusion(f, v)) return 1;
+  if (!f.binomial121) return 4;  // float temporal kernel: ALU-bound, a shallow trapezoid
   // Grey frames far beyond the Infinity Cache: 12 repetitions per launch
   // measured 2-6 % faster than 8 in every run (32768^2: 113.2-116.2 vs
   // 116.9-121.1 us/rep over four boxes; 16384^2: 30.6 vs 32.2;
@@ -518,7 +522,13 @@ void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hip
   const bool own_dst_pitch = a.dst_pitch != 0 && a.dst_pitch != a.pitch;
   if (v == KernelVariant::Auto)
     v = f.binomial121 ? (a.steps > 1 || own_dst_pitch ? KernelVariant::Temporal : KernelVariant::Binomial)
-                      : (f.int_exact ? KernelVariant::Int9 : KernelVariant::Float9);
+                      : (a.steps > 1 ? KernelVariant::FloatTemporal
+                                     : (f.int_exact ? KernelVariant::Int9 : KernelVariant::Float9));
+  if (v == KernelVariant::FloatTemporal) {
+    launch_float_temporal(f, ch, a, stream);
+    PCONV_HIP_CHECK(hipGetLastError());
+    return;
+  }
   PCONV_CHECK(!own_dst_pitch || (v == KernelVariant::Temporal && a.dst_pitch >= a.row_bytes && a.dst_pitch % 4 == 0),
               "launch_stencil: a separate destination pitch needs the SWAR temporal kernel");
   PCONV_CHECK(a.steps == 1 || v == KernelVariant::Temporal || v == KernelVariant::TemporalPk,

@@ -1,0 +1,240 @@
+// Temporal-blocked kernel for ANY 3x3 filter in the reference's float32
+// semantics (box/9 and "edge_detection"/28 of mpi/mpi_convolution.c:90-100,
+// custom filters): `steps` repetitions per launch, the tile resident in
+// registers between steps — one HBM/Infinity-Cache round trip per launch
+// instead of per repetition (k_generic9 in stencil.hip, one launch per rep).
+//
+// Numerics, per output byte and step, exactly the reference's
+// (mpi/mpi_convolution.c:303-307):
+//   acc = 0; for k in 0..2, l in 0..2: acc = fl(acc + fl(p[k][l] * w[k*3+l]))
+//   out = trunc(acc) clamped to [0, 255]
+// separate multiply and add (no contraction: the TU is built with
+// -ffp-contract=off and the arithmetic goes through __fmul_rn/__fadd_rn),
+// row-major tap order, truncation after EVERY step, zero outside the image at
+// every step.  UNIFORM filters (all nine weights equal, e.g. box) compute each
+// input byte's product once per row instead of once per tap: fl(p * w) does
+// not depend on the tap, so the chain of additions is unchanged.
+//
+// Tile: NW waves stacked vertically, wave w keeps M rows x 8 bytes per lane
+// (a 512-byte strip per wave row) as packed bytes.  Horizontal neighbours at
+// distance CH (<= 4) come from the adjacent lanes by DPP wave_shr / wave_shl;
+// vertical neighbours across waves through LDS (double-buffered by step
+// parity, one barrier per step).  The tile's halo (`steps` rows, ceil(steps *
+// CH / 8) lanes per side) absorbs what enters from outside the tile.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "pconv/kernels.hpp"
+
+namespace pconv {
+namespace {
+
+using u32 = uint32_t;
+
+struct FloatTaps {
+  float w[9];
+};
+
+__device__ __forceinline__ float ub(u32 x, int k) { return static_cast<float>((x >> (8 * k)) & 0xffu); }
+
+// Row (8 bytes per lane) -> floats of bytes [-CH, 8 + CH) (times w when UNIFORM).
+template <int CH, bool UNIFORM>
+__device__ __forceinline__ void expand(const u32 (&X)[2], float w, float (&e)[8 + 2 * CH]) {
+  const u32 l = __builtin_amdgcn_mov_dpp(X[1], 0x138, 0xf, 0xf, true);  // wave_shr:1 -> left lane's bytes 4..7
+  const u32 r = __builtin_amdgcn_mov_dpp(X[0], 0x130, 0xf, 0xf, true);  // wave_shl:1 -> right lane's bytes 0..3
+#pragma unroll
+  for (int j = 0; j < CH; ++j) e[j] = ub(l, 4 - CH + j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[CH + j] = ub(X[j >> 2], j & 3);
+#pragma unroll
+  for (int j = 0; j < CH; ++j) e[CH + 8 + j] = ub(r, j);
+  if constexpr (UNIFORM) {
+#pragma unroll
+    for (int j = 0; j < 8 + 2 * CH; ++j) e[j] = __fmul_rn(e[j], w);
+  }
+}
+
+template <int CH, bool UNIFORM>
+__device__ __forceinline__ u32 out_byte(const float (&a)[8 + 2 * CH], const float (&b)[8 + 2 * CH],
+                                        const float (&c)[8 + 2 * CH], int j, const FloatTaps& tp) {
+  // reference order: row k (a: above, b: this row, c: below), then column l
+  float acc;
+  if constexpr (UNIFORM) {
+    acc = a[j];  // 0 + fl(p*w) is exact
+    acc = __fadd_rn(acc, a[j + CH]);
+    acc = __fadd_rn(acc, a[j + 2 * CH]);
+    acc = __fadd_rn(acc, b[j]);
+    acc = __fadd_rn(acc, b[j + CH]);
+    acc = __fadd_rn(acc, b[j + 2 * CH]);
+    acc = __fadd_rn(acc, c[j]);
+    acc = __fadd_rn(acc, c[j + CH]);
+    acc = __fadd_rn(acc, c[j + 2 * CH]);
+  } else {
+    acc = __fmul_rn(a[j], tp.w[0]);
+    acc = __fadd_rn(acc, __fmul_rn(a[j + CH], tp.w[1]));
+    acc = __fadd_rn(acc, __fmul_rn(a[j + 2 * CH], tp.w[2]));
+    acc = __fadd_rn(acc, __fmul_rn(b[j], tp.w[3]));
+    acc = __fadd_rn(acc, __fmul_rn(b[j + CH], tp.w[4]));
+    acc = __fadd_rn(acc, __fmul_rn(b[j + 2 * CH], tp.w[5]));
+    acc = __fadd_rn(acc, __fmul_rn(c[j], tp.w[6]));
+    acc = __fadd_rn(acc, __fmul_rn(c[j + CH], tp.w[7]));
+    acc = __fadd_rn(acc, __fmul_rn(c[j + 2 * CH], tp.w[8]));
+  }
+  return acc > 0.0f ? (acc >= 255.0f ? 255u : static_cast<u32>(acc)) : 0u;
+}
+
+template <int CH, bool UNIFORM, int M, int NW>
+__global__ __launch_bounds__(64 * NW) void k_float_temporal(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                            int64_t pitch, int row_bytes, int r0, int r1, int steps,
+                                                            int g_row0, int height, FloatTaps tp) {
+  __shared__ uint2 lds[2][NW][2][64];  // [parity][wave][top/bottom][lane]
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hl = (steps * CH + 7) >> 3;  // halo lanes per side
+  const int vlanes = 64 - 2 * hl;
+  const int chunk = static_cast<int>(blockIdx.x) * vlanes - hl + lane;  // 8-byte column chunk of this lane
+  const int x = chunk * 8;
+  const int nchunks = (row_bytes + 7) >> 3;
+  const bool col_in = chunk >= 0 && chunk < nchunks;
+  const int vrows = NW * M - 2 * steps;
+  const int tile_r0 = r0 + static_cast<int>(blockIdx.y) * vrows;
+  const int row_base = tile_r0 - steps + w * M;
+  const float w0 = tp.w[0];
+
+  // bytes of this lane inside the image row (0..8)
+  const int valid = col_in ? min(row_bytes - x, 8) : 0;
+  const u32 m0 = valid >= 4 ? 0xffffffffu : (valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u));
+  const u32 m1 = valid >= 8 ? 0xffffffffu : (valid <= 4 ? 0u : ((1u << (8 * (valid - 4))) - 1u));
+  const bool edge_strip = blockIdx.x == 0 || static_cast<int>(blockIdx.x) * vlanes - hl + 64 >= nchunks;
+
+  u32 D[M][2];
+  const int lo_ok = max(r0 - steps, -g_row0), hi_ok = min(r1 + steps, height - g_row0);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const int fr = row_base + i;
+    uint2 v = make_uint2(0, 0);
+    if (col_in && fr >= lo_ok && fr < hi_ok) {
+      // 8-byte aligned (pitch % 16 == 0, data column 0 is 16-byte aligned); the
+      // partial last chunk reads into the zero pad columns of the frame row
+      v = *reinterpret_cast<const uint2*>(src + static_cast<int64_t>(fr) * pitch + x);
+    }
+    D[i][0] = v.x & m0;
+    D[i][1] = v.y & m1;
+  }
+  const int out_top = min(max(-g_row0 - row_base, 0), M);
+  const int out_bot = min(max(height - g_row0 - row_base, 0), M);
+
+  for (int s = 0; s < steps; ++s) {
+    const int par = s & 1;
+    lds[par][w][0][lane] = make_uint2(D[0][0], D[0][1]);
+    lds[par][w][1][lane] = make_uint2(D[M - 1][0], D[M - 1][1]);
+    __syncthreads();
+    u32 A[2], B[2];
+    {
+      const int wa = w > 0 ? w - 1 : 0;
+      const int wb = w < NW - 1 ? w + 1 : w;
+      const uint2 a = lds[par][wa][1][lane], b = lds[par][wb][0][lane];
+      A[0] = a.x;
+      A[1] = a.y;
+      B[0] = b.x;
+      B[1] = b.y;
+    }
+    float ea[8 + 2 * CH], eb[8 + 2 * CH], ec[8 + 2 * CH];
+    expand<CH, UNIFORM>(A, w0, ea);
+    expand<CH, UNIFORM>(D[0], w0, eb);
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      if (i + 1 < M)
+        expand<CH, UNIFORM>(D[i + 1], w0, ec);
+      else
+        expand<CH, UNIFORM>(B, w0, ec);
+      u32 o0 = 0, o1 = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o0 |= out_byte<CH, UNIFORM>(ea, eb, ec, j, tp) << (8 * j);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o1 |= out_byte<CH, UNIFORM>(ea, eb, ec, 4 + j, tp) << (8 * j);
+      D[i][0] = o0;
+      D[i][1] = o1;
+#pragma unroll
+      for (int j = 0; j < 8 + 2 * CH; ++j) {
+        ea[j] = eb[j];
+        eb[j] = ec[j];
+      }
+    }
+    if (edge_strip) {
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        D[i][0] &= m0;
+        D[i][1] &= m1;
+      }
+    }
+    if (out_top > 0 || out_bot < M) {
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+        if (i < out_top || i >= out_bot) {
+          D[i][0] = 0;
+          D[i][1] = 0;
+        }
+    }
+  }
+
+  const bool lane_ok = col_in && lane >= hl && lane < 64 - hl;
+  const int st_lo = max(tile_r0, r0), st_hi = min(min(tile_r0 + vrows, r1), height - g_row0);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const int fr = row_base + i;
+    if (lane_ok && fr >= st_lo && fr < st_hi) {
+      uint8_t* q = dst + static_cast<int64_t>(fr) * pitch + x;
+      if (valid == 8) {
+        *reinterpret_cast<uint2*>(q) = make_uint2(D[i][0], D[i][1]);
+      } else {  // partial last chunk: never write past the row's last byte
+        for (int b = 0; b < valid; ++b) q[b] = static_cast<uint8_t>(D[i][b >> 2] >> (8 * (b & 3)));
+      }
+    }
+  }
+}
+
+template <int CH, bool UNIFORM>
+void launch_ft(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s) {
+  constexpr int M = 8, NW = 8;
+  const int steps = a.steps;
+  const int hl = (steps * CH + 7) / 8;
+  const int vlanes = 64 - 2 * hl;
+  const int vrows = M * NW - 2 * steps;
+  PCONV_CHECK(vlanes > 0 && vrows > 0, "float temporal kernel: steps too large for the tile");
+  const int nchunks = static_cast<int>(ceil_div<int64_t>(a.row_bytes, 8));
+  const dim3 grid(ceil_div(nchunks, vlanes), ceil_div(static_cast<int>(a.r1 - a.r0), vrows));
+  k_float_temporal<CH, UNIFORM, M, NW><<<grid, dim3(64 * NW), 0, s>>>(
+      a.src, a.dst, a.pitch, static_cast<int>(a.row_bytes), static_cast<int>(a.r0), static_cast<int>(a.r1), steps,
+      static_cast<int>(a.g_row0), static_cast<int>(std::min<int64_t>(a.height, int64_t(1) << 30)), tp);
+}
+
+template <int CH>
+void launch_ft_ch(const Filter& f, const StencilLaunch& a, hipStream_t s) {
+  FloatTaps tp;
+  bool uniform = true;
+  for (int i = 0; i < 9; ++i) {
+    tp.w[i] = f.weights[i];
+    uniform = uniform && f.weights[i] == f.weights[0];
+  }
+  if (uniform)
+    launch_ft<CH, true>(a, tp, s);
+  else
+    launch_ft<CH, false>(a, tp, s);
+}
+
+}  // namespace
+
+void launch_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream) {
+  PCONV_CHECK(a.steps >= 1 && a.steps <= kMaxFusedSteps, "float temporal kernel: steps out of range");
+  PCONV_CHECK(a.dst_pitch == 0 || a.dst_pitch == a.pitch, "float temporal kernel: no separate destination pitch");
+  PCONV_CHECK(a.height < (int64_t(1) << 30) && a.g_row0 < (int64_t(1) << 30), "float temporal kernel: rows exceed 2^30");
+  switch (ch) {
+    case Channels::Grey: launch_ft_ch<1>(f, a, stream); break;
+    case Channels::Rgb: launch_ft_ch<3>(f, a, stream); break;
+    case Channels::Rgba: launch_ft_ch<4>(f, a, stream); break;
+  }
+}
+
+}  // namespace pconv

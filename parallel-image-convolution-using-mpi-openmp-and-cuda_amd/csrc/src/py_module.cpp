@@ -59,6 +59,7 @@ KernelVariant parse_variant(const std::string& s) {
   if (s == "temporal_pk") return KernelVariant::TemporalPk;
   if (s == "int9") return KernelVariant::Int9;
   if (s == "float9") return KernelVariant::Float9;
+  if (s == "float_temporal") return KernelVariant::FloatTemporal;
   PCONV_FAIL("unknown kernel variant '" + s + "'");
 }
 

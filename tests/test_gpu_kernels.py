@@ -97,7 +97,7 @@ def test_shape_guard_rejects_out_of_frame(native):
                               lay["pitch"], 64, -1, 8, -1, 9, 1, 100, 1 << 40, 0, "auto")
 
 
-def _run_fused(native, img, steps, r0, r1, halo, g_row0, height, variant="auto"):
+def _run_fused(native, img, steps, r0, r1, halo, g_row0, height, variant="auto", filt="gaussian"):
     """Run one fused launch on a band frame whose row 0 is global row g_row0;
     returns (gpu_rows, cpu_rows) of the whole frame's data columns."""
     import torch
@@ -115,7 +115,7 @@ def _run_fused(native, img, steps, r0, r1, halo, g_row0, height, variant="auto")
             full[halo + fr, 16 : 16 + row_bytes] = rng.integers(0, 256, row_bytes, dtype=np.uint8)
     src[GUARD : GUARD + lay["bytes"]] = torch.from_numpy(full.reshape(-1)).cuda()
     base = lay["pitch"] * halo + 16
-    native.launch_stencil("gaussian", ch, src.data_ptr() + GUARD + base, dst.data_ptr() + GUARD + base,
+    native.launch_stencil(filt, ch, src.data_ptr() + GUARD + base, dst.data_ptr() + GUARD + base,
                           lay["pitch"], row_bytes, r0, r1, -halo, h + halo, steps, g_row0, height,
                           torch.cuda.current_stream().cuda_stream, variant)
     torch.cuda.synchronize()
@@ -123,7 +123,7 @@ def _run_fused(native, img, steps, r0, r1, halo, g_row0, height, variant="auto")
     assert (d[:GUARD] == CANARY).all() and (d[-GUARD:] == CANARY).all(), "write outside the frame"
     gpu = d[GUARD:-GUARD].reshape(h + 2 * halo, lay["pitch"])
     cpu = np.zeros(lay["bytes"], np.uint8)
-    native.cpu_fused_launch("gaussian", ch, row_bytes, h, halo, full.reshape(-1), cpu, r0, r1, steps, g_row0, height)
+    native.cpu_fused_launch(filt, ch, row_bytes, h, halo, full.reshape(-1), cpu, r0, r1, steps, g_row0, height)
     return gpu, cpu.reshape(h + 2 * halo, lay["pitch"])
 
 
@@ -138,13 +138,53 @@ def test_temporal_matches_fused_reference(native, rng, channels, steps, variant)
         assert np.array_equal(gpu, cpu), (h, w, steps)
 
 
+def _custom_filter(native):
+    # asymmetric, non-uniform, one negative tap: exercises the tap order and the clamp at 0
+    return native.Filter.custom([3, 1, 0, 2, 5, 1, -1, 2, 4], 17, "custom")
+
+
+FLOAT_FILTERS = ["box", "edge", "custom"]
+
+
+@pytest.mark.parametrize("filt", FLOAT_FILTERS)
+@pytest.mark.parametrize("channels", ["grey", "rgb", "rgba"])
+@pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 8, 11, 16])
+def test_float_temporal_matches_fused_reference(native, rng, filt, channels, steps):
+    """Any 3x3 filter in the reference's float32 semantics (mul then add, row-
+    major tap order, truncation every step), `steps` per launch: byte for byte
+    the CPU twin of a fused launch (mpi/mpi_convolution.c:90-100,303-307),
+    guard-band canaries and pad columns untouched (checked by _run_fused)."""
+    f = _custom_filter(native) if filt == "custom" else filt
+    c = CH[channels]
+    for (h, w) in [(1, 3), (7, 5), (40, 33), (97, 130), (150, 700), (33, 1500)]:
+        img = rng.integers(0, 256, size=(h, w, c) if c > 1 else (h, w), dtype=np.uint8)
+        gpu, cpu = _run_fused(native, img, steps, 0, h, steps, 0, h, variant="float_temporal", filt=f)
+        assert np.array_equal(gpu, cpu), (filt, h, w, steps)
+
+
+@pytest.mark.parametrize("filt", FLOAT_FILTERS)
+@pytest.mark.parametrize("steps", [2, 4, 8, 16])
+def test_float_temporal_band_regions(native, filt, steps):
+    f = _custom_filter(native) if filt == "custom" else filt
+    _band_regions(native, steps, "float_temporal", f)
+
+
+def test_float_temporal_equals_repeated_single_steps(pconv_mod, rng):
+    """A fused float launch of T steps == T reference single steps (NumPy float32 oracle)."""
+    img = rng.integers(0, 256, size=(123, 211, 3), dtype=np.uint8)
+    for f in ("box", "edge"):
+        for t in (2, 5, 13):
+            got = _run_kernel(pconv_mod.native, img, f, "float_temporal", steps=t)
+            assert np.array_equal(got, pconv_mod.numpy_convolve(img, t, f)), (f, t)
+
+
 @pytest.mark.parametrize("steps", [2, 4, 8, 16])
 def test_temporal_band_regions(native, rng, steps):
     _band_regions(native, steps, "temporal")
     _band_regions(native, steps, "temporal_pk")
 
 
-def _band_regions(native, steps, variant):
+def _band_regions(native, steps, variant, filt="gaussian"):
     """Bands in the middle / at the edges of a taller image, regions reaching
     into ghost rows (what the distributed schedule asks for)."""
     H = 300
@@ -155,7 +195,7 @@ def _band_regions(native, steps, variant):
         for (r0, r1) in [(0, h), (-(halo - steps), h + (halo - steps)), (steps, h - steps), (-3, 5), (h - 2, h + 1)]:
             if r0 - steps < -halo or r1 + steps > h + halo or r0 >= r1:
                 continue
-            gpu, cpu = _run_fused(native, img, steps, r0, r1, halo, g_row0, H, variant=variant)
+            gpu, cpu = _run_fused(native, img, steps, r0, r1, halo, g_row0, H, variant=variant, filt=filt)
             fr0, fr1 = halo + r0, halo + r1
             assert np.array_equal(gpu[fr0:fr1], cpu[fr0:fr1]), (variant, g_row0, r0, r1, steps)
             # nothing written outside [r0, r1)
