@@ -114,6 +114,10 @@ def parse():
     p.add_argument("--emulate", default=None, metavar="WORLD:RANK",
                    help="time ONE rank of a WORLD-way split on this GPU (pre-loaded halos, no peers): a "
                         "single-GPU proxy of the per-rank step; reported as emulated, never as the headline")
+    p.add_argument("--emulate-halo", default="preload", choices=("preload",) + HALO_MODES,
+                   help="with --emulate: the halo mode of the emulated rank; an exchange mode replaces the rank's "
+                        "neighbours by itself (1-rank RCCL communicator, send/recv to self: real exchange costs, "
+                        "ghost contents not checked)")
     p.add_argument("--emulate-rccl", action="store_true",
                    help="with --emulate: also hold a 1-rank RCCL communicator during the timed region (its "
                         "streams and queues, as a real N>1 rank has)")
@@ -360,19 +364,29 @@ def main():
             raise SystemExit("--emulate runs in a single process")
         world, rank = (int(v) for v in a.emulate.split(":"))
         a.preload_halo, transport, head_transport = True, "none", "none"
+        if a.emulate_halo != "preload":
+            a.preload_halo, transport, head_transport = False, "rccl", "rccl"
     device = ctx.local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     # host thread + first-touch pinned buffers on the GPU's own socket
     cpu_bind = bind_to_device_numa(device)
 
-    blur = DistributedBlur(a.width, a.height, a.channels, a.filter, a.reps, rank=rank, world=world,
-                           device=device, halo=a.halo, fuse=a.fuse, overlap=not a.no_overlap,
-                           preload_halo=a.preload_halo, slots=a.slots, variant=a.variant,
-                           transport=head_transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
-                           step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
-                           zero_copy_out=a.zero_copy_out == "on", graph_capture=a.graph_capture == "on",
-                           split_d2h=a.pipeline == "split", packed_out=a.packed_d2h == "on",
-                           kernel_d2h=a.d2h == "kernel")
+    if a.emulate and a.emulate_halo != "preload":
+        fuse0 = a.fuse if a.fuse is not None else DistributedBlur(
+            a.width, a.height, a.channels, a.filter, a.reps, rank=rank, world=world, device=device,
+            preload_halo=True, slots=1, transport="none").engine.fuse
+        blur = DistributedBlur(a.width, a.height, a.channels, a.filter, a.reps, rank=rank, world=world,
+                               device=device, transport="rccl", self_neighbours=True,
+                               **mode_kwargs(a, a.emulate_halo, fuse0))
+    else:
+        blur = DistributedBlur(a.width, a.height, a.channels, a.filter, a.reps, rank=rank, world=world,
+                               device=device, halo=a.halo, fuse=a.fuse, overlap=not a.no_overlap,
+                               preload_halo=a.preload_halo, slots=a.slots, variant=a.variant,
+                               transport=head_transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
+                               step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
+                               zero_copy_out=a.zero_copy_out == "on", graph_capture=a.graph_capture == "on",
+                               split_d2h=a.pipeline == "split", packed_out=a.packed_d2h == "on",
+                               kernel_d2h=a.d2h == "kernel")
     blur.load_synthetic(a.seed)
     # --emulate-rccl: hold a (1-rank) RCCL communicator through the timed
     # region, as every real N>1 rank of the exchange path does.
@@ -515,6 +529,10 @@ def main():
         if a.emulate:
             out["emulated"] = f"rank {rank} of a {a.emulate.split(':')[0]}-way split on one GPU; value = this " \
                               "rank's step rate x full-image pixels (proxy, not a multi-GPU measurement)"
+            out["config"]["halo_mode"] = a.emulate_halo
+            if a.emulate_halo != "preload":
+                out["emulated"] += "; halos exchanged with the rank itself (RCCL send/recv to self): real " \
+                                   "exchange costs, ghost contents not those of its neighbours"
 
     import threading
 

@@ -59,7 +59,7 @@ class DistributedBlur:
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
                  step_graphs: Optional[bool] = None, zero_copy_out: bool = False, graph_capture: bool = True,
                  slot_exchange: bool = False, split_d2h: bool = False, packed_out: bool = False,
-                 kernel_d2h: bool = False):
+                 kernel_d2h: bool = False, self_neighbours: bool = False):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -74,6 +74,17 @@ class DistributedBlur:
             halo = auto_halo(self.height, self.world, reps, fuse, preload=bool(preload_halo) and not slot_exchange)
         kw = dict(halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant, slots=int(slots),
                   concurrent=int(concurrent))
+        if self_neighbours:
+            # One-GPU emulation of rank `rank` of a `world`-way split whose halos
+            # really move: its neighbours are replaced by itself (a 1-rank
+            # communicator, RCCL send/recv to self), so every exchange costs
+            # what it costs (kernels, latency, host calls) while the ghost
+            # CONTENT is not its neighbours' (timing only; bytes not checked).
+            b = n.row_band(self.height, self.world, self.rank)
+            b.up = 0 if b.up >= 0 else -1
+            b.down = 0 if b.down >= 0 else -1
+            b.rank, b.world = 0, 1
+            kw["band"] = b
         self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device, **kw)
         self.preload_halo = bool(preload_halo) and self.world > 1
         # Whole-step graphs (one host call per image, slots on their own
