@@ -9,7 +9,7 @@
 //   acc = 0; for k in 0..2, l in 0..2: acc = fl(acc + fl(p[k][l] * w[k*3+l]))
 //   out = trunc(acc) clamped to [0, 255]
 // separate multiply and add (no contraction: the TU is built with
-// -ffp-contract=off and the arithmetic goes through __fmul_rn/__fadd_rn),
+// -ffp-contract=off; products and sums are packed f32 ops, one rounding each),
 // row-major tap order, truncation after EVERY step, zero outside the image at
 // every step.  UNIFORM filters (all nine weights equal, e.g. box) compute each
 // input byte's product once per row instead of once per tap: fl(p * w) does
@@ -24,6 +24,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
 
 #include "pconv/kernels.hpp"
 
@@ -38,50 +41,66 @@ struct FloatTaps {
 
 __device__ __forceinline__ float ub(u32 x, int k) { return static_cast<float>((x >> (8 * k)) & 0xffu); }
 
-// Row (8 bytes per lane) -> floats of bytes [-CH, 8 + CH) (times w when UNIFORM).
+// Pairs of floats (bytes j and j + 4 of a lane's 8): every operation on a pair
+// is one packed f32 instruction (v_pk_mul_f32 / v_pk_add_f32), each half
+// rounded exactly like its scalar twin.  The TU is built with
+// -ffp-contract=off, so a product never fuses into the following add.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Row (8 bytes per lane) -> pairs E[j] = (byte j - CH, byte j + 4 - CH) for
+// j in [0, 4 + 2 CH): bytes [-CH, 8 + CH) of the row (times w when UNIFORM).
 template <int CH, bool UNIFORM>
-__device__ __forceinline__ void expand(const u32 (&X)[2], float w, float (&e)[8 + 2 * CH]) {
+__device__ __forceinline__ void expand(const u32 (&X)[2], float w, f2 (&E)[4 + 2 * CH]) {
   const u32 l = __builtin_amdgcn_mov_dpp(X[1], 0x138, 0xf, 0xf, true);  // wave_shr:1 -> left lane's bytes 4..7
   const u32 r = __builtin_amdgcn_mov_dpp(X[0], 0x130, 0xf, 0xf, true);  // wave_shl:1 -> right lane's bytes 0..3
+  float e[8 + 2 * CH];
 #pragma unroll
   for (int j = 0; j < CH; ++j) e[j] = ub(l, 4 - CH + j);
 #pragma unroll
   for (int j = 0; j < 8; ++j) e[CH + j] = ub(X[j >> 2], j & 3);
 #pragma unroll
   for (int j = 0; j < CH; ++j) e[CH + 8 + j] = ub(r, j);
-  if constexpr (UNIFORM) {
 #pragma unroll
-    for (int j = 0; j < 8 + 2 * CH; ++j) e[j] = __fmul_rn(e[j], w);
+  for (int j = 0; j < 4 + 2 * CH; ++j) E[j] = (f2){e[j], e[j + 4]};
+  if constexpr (UNIFORM) {
+    const f2 ww = (f2){w, w};
+#pragma unroll
+    for (int j = 0; j < 4 + 2 * CH; ++j) E[j] = E[j] * ww;
   }
 }
 
+// Output bytes j and j + 4 (j < 4) as floats holding trunc(clamp(acc, 0,
+// 255)): integers, so v_cvt_pk_u8_f32 packs them exactly whatever its
+// rounding mode.  Reference order: row k (a: above, b: this row, c: below),
+// then column l.
 template <int CH, bool UNIFORM>
-__device__ __forceinline__ u32 out_byte(const float (&a)[8 + 2 * CH], const float (&b)[8 + 2 * CH],
-                                        const float (&c)[8 + 2 * CH], int j, const FloatTaps& tp) {
-  // reference order: row k (a: above, b: this row, c: below), then column l
-  float acc;
+__device__ __forceinline__ f2 out_pair(const f2 (&a)[4 + 2 * CH], const f2 (&b)[4 + 2 * CH],
+                                       const f2 (&c)[4 + 2 * CH], int j, const f2 (&w)[9]) {
+  f2 acc;
   if constexpr (UNIFORM) {
     acc = a[j];  // 0 + fl(p*w) is exact
-    acc = __fadd_rn(acc, a[j + CH]);
-    acc = __fadd_rn(acc, a[j + 2 * CH]);
-    acc = __fadd_rn(acc, b[j]);
-    acc = __fadd_rn(acc, b[j + CH]);
-    acc = __fadd_rn(acc, b[j + 2 * CH]);
-    acc = __fadd_rn(acc, c[j]);
-    acc = __fadd_rn(acc, c[j + CH]);
-    acc = __fadd_rn(acc, c[j + 2 * CH]);
+    acc = acc + a[j + CH];
+    acc = acc + a[j + 2 * CH];
+    acc = acc + b[j];
+    acc = acc + b[j + CH];
+    acc = acc + b[j + 2 * CH];
+    acc = acc + c[j];
+    acc = acc + c[j + CH];
+    acc = acc + c[j + 2 * CH];
   } else {
-    acc = __fmul_rn(a[j], tp.w[0]);
-    acc = __fadd_rn(acc, __fmul_rn(a[j + CH], tp.w[1]));
-    acc = __fadd_rn(acc, __fmul_rn(a[j + 2 * CH], tp.w[2]));
-    acc = __fadd_rn(acc, __fmul_rn(b[j], tp.w[3]));
-    acc = __fadd_rn(acc, __fmul_rn(b[j + CH], tp.w[4]));
-    acc = __fadd_rn(acc, __fmul_rn(b[j + 2 * CH], tp.w[5]));
-    acc = __fadd_rn(acc, __fmul_rn(c[j], tp.w[6]));
-    acc = __fadd_rn(acc, __fmul_rn(c[j + CH], tp.w[7]));
-    acc = __fadd_rn(acc, __fmul_rn(c[j + 2 * CH], tp.w[8]));
+    acc = a[j] * w[0];
+    acc = acc + a[j + CH] * w[1];
+    acc = acc + a[j + 2 * CH] * w[2];
+    acc = acc + b[j] * w[3];
+    acc = acc + b[j + CH] * w[4];
+    acc = acc + b[j + 2 * CH] * w[5];
+    acc = acc + c[j] * w[6];
+    acc = acc + c[j + CH] * w[7];
+    acc = acc + c[j + 2 * CH] * w[8];
   }
-  return acc > 0.0f ? (acc >= 255.0f ? 255u : static_cast<u32>(acc)) : 0u;
+  // reference store: float -> uint8 truncation (clamped like the CPU oracle)
+  return (f2){__builtin_truncf(__builtin_amdgcn_fmed3f(acc.x, 0.0f, 255.0f)),
+              __builtin_truncf(__builtin_amdgcn_fmed3f(acc.y, 0.0f, 255.0f))};
 }
 
 template <int CH, bool UNIFORM, int M, int NW>
@@ -101,6 +120,9 @@ __global__ __launch_bounds__(64 * NW) void k_float_temporal(const uint8_t* __res
   const int tile_r0 = r0 + static_cast<int>(blockIdx.y) * vrows;
   const int row_base = tile_r0 - steps + w * M;
   const float w0 = tp.w[0];
+  f2 wv[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) wv[k] = (f2){tp.w[k], tp.w[k]};
 
   // bytes of this lane inside the image row (0..8)
   const int valid = col_in ? min(row_bytes - x, 8) : 0;
@@ -140,7 +162,7 @@ __global__ __launch_bounds__(64 * NW) void k_float_temporal(const uint8_t* __res
       B[0] = b.x;
       B[1] = b.y;
     }
-    float ea[8 + 2 * CH], eb[8 + 2 * CH], ec[8 + 2 * CH];
+    f2 ea[4 + 2 * CH], eb[4 + 2 * CH], ec[4 + 2 * CH];
     expand<CH, UNIFORM>(A, w0, ea);
     expand<CH, UNIFORM>(D[0], w0, eb);
 #pragma unroll
@@ -151,13 +173,15 @@ __global__ __launch_bounds__(64 * NW) void k_float_temporal(const uint8_t* __res
         expand<CH, UNIFORM>(B, w0, ec);
       u32 o0 = 0, o1 = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o0 |= out_byte<CH, UNIFORM>(ea, eb, ec, j, tp) << (8 * j);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o1 |= out_byte<CH, UNIFORM>(ea, eb, ec, 4 + j, tp) << (8 * j);
+      for (int j = 0; j < 4; ++j) {
+        const f2 v = out_pair<CH, UNIFORM>(ea, eb, ec, j, wv);
+        o0 = __builtin_amdgcn_cvt_pk_u8_f32(v.x, j, o0);
+        o1 = __builtin_amdgcn_cvt_pk_u8_f32(v.y, j, o1);
+      }
       D[i][0] = o0;
       D[i][1] = o1;
 #pragma unroll
-      for (int j = 0; j < 8 + 2 * CH; ++j) {
+      for (int j = 0; j < 4 + 2 * CH; ++j) {
         ea[j] = eb[j];
         eb[j] = ec[j];
       }
@@ -189,15 +213,60 @@ __global__ __launch_bounds__(64 * NW) void k_float_temporal(const uint8_t* __res
       if (valid == 8) {
         *reinterpret_cast<uint2*>(q) = make_uint2(D[i][0], D[i][1]);
       } else {  // partial last chunk: never write past the row's last byte
-        for (int b = 0; b < valid; ++b) q[b] = static_cast<uint8_t>(D[i][b >> 2] >> (8 * (b & 3)));
+        const u32 lo = D[i][0], hi = D[i][1];
+        for (int b = 0; b < valid; ++b) q[b] = static_cast<uint8_t>((b < 4 ? lo : hi) >> (8 * (b & 3)));
       }
     }
   }
 }
 
-template <int CH, bool UNIFORM>
-void launch_ft(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s) {
-  constexpr int M = 8, NW = 8;
+struct FtShape {
+  int m, nw;
+};
+
+// Tile shape: the image is small per CU (1920x2520 RGB is 57 KB per CU), so
+// the grid must neither leave CUs idle nor end in a nearly empty second round
+// of workgroups; among the shapes whose vertical halo stays <= 25 % of the
+// tile, take the one whose workgroups fill the CUs most evenly (fewest
+// workgroup rounds, then the least halo).  PCONV_FLOAT_SHAPE="M,NW" forces one.
+FtShape pick_ft_shape(int steps, int ch, int64_t rows, int64_t row_bytes) {
+  static const FtShape cands[] = {{16, 8}, {8, 8}, {16, 4}, {8, 4}, {4, 8}};
+  if (const char* e = std::getenv("PCONV_FLOAT_SHAPE")) {
+    int m = 0, nw = 0;
+    if (std::sscanf(e, "%d,%d", &m, &nw) == 2)
+      for (const auto& c : cands)
+        if (c.m == m && c.nw == nw) return c;
+  }
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess)
+      n = 256;
+    return std::max(1, n);
+  }();
+  const int hl = (steps * ch + 7) / 8;
+  const int64_t ctiles = ceil_div<int64_t>(ceil_div<int64_t>(row_bytes, 8), 64 - 2 * hl);
+  FtShape best{16, 8};
+  double best_cost = 1e30;
+  for (const auto& c : cands) {
+    const int rows_tile = c.m * c.nw, vrows = rows_tile - 2 * steps;
+    if (vrows <= 0 || 2 * steps * 4 > rows_tile) continue;
+    const int64_t wgs = ctiles * ceil_div<int64_t>(rows, vrows);
+    // resident workgroups per CU: 32 waves per CU at ~100 VGPRs (4 per SIMD x 4 SIMDs... x2 for headroom)
+    const int per_cu = std::max(1, 16 / c.nw);
+    const double rounds = std::ceil(static_cast<double>(wgs) / (static_cast<double>(cus) * per_cu));
+    // time ~ rounds x rows per wave (a wave's work per step) x (1 + halo share)
+    const double cost = rounds * c.m * (static_cast<double>(rows_tile) / vrows);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  return best;
+}
+
+template <int CH, bool UNIFORM, int M, int NW>
+void launch_ft_shape(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s) {
   const int steps = a.steps;
   const int hl = (steps * CH + 7) / 8;
   const int vlanes = 64 - 2 * hl;
@@ -208,6 +277,23 @@ void launch_ft(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s) {
   k_float_temporal<CH, UNIFORM, M, NW><<<grid, dim3(64 * NW), 0, s>>>(
       a.src, a.dst, a.pitch, static_cast<int>(a.row_bytes), static_cast<int>(a.r0), static_cast<int>(a.r1), steps,
       static_cast<int>(a.g_row0), static_cast<int>(std::min<int64_t>(a.height, int64_t(1) << 30)), tp);
+}
+
+template <int CH, bool UNIFORM>
+void launch_ft(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s) {
+  const FtShape sh = pick_ft_shape(a.steps, CH, a.r1 - a.r0, a.row_bytes);
+#define PCONV_FT(M_, NW_)                                  \
+  if (sh.m == M_ && sh.nw == NW_) {                        \
+    launch_ft_shape<CH, UNIFORM, M_, NW_>(a, tp, s);       \
+    return;                                                \
+  }
+  PCONV_FT(16, 8)
+  PCONV_FT(8, 8)
+  PCONV_FT(16, 4)
+  PCONV_FT(8, 4)
+  PCONV_FT(4, 8)
+#undef PCONV_FT
+  PCONV_FAIL("float temporal kernel: unsupported tile shape");
 }
 
 template <int CH>
