@@ -71,6 +71,10 @@ void prepare_stencil(const Filter& f, Channels ch, const StencilLaunch& a, hipSt
 // `steps` repetitions of ANY 3x3 filter in the reference's float32 semantics
 // in one launch (kernels/stencil_float.hip): box/9, edge/28, custom filters.
 void launch_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream);
+// Tune the float kernel's tile shape for this launch geometry now (before a
+// graph capture); clear the cache of tuned shapes.
+void prepare_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream);
+void clear_float_tuning();
 
 // Whether `v` (or Auto) can fuse `steps` > 1 for this filter.
 bool supports_fusion(const Filter& f, KernelVariant v);
@@ -128,5 +132,6 @@ void launch_resident(const ResidentLaunch& a, Channels ch, const ResidentPlan& p
 // returns the previous setting.  A one-shot process turns it off: timing a
 // dozen candidates costs more than the loop they would speed up.
 bool set_shape_tuning(bool on);
+bool shape_tuning_enabled();
 
 }  // namespace pconv

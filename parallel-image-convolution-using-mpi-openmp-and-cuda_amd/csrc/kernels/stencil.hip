@@ -481,7 +481,9 @@ bool supports_fusion(const Filter& f, KernelVariant v) {
 
 int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes, int channels) {
   if (!supports_fusion(f, v)) return 1;
-  if (!f.binomial121) return 4;  // float temporal kernel: ALU-bound, a shallow trapezoid
+  // float temporal kernel (gpurun_out/r03/g/float_sweep.jsonl, tuned shapes):
+  // grey 1920x2520 box 3.5 us/rep at 8 vs 3.9 at 4; RGB 8.0 at 4 vs 9.5 at 8
+  if (!f.binomial121) return channels == 1 ? 8 : 4;
   // Grey frames far beyond the Infinity Cache: 12 repetitions per launch
   // measured 2-6 % faster than 8 in every run (32768^2: 113.2-116.2 vs
   // 116.9-121.1 us/rep over four boxes; 16384^2: 30.6 vs 32.2;
@@ -499,7 +501,9 @@ void prepare_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hi
   if (a.r1 <= a.r0) return;
   const bool own_dst_pitch = a.dst_pitch != 0 && a.dst_pitch != a.pitch;
   if (v == KernelVariant::Auto && f.binomial121 && (a.steps > 1 || own_dst_pitch)) v = KernelVariant::Temporal;
+  if (v == KernelVariant::Auto && !f.binomial121 && a.steps > 1) v = KernelVariant::FloatTemporal;
   if (v == KernelVariant::Temporal && f.binomial121 && a.steps <= kMaxFusedSteps) prepare_swar(a, ch, stream);
+  if (v == KernelVariant::FloatTemporal && a.steps <= kMaxFusedSteps) prepare_float_temporal(f, ch, a, stream);
 }
 
 void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hipStream_t stream, KernelVariant v) {

@@ -24,10 +24,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 
+#include "pconv/device.hpp"
 #include "pconv/kernels.hpp"
 
 namespace pconv {
@@ -280,8 +285,7 @@ void launch_ft_shape(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s)
 }
 
 template <int CH, bool UNIFORM>
-void launch_ft(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s) {
-  const FtShape sh = pick_ft_shape(a.steps, CH, a.r1 - a.r0, a.row_bytes);
+void launch_ft_with(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s, FtShape sh) {
 #define PCONV_FT(M_, NW_)                                  \
   if (sh.m == M_ && sh.nw == NW_) {                        \
     launch_ft_shape<CH, UNIFORM, M_, NW_>(a, tp, s);       \
@@ -296,8 +300,75 @@ void launch_ft(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s) {
   PCONV_FAIL("float temporal kernel: unsupported tile shape");
 }
 
+// Empirical shape tuning, as for the SWAR kernel (stencil_swar.hip): on the
+// first launch of a geometry every candidate runs the REAL launch (same src
+// -> dst, so repeats write the same bytes) in two interleaved timed passes and
+// the fastest is cached per (channels, uniform, steps, rows, row bytes).  The
+// shape is a large lever on these small frames and not monotonic in the
+// model (1920x2520 RGB box, 4 steps: 8.0 us/rep with 16x8 tiles, 9.2-10.4
+// with the others; gpurun_out/r03/g/float_sweep.jsonl).  Never while the
+// stream is being captured: the engine tunes a step's launches first.
+struct FtKey {
+  int ch;
+  bool uniform;
+  int steps;
+  int64_t rows, row_bytes;
+  bool operator<(const FtKey& o) const {
+    return std::tie(ch, uniform, steps, rows, row_bytes) < std::tie(o.ch, o.uniform, o.steps, o.rows, o.row_bytes);
+  }
+};
+std::mutex g_ft_mu;
+std::map<FtKey, FtShape> g_ft_tuned;
+
+bool capturing_ft(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+template <int CH, bool UNIFORM>
+FtShape tuned_ft_shape(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s) {
+  const FtShape model = pick_ft_shape(a.steps, CH, a.r1 - a.r0, a.row_bytes);
+  if (std::getenv("PCONV_FLOAT_SHAPE") || !shape_tuning_enabled()) return model;
+  const FtKey key{CH, UNIFORM, a.steps, a.r1 - a.r0, a.row_bytes};
+  {
+    std::lock_guard<std::mutex> lk(g_ft_mu);
+    auto it = g_ft_tuned.find(key);
+    if (it != g_ft_tuned.end()) return it->second;
+  }
+  if (capturing_ft(s)) return model;
+  static const FtShape cands[] = {{16, 8}, {8, 8}, {16, 4}, {8, 4}, {4, 8}};
+  std::vector<FtShape> ok;
+  for (const auto& c : cands)
+    if (c.m * c.nw - 2 * a.steps > 0) ok.push_back(c);
+  PCONV_CHECK(!ok.empty(), "float temporal kernel: steps too large for every tile shape");
+  FtShape best = ok.front();
+  if (ok.size() > 1) {
+    Event e0 = Event::create(true), e1 = Event::create(true);
+    std::vector<float> t(ok.size(), 1e30f);
+    for (int pass = 0; pass < 2; ++pass)
+      for (size_t i = 0; i < ok.size(); ++i) {
+        if (pass == 0) launch_ft_with<CH, UNIFORM>(a, tp, s, ok[i]);  // warm
+        e0.record(s);
+        for (int r = 0; r < 3; ++r) launch_ft_with<CH, UNIFORM>(a, tp, s, ok[i]);
+        e1.record(s);
+        PCONV_HIP_CHECK(hipEventSynchronize(e1.get()));
+        t[i] = std::min(t[i], Event::elapsed_ms(e0, e1));
+      }
+    best = ok[std::min_element(t.begin(), t.end()) - t.begin()];
+  }
+  std::lock_guard<std::mutex> lk(g_ft_mu);
+  g_ft_tuned.emplace(key, best);
+  return best;
+}
+
+template <int CH, bool UNIFORM>
+void launch_ft(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s, bool launch) {
+  const FtShape sh = tuned_ft_shape<CH, UNIFORM>(a, tp, s);
+  if (launch) launch_ft_with<CH, UNIFORM>(a, tp, s, sh);
+}
+
 template <int CH>
-void launch_ft_ch(const Filter& f, const StencilLaunch& a, hipStream_t s) {
+void launch_ft_ch(const Filter& f, const StencilLaunch& a, hipStream_t s, bool launch) {
   FloatTaps tp;
   bool uniform = true;
   for (int i = 0; i < 9; ++i) {
@@ -305,22 +376,39 @@ void launch_ft_ch(const Filter& f, const StencilLaunch& a, hipStream_t s) {
     uniform = uniform && f.weights[i] == f.weights[0];
   }
   if (uniform)
-    launch_ft<CH, true>(a, tp, s);
+    launch_ft<CH, true>(a, tp, s, launch);
   else
-    launch_ft<CH, false>(a, tp, s);
+    launch_ft<CH, false>(a, tp, s, launch);
+}
+
+}  // namespace
+
+namespace {
+
+void float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream, bool launch) {
+  PCONV_CHECK(a.steps >= 1 && a.steps <= kMaxFusedSteps, "float temporal kernel: steps out of range");
+  PCONV_CHECK(a.dst_pitch == 0 || a.dst_pitch == a.pitch, "float temporal kernel: no separate destination pitch");
+  PCONV_CHECK(a.height < (int64_t(1) << 30) && a.g_row0 < (int64_t(1) << 30), "float temporal kernel: rows exceed 2^30");
+  switch (ch) {
+    case Channels::Grey: launch_ft_ch<1>(f, a, stream, launch); break;
+    case Channels::Rgb: launch_ft_ch<3>(f, a, stream, launch); break;
+    case Channels::Rgba: launch_ft_ch<4>(f, a, stream, launch); break;
+  }
 }
 
 }  // namespace
 
 void launch_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream) {
-  PCONV_CHECK(a.steps >= 1 && a.steps <= kMaxFusedSteps, "float temporal kernel: steps out of range");
-  PCONV_CHECK(a.dst_pitch == 0 || a.dst_pitch == a.pitch, "float temporal kernel: no separate destination pitch");
-  PCONV_CHECK(a.height < (int64_t(1) << 30) && a.g_row0 < (int64_t(1) << 30), "float temporal kernel: rows exceed 2^30");
-  switch (ch) {
-    case Channels::Grey: launch_ft_ch<1>(f, a, stream); break;
-    case Channels::Rgb: launch_ft_ch<3>(f, a, stream); break;
-    case Channels::Rgba: launch_ft_ch<4>(f, a, stream); break;
-  }
+  float_temporal(f, ch, a, stream, true);
+}
+
+void prepare_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream) {
+  float_temporal(f, ch, a, stream, false);
+}
+
+void clear_float_tuning() {
+  std::lock_guard<std::mutex> lk(g_ft_mu);
+  g_ft_tuned.clear();
 }
 
 }  // namespace pconv

@@ -1134,9 +1134,14 @@ bool set_shape_tuning(bool on) {
   return prev;
 }
 
+bool shape_tuning_enabled() { return autotune_enabled(); }
+
 void clear_swar_tuning() {
-  std::lock_guard<std::mutex> lk(g_tune_mu);
-  g_tuned.clear();
+  {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    g_tuned.clear();
+  }
+  clear_float_tuning();
 }
 
 std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned() {

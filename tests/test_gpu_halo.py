@@ -91,8 +91,25 @@ def _mid_band(n, y0, rows):
 
 @pytest.fixture(scope="module")
 def self_comm(pconv_mod):
+    import gc
+
     n = pconv_mod.native
-    return n.RcclComm(n.rccl_unique_id(), 0, 1, 0)
+    c = n.RcclComm(n.rccl_unique_id(), 0, 1, 0)
+    yield c
+    # communicators hold device queues and proxy threads: release them before
+    # later tests (the multi-process ones) open their own
+    del c
+    gc.collect()
+
+
+@pytest.fixture(autouse=True)
+def _release_native_objects():
+    """Collect every engine / pipeline / communicator a test created when it
+    ends (their streams and RCCL resources are process-wide)."""
+    import gc
+
+    yield
+    gc.collect()
 
 
 @pytest.mark.parametrize("ch,w", [("rgb", 57), ("grey", 1920)])
