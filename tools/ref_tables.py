@@ -190,14 +190,20 @@ def cmd_mpi_cpu(a):
             for h in ([int(x) for x in a.sizes.split(",")] if a.sizes else SIZES):
                 img = make_image(d, ch, h)
                 for n in [int(x) for x in a.ranks.split(",")]:
+                    env = dict(os.environ, PYTHONPATH=ROOT)
+                    extra = []
+                    threads = None
                     if a.unbound:  # round-2 policy (A/B): unbound ranks, team = CPUs // ranks
                         threads = max(1, ncpu // n) if backend == "omp" else 1
-                        env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS=str(threads), PCONV_CPU_BIND="0")
+                        env.update(OMP_NUM_THREADS=str(threads), PCONV_CPU_BIND="0")
                         extra = ["--threads", str(threads)] if backend == "omp" else []
-                    else:  # the runner's own policy: disjoint CPU slices of the budget, team = slice
-                        threads = None
-                        env = dict(os.environ, PYTHONPATH=ROOT)
-                        extra = []
+                    if a.bind == "off":
+                        env["PCONV_CPU_BIND"] = "0"
+                    if a.wait:
+                        env["OMP_WAIT_POLICY"] = a.wait
+                    if a.spin is not None:
+                        env["GOMP_SPINCOUNT"] = str(a.spin)
+                        env.setdefault("OMP_WAIT_POLICY", "active")  # the spin count decides (libgomp)
                     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                            "--master-addr=127.0.0.1", f"--master-port={_port()}", "-m", "pconv.parallel.run",
                            img, "1920", str(h), "20", ch, "--backend", backend, "--json", "--quiet",
@@ -213,7 +219,8 @@ def cmd_mpi_cpu(a):
                     ref = (MPI_REF if backend == "cpu" else OMP_REF)[(ch, h)]
                     emit(a.out, {"table": "mpi-cpu", "backend": backend, "channels": ch, "height": h, "reps": 20,
                                  "ranks": n, "omp_threads": meta.get("omp_threads", threads),
-                                 "rank0_cpus": meta.get("rank0_cpus"), "bound": not a.unbound,
+                                 "rank0_cpus": meta.get("rank0_cpus"), "bound": meta.get("rank0_cpus") is not None,
+                                 "wait_policy": a.wait or "runner default", "spin": a.spin,
                                  "loop_s": loops[len(loops) // 2],
                                  "loop_all_s": loops, "ref_s": ref[NS.index(n)] if n in NS else None,
                                  "cpus": ncpu})
@@ -332,6 +339,10 @@ def main():
             s.add_argument("--channels", default="grey,rgb")
             s.add_argument("--unbound", action="store_true",
                            help="A/B: the round-2 policy (no CPU binding, team = CPUs // ranks)")
+            s.add_argument("--bind", choices=["on", "off"], default="on", help="A/B: CPU slices per rank")
+            s.add_argument("--wait", choices=["passive", "active"], default=None,
+                           help="A/B: OMP_WAIT_POLICY of the ranks (default: the runner's choice)")
+            s.add_argument("--spin", type=int, default=None, help="A/B: GOMP_SPINCOUNT of the ranks")
     s = sub.add_parser("report")
     s.add_argument("inputs", nargs="+")
     s.add_argument("--md", default=None)
