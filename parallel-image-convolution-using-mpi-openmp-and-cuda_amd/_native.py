@@ -20,9 +20,12 @@ import torch  # noqa: F401  -- see module docstring
 # extension below) sleep between parallel regions instead of spinning: CPU
 # ranks of the MPI+OpenMP analog share a node's CPU quota, and spinning
 # workers of one rank burn the quota the others' compute needs (a throttled
-# cgroup stalls every rank for the rest of its 100 ms period).  Measured cost
-# on one process: ~5 % on a 20-region loop.  An explicit setting wins.
-os.environ.setdefault("OMP_WAIT_POLICY", "passive")
+# cgroup stalls every rank for the rest of its 100 ms period: the round-2
+# hybrid table had 0.1-0.2 s outliers and got slower with more ranks;
+# profiles/r03/hybrid/).  An explicit setting (OMP_WAIT_POLICY or
+# GOMP_SPINCOUNT) wins.
+if "OMP_WAIT_POLICY" not in os.environ and "GOMP_SPINCOUNT" not in os.environ:
+    os.environ["OMP_WAIT_POLICY"] = "passive"
 
 _ERR = None
 try:

@@ -179,22 +179,22 @@ def cpu_rank_slice(local_rank: int, local_world: int, allowed, budget: int) -> l
 
 
 def bind_cpu_rank(local_rank: int, local_world: int) -> Optional[list]:
-    """Bind this CPU rank to its slice (``cpu_rank_slice``) BEFORE its
-    OpenMP team starts (team threads inherit the affinity of the thread that
-    creates them) and size torch's own pools to one thread, so that the ranks
-    of a node never run more busy threads than the node's CPU budget.
+    """Opt-in (PCONV_CPU_BIND=1): bind this CPU rank to its slice
+    (``cpu_rank_slice``) before its OpenMP team starts (team threads inherit
+    the affinity of the thread that creates them).  Always: torch's own pools
+    drop to one thread, so a rank runs its team and nothing else.
 
-    Why: with unbound teams of ``budget / n`` threads, spinning OpenMP
-    workers of n ranks plus torch and gloo threads exceed a CFS quota (the
-    GPU box grants 16 CPUs of a 256-CPU host) and the whole cgroup is
-    throttled for the rest of the 100 ms period — the hybrid table got slower
-    as ranks were added (reference: one team per rank,
-    open-mp/omp_convolution.c:292,297).  PCONV_CPU_BIND=0 disables."""
-    if os.environ.get("PCONV_CPU_BIND", "1") == "0" or not hasattr(os, "sched_setaffinity"):
+    Measured on the GPU box's CPU share (16 CPUs of a shared 256-CPU host,
+    profiles/r03/hybrid/): binding to fixed CPUs puts the teams on CPUs other
+    tenants also use (bound teams showed 14-190 ms stalls); unbound teams
+    sized budget / ranks with passive waits (the package default, _native.py)
+    were the steadiest, so binding is off by default.  Reference: one team
+    per rank (open-mp/omp_convolution.c:292,297)."""
+    torch.set_num_threads(1)
+    if os.environ.get("PCONV_CPU_BIND", "0") != "1" or not hasattr(os, "sched_setaffinity"):
         return None
     n = require_native()
     budget = n.default_cpu_threads()
     mine = cpu_rank_slice(local_rank, local_world, os.sched_getaffinity(0), budget)
     os.sched_setaffinity(0, mine)
-    torch.set_num_threads(1)
     return mine

@@ -203,3 +203,18 @@ def test_reflected_ghost_oracle_cpu(native, rng, reps, halo, fuse, overlap, y0):
     owned = rng.integers(0, 256, size=(rows, w), dtype=np.uint8)
     got = reflected_ghost_oracle(native, plan, d, owned, y0, height, "grey")
     assert np.array_equal(got, _ext_model(owned, y0, height, plan, d, reps))
+
+
+def test_cpu_rank_slices_are_disjoint():
+    """MPI+OpenMP analog: the node's CPU budget split between its ranks
+    (opt-in binding, parallel/bootstrap.py)."""
+    from pconv.parallel.bootstrap import cpu_rank_slice
+
+    allowed = set(range(0, 64, 2)) | {100, 101}
+    for world in (1, 2, 3, 4, 9):
+        slices = [cpu_rank_slice(r, world, allowed, 15) for r in range(world)]
+        assert all(len(s) == max(1, 15 // world) for s in slices)
+        flat = [c for s in slices for c in s]
+        assert len(flat) == len(set(flat)) and set(flat) <= set(sorted(allowed)[:15])
+    # more ranks than budget CPUs: round-robin sharing, never empty
+    assert all(len(cpu_rank_slice(r, 20, allowed, 4)) == 1 for r in range(20))

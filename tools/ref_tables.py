@@ -197,8 +197,8 @@ def cmd_mpi_cpu(a):
                         threads = max(1, ncpu // n) if backend == "omp" else 1
                         env.update(OMP_NUM_THREADS=str(threads), PCONV_CPU_BIND="0")
                         extra = ["--threads", str(threads)] if backend == "omp" else []
-                    if a.bind == "off":
-                        env["PCONV_CPU_BIND"] = "0"
+                    if a.bind != "default":
+                        env["PCONV_CPU_BIND"] = "1" if a.bind == "on" else "0"
                     if a.wait:
                         env["OMP_WAIT_POLICY"] = a.wait
                     if a.spin is not None:
@@ -339,7 +339,8 @@ def main():
             s.add_argument("--channels", default="grey,rgb")
             s.add_argument("--unbound", action="store_true",
                            help="A/B: the round-2 policy (no CPU binding, team = CPUs // ranks)")
-            s.add_argument("--bind", choices=["on", "off"], default="on", help="A/B: CPU slices per rank")
+            s.add_argument("--bind", choices=["default", "on", "off"], default="default",
+                           help="A/B: CPU slices per rank (default: the runner's choice, off)")
             s.add_argument("--wait", choices=["passive", "active"], default=None,
                            help="A/B: OMP_WAIT_POLICY of the ranks (default: the runner's choice)")
             s.add_argument("--spin", type=int, default=None, help="A/B: GOMP_SPINCOUNT of the ranks")
