@@ -52,6 +52,7 @@ enum class KernelVariant : int {
   Float9 = 4,    // generic float32 9-tap (reference rounding)
   TemporalPk = 5,  // packed-u16 (VOP3P) fused gaussian, kept for A/B measurements
   FloatTemporal = 6,  // any 3x3 filter, float32 reference rounding, `steps` fused in registers
+  Mfma = 7,           // prototype: one gaussian step on a grey frame as two banded f16 MFMA products
 };
 
 const char* kernel_variant_name(KernelVariant v);
@@ -75,6 +76,8 @@ void launch_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a,
 // graph capture); clear the cache of tuned shapes.
 void prepare_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream);
 void clear_float_tuning();
+// MFMA prototype (kernels/stencil_mfma.hip): one gaussian step, grey frames.
+void launch_mfma_grey_step(const StencilLaunch& a, hipStream_t stream);
 
 // Whether `v` (or Auto) can fuse `steps` > 1 for this filter.
 bool supports_fusion(const Filter& f, KernelVariant v);

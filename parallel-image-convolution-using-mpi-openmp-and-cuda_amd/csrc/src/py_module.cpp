@@ -60,6 +60,7 @@ KernelVariant parse_variant(const std::string& s) {
   if (s == "int9") return KernelVariant::Int9;
   if (s == "float9") return KernelVariant::Float9;
   if (s == "float_temporal") return KernelVariant::FloatTemporal;
+  if (s == "mfma") return KernelVariant::Mfma;
   PCONV_FAIL("unknown kernel variant '" + s + "'");
 }
 
