@@ -127,7 +127,7 @@ def parse():
                         "result; reported under 'halo_modes' (auto: on for N>1)")
     p.add_argument("--halo-modes", default=",".join(HALO_MODES),
                    help="comma list of the halo modes timed after the headline at N>1: " + ", ".join(HALO_MODES))
-    p.add_argument("--exchange-timeout", type=float, default=60.0, help="seconds before a mode's drain aborts")
+    p.add_argument("--exchange-timeout", type=float, default=30.0, help="seconds before a mode's drain aborts")
     p.add_argument("--halo-select", choices=["auto", "off", "exchange"] + list(HALO_MODES), default="auto",
                    help="N>1: report as the headline the fastest bit-exact halo mode when it is at least 3 %% faster "
                         "than the pre-loaded pipeline (auto; the halo mode chosen by measurement, like the kernel "
@@ -135,7 +135,7 @@ def parse():
                         "mode's timing stays in 'halo_modes'")
     p.add_argument("--watchdog", type=float, default=None,
                    help="seconds the whole halo-mode measurement may take, communicator set-up included, before "
-                        "every rank exits with the line as it stands printed (default modes x (timeout + 15) + 30)")
+                        "every rank exits with the line as it stands printed (default modes x (timeout + 10) + 30)")
     p.add_argument("--stall-exchange", action="store_true", help=argparse.SUPPRESS)  # tests: a hung peer
     p.add_argument("--hw-queues", type=int, default=0,
                    help="GPU_MAX_HW_QUEUES for this process (default: max(8, slots + 3))")
@@ -578,7 +578,7 @@ def main():
             os._exit(0)
 
         dog = threading.Timer(a.watchdog if a.watchdog is not None else
-                              len(modes) * (a.exchange_timeout + 15.0) + 30.0, expire)
+                              len(modes) * (a.exchange_timeout + 10.0) + 30.0, expire)
         dog.daemon = True
         dog.start()
         ref_rows = blur.step(a.reps).copy()
