@@ -1062,7 +1062,9 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   }
   PCONV_CHECK(!ranked.empty(), "swar temporal kernel: steps too large for every tile shape");
   std::sort(ranked.begin(), ranked.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-  if (ranked.size() > static_cast<size_t>(kTuneCandidates)) ranked.resize(kTuneCandidates);
+  size_t keep = kTuneCandidates;  // PCONV_TUNE_CANDIDATES widens the timed set (A/B of the model's ranking)
+  if (const char* e = std::getenv("PCONV_TUNE_CANDIDATES")) keep = static_cast<size_t>(std::max(1, std::atoi(e)));
+  if (ranked.size() > keep) ranked.resize(keep);
   std::vector<SwarChoice> cands;
   for (const auto& r : ranked)
     for (int alt = 0; alt <= 1; ++alt)
