@@ -513,8 +513,8 @@ def main():
                            "floor_ms": round(max(h2d_ms, d2h_ms), 4)},
             "loop_only": {
                 "ms_per_step": round(loop_elapsed / ls * 1e3, 4) if ls else None,
-                "mpix_per_s": round(loop_value, 2) if loop_value else None,
-                "us_per_rep": round(loop_elapsed / ls / a.reps * 1e6, 3) if ls else None,
+                "mpix_per_s": round(loop_value, 2) if loop_value else None,  # (reps 0: copy-only diagnostics)
+                "us_per_rep": round(loop_elapsed / ls / a.reps * 1e6, 3) if ls and a.reps else None,
             },
             "device": torch.cuda.get_device_name(device),
             "runtime": runtime,
