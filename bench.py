@@ -192,9 +192,10 @@ def gather_floats(v: float):
 #       image k computes (event-ordered);
 #   overlap: the reference's algorithm (mpi/mpi_convolution.c:156-240,
 #       Isend/Irecv, inner compute, Wait, edges) with a T-deep halo: an
-#       exchange every fused launch on the comm stream, the interior launch
-#       concurrently on the compute stream, the edge strips after the halo
-#       event.
+#       exchange every fused launch on the slot's comm stream, the interior
+#       launch concurrently on the slot stream, the edge strips after the
+#       halo event; with RCCL each image (all its phases) is ONE captured
+#       graph with a fork/join per exchange.
 HALO_MODES = ("slot_exchange", "slot_exchange_direct", "event", "overlap")
 
 
@@ -205,8 +206,10 @@ def mode_kwargs(a, mode: str, fuse: int) -> dict:
         kw["slot_exchange"] = True
         kw["graph_capture"] = mode == "slot_exchange"
     elif mode == "overlap":
-        kw["halo"] = int(fuse)  # T-deep ghost zone: one exchange per fused launch
-        kw["overlap"] = True
+        # T-deep ghost zone: one exchange per fused launch, on the slot's comm
+        # stream beside the interior launch, edges after the halo event; with
+        # RCCL the whole image is one captured graph
+        kw.update(halo=int(fuse), overlap=True, slot_exchange=True, slot_comm=True, graph_capture=True)
     elif mode != "event":
         raise ValueError(f"unknown halo mode {mode!r}")
     return kw
@@ -247,7 +250,8 @@ def measure_mode(a, mode, ref_rows, world, rank, device, transport, fuse):
                    halo_depth=int(xb.engine.halo), fuse=int(xb.engine.fuse),
                    launches_per_step=int(st.launches), exchanges_per_step=int(st.exchanges),
                    slot_streams=bool(xb.pipe.graphs), step_graphs=bool(xb.pipe.step_graphs),
-                   concurrent_images=bool(xb.pipe.concurrent), overlap_split=bool(mode_kwargs(a, mode, fuse)["overlap"]))
+                   concurrent_images=bool(xb.pipe.concurrent),
+                   overlap_split=mode == "overlap" or (mode == "event" and not a.no_overlap))
     except Exception as e:  # reported, never fatal for the headline line
         res["status"] = f"error: {type(e).__name__}: {e}"[:400]
     finally:

@@ -253,8 +253,15 @@ class BandPipeline {
   // per-stream serial chain is H2D + reps instead of H2D + reps + D2H, with
   // one more busy queue (slots/2 + 1 in total).  Engine reuse waits for that
   // engine's previous download (events), so no frame is overwritten early.
+  // slot_comm (slot-stream mode): every slot also gets its own
+  // communication stream and keeps opt.overlap, so an exchange phase splits
+  // into the interior launch on the slot stream ‖ the exchange on its comm
+  // stream, the edge strips after the halo event — and, captured, the whole
+  // image (the reference's Isend/inner/Wait/edges loop for every phase) is
+  // ONE graph with a fork/join per exchange.
   BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt, int slots,
-               int concurrent = -1, bool slot_streams = false, bool step_graphs = true, bool split_d2h = false);
+               int concurrent = -1, bool slot_streams = false, bool step_graphs = true, bool split_d2h = false,
+               bool slot_comm = false);
   ~BandPipeline();
   int slots() const { return static_cast<int>(slots_.size()); }
   BandEngine& slot(int i) { return *slots_.at(i); }
@@ -286,6 +293,7 @@ class BandPipeline {
   void trace_mark(int stage, hipStream_t s);
   Stream h2d_, d2h_, comm_;
   std::vector<Stream> computes_;
+  std::vector<Stream> slot_comms_;  // slot_comm: one communication stream per slot
   bool concurrent_ = false;
   bool graphs_ = false;  // slot-stream mode
   bool step_graphs_ = true;

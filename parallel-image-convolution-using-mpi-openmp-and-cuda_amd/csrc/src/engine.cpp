@@ -479,7 +479,7 @@ void BandEngine::synchronize() {
 // --------------------------------------------------------------- BandPipeline
 
 BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt,
-                           int slots, int concurrent, bool graphs, bool step_graphs, bool split_d2h) {
+                           int slots, int concurrent, bool graphs, bool step_graphs, bool split_d2h, bool slot_comm) {
   PCONV_CHECK(slots >= 1 && slots <= 8, "pipeline slots must be in [1, 8]");
   set_device(opt.device);
   if (split_d2h) {
@@ -518,11 +518,19 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
     // engine's cached rep-loop graph whenever no exchange phase remains.
     o.use_graph = !step_graphs;
     o.timing = false;
-    o.overlap = false;  // an image's exchange and launches share its stream: no split launches
+    // Without slot_comm an image's exchange and launches share its stream:
+    // no split launches.  With it, each slot's exchanges run on the slot's
+    // own communication stream beside the interior launch.
+    o.overlap = slot_comm && opt.overlap;
     for (int i = 0; i < slots; ++i) {
       computes_.push_back(Stream::create(0));
       o.compute_stream = computes_.back().get();
-      o.comm_stream = computes_.back().get();
+      if (slot_comm) {
+        slot_comms_.push_back(Stream::create(-1));
+        o.comm_stream = slot_comms_.back().get();
+      } else {
+        o.comm_stream = computes_.back().get();
+      }
       slots_.push_back(std::make_unique<BandEngine>(geom, band, filter, o));
     }
     used_.assign(slots, false);
@@ -564,6 +572,7 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
 BandPipeline::~BandPipeline() {
   if (h2d_.get()) (void)hipStreamSynchronize(h2d_.get());
   for (auto& c : computes_) (void)hipStreamSynchronize(c.get());
+  for (auto& c : slot_comms_) (void)hipStreamSynchronize(c.get());
   if (d2h_.get()) (void)hipStreamSynchronize(d2h_.get());
   if (comm_.get()) (void)hipStreamSynchronize(comm_.get());
 }

@@ -557,7 +557,7 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
                        int concurrent, bool graphs, bool zero_copy_out, bool step_graphs, bool split_d2h,
-                       bool packed_out, bool kernel_d2h, py::object band) {
+                       bool packed_out, bool kernel_d2h, py::object band, bool slot_comm) {
              EngineOptions o;
              o.zero_copy_out = zero_copy_out;
              o.packed_out = packed_out;
@@ -571,14 +571,14 @@ PYBIND11_MODULE(_pconv_native, m) {
              // band: an explicit Band (tests: a self-neighbour band on a 1-rank communicator)
              const Band b = band.is_none() ? row_band(h, world, rank) : band.cast<Band>();
              return std::make_unique<BandPipeline>(g, b, make_filter(filter), o, slots, concurrent, graphs,
-                                                   step_graphs, split_d2h);
+                                                   step_graphs, split_d2h, slot_comm);
            }),
            py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
            py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
            py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1,
            py::arg("graphs") = false, py::arg("zero_copy_out") = false, py::arg("step_graphs") = true,
            py::arg("split_d2h") = false, py::arg("packed_out") = false, py::arg("kernel_d2h") = false,
-           py::arg("band") = py::none())
+           py::arg("band") = py::none(), py::arg("slot_comm") = false)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",

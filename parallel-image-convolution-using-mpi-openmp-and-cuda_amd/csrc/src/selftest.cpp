@@ -234,17 +234,21 @@ std::string rccl_selftest_multicomm(int device, int slots, int images, double ti
   };
   // halo >= reps: one whole-zone exchange per image, then a cached rep-loop
   // graph; halo < reps: exchange phases inside the run (stream-ordered).
-  const Case cases[] = {{40, 40, 8}, {20, 8, 4}};
+  const Case cases[] = {{40, 40, 8}, {20, 8, 4}, {24, 8, 8}};
   int checked = 0;
   // directly issued images, then images captured as ONE graph each (upload,
   // RCCL exchange(s), launches, download: BandEngine::process_graph)
+  // slot_comm: the exchange phases split (interior || exchange on the slot's
+  // comm stream, edges after the halo event), captured with a fork/join
+  for (const bool slot_comm : {false, true})
   for (const bool captured : {false, true})
   for (const Case& c : cases) {
     EngineOptions o;
     o.device = device;
     o.halo_depth = c.halo;
     o.fuse = c.fuse;
-    BandPipeline pipe(g, self_band(y0, rows), f, o, slots, -1, /*slot_streams=*/true, /*step_graphs=*/captured);
+    BandPipeline pipe(g, self_band(y0, rows), f, o, slots, -1, /*slot_streams=*/true, /*step_graphs=*/captured,
+                      /*split_d2h=*/false, slot_comm);
     std::vector<std::shared_ptr<RcclComm>> comms;
     for (int k = 0; k < slots; ++k) {
       comms.push_back(std::make_shared<RcclComm>(rccl_unique_id(), 0, 1, device));
@@ -286,7 +290,7 @@ std::string rccl_selftest_multicomm(int device, int slots, int images, double ti
   }
   std::ostringstream os;
   os << "{\"selftest\": \"rccl_multicomm\", \"communicators\": " << slots << ", \"images_per_case\": " << images
-     << ", \"cases\": " << checked << ", \"captured_cases\": " << checked / 2 << ", \"status\": \"ok\", \"rccl_version\": \"" << rccl_version()
+     << ", \"cases\": " << checked << ", \"captured_cases\": " << checked / 2 << ", \"split_cases\": " << checked / 2 << ", \"status\": \"ok\", \"rccl_version\": \"" << rccl_version()
      << "\", \"rccl_path\": \"" << json_escape(rccl_library_path()) << "\"}";
   return os.str();
 }

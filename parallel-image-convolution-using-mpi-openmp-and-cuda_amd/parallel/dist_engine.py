@@ -59,7 +59,7 @@ class DistributedBlur:
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
                  step_graphs: Optional[bool] = None, zero_copy_out: bool = False, graph_capture: bool = True,
                  slot_exchange: bool = False, split_d2h: bool = False, packed_out: bool = False,
-                 kernel_d2h: bool = False, self_neighbours: bool = False):
+                 kernel_d2h: bool = False, self_neighbours: bool = False, slot_comm: bool = False):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -115,10 +115,15 @@ class DistributedBlur:
             raise ValueError("split_d2h needs an even number of slots (two engines per compute stream)")
         if self.slot_exchange or split or (free if step_graphs is None else bool(step_graphs)):
             del self.pipe
+            # slot_comm (exchange images): each slot also gets a communication
+            # stream, so an exchange phase runs beside the interior launch and
+            # the edges follow the halo event — captured, the reference's per-
+            # phase loop becomes ONE graph per image.
             self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
                                        graphs=True, zero_copy_out=bool(zero_copy_out), packed_out=bool(packed_out),
                                        kernel_d2h=bool(kernel_d2h),
-                                       step_graphs=bool(graph_capture) or split, split_d2h=split, **kw)
+                                       step_graphs=bool(graph_capture) or split, split_d2h=split,
+                                       slot_comm=bool(slot_comm) and self.slot_exchange, **kw)
         self.engine = self.pipe.slot(0)
         self.band = self.engine.band
         self.row_bytes = self.engine.row_bytes

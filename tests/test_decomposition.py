@@ -155,7 +155,10 @@ def test_auto_fuse_policy(native, pconv_mod):
     assert native.auto_fuse(g, "auto", 1920 * 2520, 1) == 8
     assert native.auto_fuse(g, "auto", 32768 * 4096, 1) == 8  # 8-way band of 32768^2
     assert native.auto_fuse(g, "auto", 32768 * 32768) == 8  # channels unknown
-    assert native.auto_fuse(get_filter("box").to_native(), "auto", 32768 * 32768, 1) == 1
+    # float filters: the temporal float32 kernel (8 grey, 4 RGB); one step with an explicit one-step kernel
+    assert native.auto_fuse(get_filter("box").to_native(), "auto", 32768 * 32768, 1) == 8
+    assert native.auto_fuse(get_filter("edge").to_native(), "auto", 1920 * 2520 * 3, 3) == 4
+    assert native.auto_fuse(get_filter("box").to_native(), "float9", 1920 * 2520 * 3, 3) == 1
 
 
 def _ext_model(owned, y0, height, plan, halo, reps):

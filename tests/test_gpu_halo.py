@@ -379,18 +379,21 @@ def test_rccl_selftests_cli_stack(name):
     assert "torch" not in lines[0]["rccl_path"] and "torch" not in lines[-1]["hip_runtime_path"]
 
 
-@pytest.mark.parametrize("captured", [True, False])
-@pytest.mark.parametrize("reps,halo,fuse", [(40, 40, 8), (20, 8, 4), (13, 13, 4)])
-def test_slot_pipeline_rccl_exchange_images(pconv_mod, captured, reps, halo, fuse):
+@pytest.mark.parametrize("captured,slot_comm", [(True, False), (False, False), (True, True), (False, True)])
+@pytest.mark.parametrize("reps,halo,fuse", [(40, 40, 8), (20, 8, 4), (13, 13, 4), (24, 8, 8)])
+def test_slot_pipeline_rccl_exchange_images(pconv_mod, captured, slot_comm, reps, halo, fuse):
     """Slot-exchange pipeline on a mid-image self-neighbour band, one 1-rank
     communicator per slot stream (three in flight together): images issued
     directly, or each captured as ONE hipGraph (upload, ncclSend/ncclRecv of
     the ghost zone, launches, download — BandEngine::process_graph).  Every
-    image equals the reflected-ghost oracle."""
+    image equals the reflected-ghost oracle.  slot_comm: each slot also has a
+    communication stream, an exchange phase's interior launch runs beside the
+    exchange and the edges after the halo event (captured: the reference's
+    per-phase loop as ONE graph with a fork/join per exchange)."""
     n = pconv_mod.native
     w, height, y0, rows, slots = 301, 520, 211, 96, 3
     pipe = n.BandPipeline(w, height, "rgb", "gaussian", 0, 1, 0, halo=halo, fuse=fuse, slots=slots, graphs=True,
-                          step_graphs=captured, band=_mid_band(n, y0, rows))
+                          step_graphs=captured, band=_mid_band(n, y0, rows), slot_comm=slot_comm)
     assert pipe.step_graphs == captured
     comms = [n.RcclComm(n.rccl_unique_id(), 0, 1, 0) for _ in range(slots)]
     for k, c in enumerate(comms):
@@ -423,5 +426,7 @@ def test_slot_pipeline_rccl_exchange_images(pconv_mod, captured, reps, halo, fus
             assert bad == 0, (rnd, k, bad)
     st = pipe.slot(0).stats
     assert st.exchanges == (1 if zone else len([p for p in plan if p.exchange_depth]))
+    if slot_comm and not zone:  # split exchange phases: interior || exchange, edges after the halo event
+        assert any(len(p.launches) > 1 for p in plan if p.exchange_depth)
     if captured:
         assert pipe.slot(0).cached_step_graphs >= 1
