@@ -24,7 +24,8 @@ namespace pconv {
 // address and a native backtrace (backtrace_symbols_fd: library + offset,
 // resolvable with llvm-addr2line) to stderr, then hand the signal to the
 // handler that was installed before (Python's faulthandler prints the Python
-// frames) or to the default action.  Idempotent.
+// frames) or to the default action.  Idempotent.  With PCONV_CRASH_LOG set,
+// the report is also appended to that file (test runners capture fd 2).
 void install_crash_handler();
 
 // CPU model of a self-neighbour band's run (1-rank communicator, up = down =
@@ -37,7 +38,9 @@ std::vector<uint8_t> reflected_band_oracle(const Filter& f, Channels ch, int64_t
                                            int64_t height, int64_t pre_exchange = 0);
 
 // Grouped ncclSend/ncclRecv to self (op "sendrecv") or a 1-rank ncclAllReduce
-// (op "allreduce") captured into a hipGraph with capture mode "global",
+// (op "allreduce"), issued on the capturing stream or (ops "*_fork") on a
+// second stream that joined the capture through an event, captured into a
+// hipGraph with capture mode "global",
 // "thread_local" or "relaxed" (or "none": issued directly, the control), the
 // graph launched `launches` times, received bytes checked.  Progress lines go
 // to stderr before each step (so a crash names its step).  Returns a JSON

@@ -199,7 +199,13 @@ void RcclTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream) {
 
 std::string rccl_capture_probe(const std::string& op, const std::string& mode, int64_t bytes, int device,
                                int launches) {
-  PCONV_CHECK(op == "sendrecv" || op == "allreduce", "rccl_capture_probe: op must be sendrecv or allreduce");
+  PCONV_CHECK(op == "sendrecv" || op == "allreduce" || op == "sendrecv_fork" || op == "allreduce_fork",
+              "rccl_capture_probe: op must be sendrecv, allreduce, sendrecv_fork or allreduce_fork");
+  // *_fork: the RCCL call goes to a SECOND stream that joined the capture
+  // through an event (record on the origin, wait on the second stream; joined
+  // back the same way) — how a split exchange phase is captured.
+  const bool fork = op.size() > 5 && op.compare(op.size() - 5, 5, "_fork") == 0;
+  const std::string base = fork ? op.substr(0, op.size() - 5) : op;
   PCONV_CHECK(bytes >= 8 && bytes % 8 == 0, "rccl_capture_probe: bytes must be a positive multiple of 8");
   hipStreamCaptureMode cm = hipStreamCaptureModeGlobal;
   const bool capture = mode != "none";
@@ -224,14 +230,26 @@ std::string rccl_capture_probe(const std::string& op, const std::string& mode, i
   PCONV_HIP_CHECK(hipMemcpy(a.data(), pat.data(), n, hipMemcpyHostToDevice));
   PCONV_HIP_CHECK(hipMemset(b.data(), 0, n));
   Stream s = Stream::create(0);
+  Stream s2 = Stream::create(-1);
+  Event ev_fork = Event::create(), ev_join = Event::create();
   auto enqueue = [&] {
-    if (op == "sendrecv") {
+    hipStream_t t = s.get();
+    if (fork) {
+      ev_fork.record(s.get());
+      ev_fork.wait_on(s2.get());
+      t = s2.get();
+    }
+    if (base == "sendrecv") {
       PCONV_RCCL_CHECK(rccl().GroupStart());
-      PCONV_RCCL_CHECK(rccl().Send(a.data(), n, ncclUint8, 0, c, s.get()));
-      PCONV_RCCL_CHECK(rccl().Recv(b.data(), n, ncclUint8, 0, c, s.get()));
+      PCONV_RCCL_CHECK(rccl().Send(a.data(), n, ncclUint8, 0, c, t));
+      PCONV_RCCL_CHECK(rccl().Recv(b.data(), n, ncclUint8, 0, c, t));
       PCONV_RCCL_CHECK(rccl().GroupEnd());
     } else {
-      PCONV_RCCL_CHECK(rccl().AllReduce(a.data(), b.data(), n, ncclUint8, ncclSum, c, s.get()));
+      PCONV_RCCL_CHECK(rccl().AllReduce(a.data(), b.data(), n, ncclUint8, ncclSum, c, t));
+    }
+    if (fork) {
+      ev_join.record(s2.get());
+      ev_join.wait_on(s.get());
     }
   };
   hipGraphExec_t ex = nullptr;

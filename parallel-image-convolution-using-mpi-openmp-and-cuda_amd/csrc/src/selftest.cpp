@@ -2,6 +2,7 @@
 #include "pconv/selftest.hpp"
 
 #include <execinfo.h>
+#include <fcntl.h>
 #include <signal.h>
 #include <unistd.h>
 
@@ -25,8 +26,12 @@ namespace {
 constexpr int kCrashSignals[] = {SIGSEGV, SIGBUS, SIGILL, SIGFPE, SIGABRT};
 struct sigaction g_prev[sizeof(kCrashSignals) / sizeof(int)];
 bool g_installed = false;
+int g_fds[2] = {2, -1};  // stderr, and PCONV_CRASH_LOG when set (test runners capture fd 2)
 
-void write_str(const char* s) { (void)!::write(2, s, std::strlen(s)); }
+void write_str(const char* s) {
+  for (int fd : g_fds)
+    if (fd >= 0) (void)!::write(fd, s, std::strlen(s));
+}
 
 void write_hex(uintptr_t v) {
   char buf[2 + 16 + 1];
@@ -58,7 +63,8 @@ void on_fatal(int sig, siginfo_t* info, void* uctx) {
   write_str("\n[pconv] native backtrace (library(+offset) -> llvm-addr2line -e library offset):\n");
   void* frames[64];
   const int n = backtrace(frames, 64);
-  backtrace_symbols_fd(frames, n, 2);
+  for (int fd : g_fds)
+    if (fd >= 0) backtrace_symbols_fd(frames, n, fd);
   // Hand over to the previous handler (faulthandler: Python frames), else
   // the default action (core / termination with the signal's status).
   size_t i = 0;
@@ -78,6 +84,9 @@ void on_fatal(int sig, siginfo_t* info, void* uctx) {
 
 void install_crash_handler() {
   if (g_installed) return;
+  // A copy of the report to a file: a test runner that captures fd 2 drops
+  // what a dying process wrote there (faulthandler writes to a saved fd).
+  if (const char* p = std::getenv("PCONV_CRASH_LOG")) g_fds[1] = ::open(p, O_WRONLY | O_CREAT | O_APPEND, 0644);
   void* prime[2];
   (void)backtrace(prime, 2);  // loads libgcc's unwinder outside the handler
   // An alternate stack: a stack overflow must still be reported.

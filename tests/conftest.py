@@ -44,7 +44,11 @@ def pconv_mod():
     import pconv
 
     assert pconv.native_available(), "native extension not built (run __graft_entry__.build())"
-    pconv.native.install_crash_handler()  # a native crash prints its C++ frames before faulthandler's
+    # a native crash prints its C++ frames before faulthandler's; pytest
+    # captures fd 2, so the report also goes to a file
+    os.environ.setdefault("PCONV_CRASH_LOG", os.path.join(ROOT, "gpurun_out", f"native_crash_{os.getpid()}.log")
+                          if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp/pconv_native_crash.log")
+    pconv.native.install_crash_handler()
     return pconv
 
 
