@@ -236,6 +236,27 @@ void BandEngine::enqueue_phase(const Phase& p) {
     PCONV_CHECK(transport_ != nullptr, "band has neighbours but no halo transport is attached");
     hipStream_t ms = comm_stream();
     const bool split = ms != cs_;  // one stream: stream order is the dependency
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (split && hipStreamIsCapturing(cs_, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) {
+      // Inside a graph capture the roles swap: the exchange stays on the
+      // capturing stream and the INTERIOR launch goes to the forked one.
+      // torch's bundled HIP 7.0 runtime recurses without end (stack overflow
+      // in hipStreamEndCapture) on a capture whose RCCL kernel sits on a
+      // stream that joined it through an event; ROCm 7.2's runtime does not
+      // (profiles/r03/capture/fork/, `rccl_capture_probe(op="*_fork")`).
+      ev_ready_.record(cs_);
+      ev_ready_.wait_on(ms);
+      for (const auto& l : p.launches)
+        if (!l.after_halo) launch(l, ms);
+      transport_->exchange(*this, p.exchange_depth, cs_);
+      for (const auto& l : p.launches)
+        if (l.after_halo) launch(l, cs_);
+      ev_halo_.record(ms);  // join: the interior rows are final before the next phase
+      ev_halo_.wait_on(cs_);
+      ++stats_.exchanges;
+      cur_ ^= 1;
+      return;
+    }
     if (split) {
       ev_ready_.record(cs_);
       ev_ready_.wait_on(ms);
