@@ -192,10 +192,9 @@ def gather_floats(v: float):
 #       image k computes (event-ordered);
 #   overlap: the reference's algorithm (mpi/mpi_convolution.c:156-240,
 #       Isend/Irecv, inner compute, Wait, edges) with a T-deep halo: an
-#       exchange every fused launch on the slot's comm stream, the interior
-#       launch concurrently on the slot stream, the edge strips after the
-#       halo event; with RCCL each image (all its phases) is ONE captured
-#       graph with a fork/join per exchange.
+#       exchange every fused launch on the comm stream, the interior launch
+#       concurrently on the compute stream, the edge strips after the halo
+#       event.
 HALO_MODES = ("slot_exchange", "slot_exchange_direct", "event", "overlap")
 
 
@@ -206,10 +205,12 @@ def mode_kwargs(a, mode: str, fuse: int) -> dict:
         kw["slot_exchange"] = True
         kw["graph_capture"] = mode == "slot_exchange"
     elif mode == "overlap":
-        # T-deep ghost zone: one exchange per fused launch, on the slot's comm
-        # stream beside the interior launch, edges after the halo event; with
-        # RCCL the whole image is one captured graph
-        kw.update(halo=int(fuse), overlap=True, slot_exchange=True, slot_comm=True, graph_capture=True)
+        # T-deep ghost zone: one exchange per fused launch on the comm stream
+        # beside the interior launch, edges after the halo event (event-ordered
+        # streams; the same loop captured as one graph per image on slot
+        # streams, DistributedBlur(slot_comm=True), measured slower: 0.303 vs
+        # 0.246 ms per 8-way rank step, profiles/r03/emulate8/captured_split/)
+        kw.update(halo=int(fuse), overlap=True)
     elif mode != "event":
         raise ValueError(f"unknown halo mode {mode!r}")
     return kw
