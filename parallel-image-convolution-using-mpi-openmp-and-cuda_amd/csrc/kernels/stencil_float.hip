@@ -229,13 +229,15 @@ struct FtShape {
   int m, nw;
 };
 
-// Tile shape: the image is small per CU (1920x2520 RGB is 57 KB per CU), so
-// the grid must neither leave CUs idle nor end in a nearly empty second round
-// of workgroups; among the shapes whose vertical halo stays <= 25 % of the
-// tile, take the one whose workgroups fill the CUs most evenly (fewest
-// workgroup rounds, then the least halo).  PCONV_FLOAT_SHAPE="M,NW" forces one.
+// Tile shape when nothing is tuned (one-shot CLI, a capture before tuning):
+// the largest tile (least halo) whose grid fills the chip — at least 3/4 of
+// a workgroup per CU — and whose last round of workgroups is at least 3/4
+// full.  Fits the sweep (gpurun_out/r03/g/float_sweep.jsonl): 1920x2520 RGB
+// at 4 steps -> 16x8 (252 workgroups: 8.0 us/rep, best), at 8 steps -> 16x4
+// (9.5, best 9.5); grey at 8 steps -> 16x4 (3.6, best 3.5); 8192^2 RGB ->
+// 16x8 (best).  PCONV_FLOAT_SHAPE="M,NW" forces one.
 FtShape pick_ft_shape(int steps, int ch, int64_t rows, int64_t row_bytes) {
-  static const FtShape cands[] = {{16, 8}, {8, 8}, {16, 4}, {8, 4}, {4, 8}};
+  static const FtShape cands[] = {{16, 8}, {16, 4}, {8, 8}, {8, 4}, {4, 8}};  // largest tiles first
   if (const char* e = std::getenv("PCONV_FLOAT_SHAPE")) {
     int m = 0, nw = 0;
     if (std::sscanf(e, "%d,%d", &m, &nw) == 2)
@@ -250,24 +252,21 @@ FtShape pick_ft_shape(int steps, int ch, int64_t rows, int64_t row_bytes) {
     return std::max(1, n);
   }();
   const int hl = (steps * ch + 7) / 8;
-  const int64_t ctiles = ceil_div<int64_t>(ceil_div<int64_t>(row_bytes, 8), 64 - 2 * hl);
-  FtShape best{16, 8};
-  double best_cost = 1e30;
+  const int64_t ctiles = ceil_div<int64_t>(ceil_div<int64_t>(row_bytes, 8), std::max(1, 64 - 2 * hl));
+  FtShape most{4, 8};
+  int64_t most_wgs = -1;
   for (const auto& c : cands) {
-    const int rows_tile = c.m * c.nw, vrows = rows_tile - 2 * steps;
-    if (vrows <= 0 || 2 * steps * 4 > rows_tile) continue;
+    const int vrows = c.m * c.nw - 2 * steps;
+    if (vrows <= 0) continue;
     const int64_t wgs = ctiles * ceil_div<int64_t>(rows, vrows);
-    // resident workgroups per CU: 32 waves per CU at ~100 VGPRs (4 per SIMD x 4 SIMDs... x2 for headroom)
-    const int per_cu = std::max(1, 16 / c.nw);
-    const double rounds = std::ceil(static_cast<double>(wgs) / (static_cast<double>(cus) * per_cu));
-    // time ~ rounds x rows per wave (a wave's work per step) x (1 + halo share)
-    const double cost = rounds * c.m * (static_cast<double>(rows_tile) / vrows);
-    if (cost < best_cost) {
-      best_cost = cost;
-      best = c;
+    const int64_t rounds = ceil_div<int64_t>(wgs, cus);
+    if (4 * wgs >= 3 * static_cast<int64_t>(cus) && 4 * wgs >= 3 * rounds * cus) return c;
+    if (wgs > most_wgs) {
+      most_wgs = wgs;
+      most = c;
     }
   }
-  return best;
+  return most;  // a small frame: the shape with the most workgroups
 }
 
 template <int CH, bool UNIFORM, int M, int NW>
