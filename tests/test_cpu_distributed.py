@@ -182,3 +182,26 @@ def test_bench_metric_names():
     assert bench.metric_for(a) == "Mpixels/sec (and wall-time) for 8192x8192 RGB, 100 reps at 1/2/4/8 MI355X"
     a = SimpleNamespace(width=1920, height=2520, channels="rgb", reps=40, filter="box")
     assert "box" in bench.metric_for(a) and bench.metric_for(a) != bench.METRIC
+
+
+def test_bench_halo_mode_kwargs():
+    """The five N>1 pipelines bench.py times (slot_exchange, slot_exchange_direct,
+    event, overlap after the pre-loaded headline) map to the intended
+    DistributedBlur configurations."""
+    import importlib.util
+    from types import SimpleNamespace
+
+    spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.HALO_MODES == ("slot_exchange", "slot_exchange_direct", "event", "overlap")
+    a = SimpleNamespace(slots=3, variant="auto", fuse=None, no_overlap=False, halo=None, concurrent="off")
+    kw = {m: bench.mode_kwargs(a, m, 8) for m in bench.HALO_MODES}
+    for m, k in kw.items():
+        assert k["preload_halo"] is False, m  # every mode moves its ghost rows GPU-to-GPU
+    assert kw["slot_exchange"]["slot_exchange"] and kw["slot_exchange"]["graph_capture"]
+    assert kw["slot_exchange_direct"]["slot_exchange"] and not kw["slot_exchange_direct"]["graph_capture"]
+    assert not kw["event"].get("slot_exchange") and kw["event"]["halo"] is None  # deep auto halo
+    assert kw["overlap"]["halo"] == 8 and kw["overlap"]["overlap"]  # T-deep halo, split phases
+    with pytest.raises(ValueError):
+        bench.mode_kwargs(a, "nope", 8)
