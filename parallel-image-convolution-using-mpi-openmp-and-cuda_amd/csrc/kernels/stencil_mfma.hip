@@ -108,6 +108,7 @@ void launch_mfma_grey_step(const StencilLaunch& a, hipStream_t stream) {
   PCONV_CHECK(a.steps == 1, "mfma prototype: one step per launch");
   PCONV_CHECK(a.dst_pitch == 0 || a.dst_pitch == a.pitch, "mfma prototype: no separate destination pitch");
   PCONV_CHECK(a.height < (int64_t(1) << 30) && a.g_row0 < (int64_t(1) << 30), "mfma prototype: rows exceed 2^30");
+  PCONV_CHECK(a.row_bytes > 0 && a.row_bytes < (int64_t(1) << 30), "mfma prototype: row bytes out of range");
   const int rows = static_cast<int>(a.r1 - a.r0);
   const dim3 grid(static_cast<unsigned>(ceil_div<int64_t>(a.row_bytes, kBlk * kNB)),
                   static_cast<unsigned>(ceil_div(ceil_div(rows, kBlk), 4)));

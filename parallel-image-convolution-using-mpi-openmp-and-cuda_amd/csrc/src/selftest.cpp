@@ -42,6 +42,18 @@ void write_hex(uintptr_t v) {
   write_str(buf);
 }
 
+// Signal names from a fixed table: strsignal() is not async-signal-safe.
+const char* signal_name(int sig) {
+  switch (sig) {
+    case SIGSEGV: return "Segmentation fault";
+    case SIGBUS: return "Bus error";
+    case SIGILL: return "Illegal instruction";
+    case SIGFPE: return "Floating point exception";
+    case SIGABRT: return "Aborted";
+    default: return "signal";
+  }
+}
+
 void on_fatal(int sig, siginfo_t* info, void* uctx) {
   // Only async-signal-safe calls up to backtrace (backtrace() itself may
   // allocate on first use: it is primed in install_crash_handler).
@@ -57,7 +69,7 @@ void on_fatal(int sig, siginfo_t* info, void* uctx) {
     write_str(c);
   }
   write_str(" (");
-  write_str(strsignal(sig));
+  write_str(signal_name(sig));
   write_str(") at address ");
   write_hex(reinterpret_cast<uintptr_t>(info ? info->si_addr : nullptr));
   write_str("\n[pconv] native backtrace (library(+offset) -> llvm-addr2line -e library offset):\n");
@@ -299,8 +311,9 @@ std::string rccl_selftest_multicomm(int device, int slots, int images, double ti
   }
   std::ostringstream os;
   os << "{\"selftest\": \"rccl_multicomm\", \"communicators\": " << slots << ", \"images_per_case\": " << images
-     << ", \"cases\": " << checked << ", \"captured_cases\": " << checked / 2 << ", \"split_cases\": " << checked / 2 << ", \"status\": \"ok\", \"rccl_version\": \"" << rccl_version()
-     << "\", \"rccl_path\": \"" << json_escape(rccl_library_path()) << "\"}";
+     << ", \"cases\": " << checked << ", \"captured_cases\": " << checked / 2 << ", \"split_cases\": " << checked / 2
+     << ", \"status\": \"ok\", \"rccl_version\": \"" << rccl_version() << "\", \"rccl_path\": \""
+     << json_escape(rccl_library_path()) << "\"}";
   return os.str();
 }
 
@@ -312,8 +325,9 @@ int selftest_main(const std::vector<std::string>& args) {
   int device = 0, slots = 3, images = 60;
   int64_t bytes = 4096;
   std::string op = "sendrecv", mode = "relaxed";
-  for (size_t i = 3; i + 1 < args.size(); i += 2) {
+  for (size_t i = 3; i < args.size(); i += 2) {
     const std::string& k = args[i];
+    PCONV_CHECK(i + 1 < args.size(), "selftest: option " + k + " needs a value");
     const std::string& v = args[i + 1];
     if (k == "--device")
       device = std::stoi(v);
