@@ -29,34 +29,44 @@ __device__ __forceinline__ u32 opaque(u32 v) {
   return v;
 }
 
-// Horizontal [1,2,1] at tap distance CH over NP pairs; taps in the
-// neighbouring lane come through DPP (wave_shr:1 / wave_shl:1, bound_ctrl: 0
-// past the wave edge).
-//   NP = 4: most taps cross lanes (RGB: 6 of 8 per row), so each one is the
-//     DPP source of its add (v_add_u32_dpp) — 2 VALU ops per pair instead of
-//     up to 4 with separate v_mov_b32_dpp;
-//   NP = 8: few taps cross lanes and the register budget is tight (the big
-//     tiles sit at 2 waves/SIMD); the plain form keeps the compiler free to
-//     schedule (folding costs these tiles ~20 VGPRs = one wave per SIMD).
+// Hides `v` from instruction combining only (non-volatile: free to
+// schedule).  On gfx950 every VOP3 encoding (v_add3_u32, v_lshl_add_u32,
+// v_perm_b32, v_bfe_u32, ...) and every DPP op issues at ~half the rate of a
+// VOP2 v_add_u32 / v_lshrrev_b32 / v_and_b32 (4.3-4.7 vs 2.4-2.7 cycles per
+// wave-instruction at 4 waves/SIMD, tools/ubench/valu_issue.hip,
+// profiles/r03/valu_issue.md).  keep() stops two dependent adds from fusing
+// into a v_add3_u32 where the first one is also needed on its own (a fused
+// add3 beside the plain add costs 2.8 issue slots for what two adds do in 2),
+// and stops a lane-crossing add from becoming v_mov_b32_dpp + v_add3_u32 (VOP3
+// cannot take a DPP source on gfx950) instead of one v_add_u32_dpp.
+__device__ __forceinline__ u32 keep(u32 v) {
+  asm("" : "+v"(v));
+  return v;
+}
+
+// Horizontal [1,2,1] at tap distance CH over NP pairs, as two pair sums:
+//   P_j = X_j + X_{j+CH},   H_k = P_{k-CH} + P_k  (= X_{k-CH} + 2 X_k + X_{k+CH}).
+// Two v_add_u32 per pair and no shift (the direct form needs v_lshlrev or a
+// VOP3 v_lshl_add_u32 for 2 X_k, then two adds); the operands that live in the
+// neighbouring lane are the DPP source of their add: X_{j+CH} past the lane's
+// last pair from lane+1 (wave_shl:1), P_{k-CH} before its first pair from
+// lane-1 (wave_shr:1); bound_ctrl gives 0 past the wave edge.  Edge lanes:
+// lane 63 sees X = 0 beyond it (as the direct form does); lane 0 misses both
+// terms of P_{k-CH} for k < CH instead of one — those bytes are halo garbage
+// either way (the tile's halo is sized for the CH bytes per step that enter
+// at a strip edge, whatever their values), and columns outside the image are
+// real zeros inside the strip, where the two forms agree exactly.
 template <int CH, int NP>
 __device__ __forceinline__ void horiz(const u32 (&X)[NP], u32 (&H)[NP]) {
   static_assert(CH <= NP, "tap distance must not exceed the pairs per lane");
+  u32 P[NP];
 #pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    const int l = k - CH, r = k + CH;
-    if constexpr (NP == 4) {
-      u32 t = X[k] << 1;
-      if (l >= 0) t += X[l];
-      if (r < NP) t += X[r];
-      if (l < 0) t = __builtin_amdgcn_mov_dpp(X[NP + l], 0x138, 0xf, 0xf, true) + opaque(t);
-      if (r >= NP) t = __builtin_amdgcn_mov_dpp(X[r - NP], 0x130, 0xf, 0xf, true) + opaque(t);
-      H[k] = t;
-    } else {
-      const u32 lv = l >= 0 ? X[l] : __builtin_amdgcn_mov_dpp(X[NP + l], 0x138, 0xf, 0xf, true);
-      const u32 rv = r < NP ? X[r] : __builtin_amdgcn_mov_dpp(X[r - NP], 0x130, 0xf, 0xf, true);
-      H[k] = (X[k] << 1) + (lv + rv);
-    }
-  }
+  for (int j = 0; j < NP; ++j)
+    P[j] = keep(j + CH < NP ? X[j] + X[j + CH]
+                            : __builtin_amdgcn_mov_dpp(X[j + CH - NP], 0x130, 0xf, 0xf, true) + X[j]);
+#pragma unroll
+  for (int k = 0; k < NP; ++k)
+    H[k] = keep(k >= CH ? P[k - CH] + P[k] : __builtin_amdgcn_mov_dpp(P[k - CH + NP], 0x138, 0xf, 0xf, true) + P[k]);
 }
 
 template <int NP>
@@ -143,31 +153,30 @@ __device__ __forceinline__ void swar_step(u32 (&D)[M][NP], uint4 (&lds)[2][NW][2
     lds[par][w][0][q][lane] = make_uint4(D[0][4 * q], D[0][4 * q + 1], D[0][4 * q + 2], D[0][4 * q + 3]);
     lds[par][w][1][q][lane] = make_uint4(D[M - 1][4 * q], D[M - 1][4 * q + 1], D[M - 1][4 * q + 2], D[M - 1][4 * q + 3]);
   }
-  u32 H0[NP], H1[NP], Hp[NP], Hc[NP];
+  // Vertical [1,2,1] as rolling pair sums S_i = H_i + H_{i+1}; row i is
+  // S_{i-1} + S_i: two v_add_u32 per pair (keep(): no v_add3_u32 that would
+  // redo an add the next row needs anyway).
+  u32 H0[NP], Hc[NP], S01[NP], Sc[NP];
   horiz<CH, NP>(D[0], H0);
-  horiz<CH, NP>(D[1], H1);
+  horiz<CH, NP>(D[1], Hc);
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
-    Hp[k] = H0[k];
-    Hc[k] = H1[k];
+    S01[k] = keep(H0[k] + Hc[k]);
+    Sc[k] = S01[k];
   }
-  u32 Sc[NP];
-#pragma unroll
-  for (int k = 0; k < NP; ++k) Sc[k] = Hp[k] + Hc[k];
 #pragma unroll
   for (int i = 1; i + 1 < M; ++i) {
     u32 Hn[NP];
     horiz<CH, NP>(D[i + 1], Hn);
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const u32 Sn = Hc[k] + Hn[k];
+      const u32 Sn = keep(Hc[k] + Hn[k]);
       D[i][k] = trunc_sum<MODE>(Sc[k] + Sn);
       Sc[k] = Sn;
-      Hp[k] = Hc[k];
       Hc[k] = Hn[k];
     }
   }
-  // Hp = H[M-2], Hc = H[M-1] (old rows); H0, H1 = H[0], H[1].
+  // Sc = S_{M-2} = H[M-2] + H[M-1], Hc = H[M-1] (old rows); S01 = H[0] + H[1].
   __syncthreads();
   {
     const int wa = w > 0 ? w - 1 : 0;       // wave 0: tile top halo, value irrelevant
@@ -184,8 +193,8 @@ __device__ __forceinline__ void swar_step(u32 (&D)[M][NP], uint4 (&lds)[2][NW][2
     horiz<CH, NP>(B, Hb);
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      D[0][k] = trunc_sum<MODE>((Ha[k] + H0[k]) + (H0[k] + H1[k]));
-      D[M - 1][k] = trunc_sum<MODE>((Hp[k] + Hc[k]) + (Hc[k] + Hb[k]));
+      D[0][k] = trunc_sum<MODE>(keep(Ha[k] + H0[k]) + S01[k]);
+      D[M - 1][k] = trunc_sum<MODE>(Sc[k] + keep(Hc[k] + Hb[k]));
     }
   }
   if (needs_mask) {
