@@ -5,25 +5,26 @@
 // (cuda/cuda_convolution.cu:9-47, 66-87).  Here one launch advances `steps`
 // repetitions of a whole tile held in registers.
 //
-// Why SWAR-32: measured on gfx950 (tools/ubench/isa_rates.hip), packed
-// 16-bit VOP3P ops (v_pk_add_u16, v_pk_mad_u16, v_pk_lshrrev_b16) and
-// v_perm_b32 issue at HALF the rate of plain 32-bit VALU ops, while
-// v_add_u32 / v_lshlrev_b32 / v_and_b32 run at full rate (v_add3_u32 at half
-// rate: one v_add3 costs what two v_add_u32 do; 64-bit adds and shifts at half
-// to a third, profiles/r02/raw/isa/isa_rates_u64.txt).  Two
+// Why SWAR-32: measured on gfx950 (tools/ubench/valu_issue.hip, exact
+// encodings in inline asm), VOP1/VOP2 ops (v_add_u32, v_lshrrev_b32,
+// v_and_b32 with a literal) issue one wave-instruction per ~2.5 cycles per
+// SIMD, every VOP3 encoding (v_add3_u32, v_lshl_add_u32, v_perm_b32, ...) and
+// every DPP op ~1.8x that, and packed 16-bit VOP3P ops (v_pk_add_u16,
+// v_pk_lshrrev_b16) are slower still (tools/ubench/isa_rates.hip).  Two
 // 16-bit fields in a u32 never carry into each other here (every sum stays
-// below 4080 < 2^16), so plain 32-bit adds do the packed work at twice the
-// throughput.
+// below 4080 < 2^16), so plain 32-bit adds do the packed work at full rate.
 //
 // Layout: per row a lane holds LW u32 "pairs" P_k = (A_k, B_k): A_k is byte k
 // of the lane's LW-byte chunk in column strip A, B_k the same byte of strip
 // B (two strips of 64*LW bytes per wave).  The horizontal neighbour of P_k at
-// distance CH is P_{k±CH}, or — across the lane boundary — the neighbouring
-// lane's register via DPP wave_shr/wave_shl (at 4-byte lanes folded into the
-// add as a DPP source operand).  Per pair per step: 2 ops horizontal
-// (v_lshl_add / v_add3 / v_add_u32_dpp), 2 vertical (rolling sum), 2
-// truncation (v_lshrrev, v_and), all full rate; the byte shuffles (v_perm)
-// happen only when a tile is loaded and stored.
+// distance CH is P_{k+-CH}, or — across the lane boundary — the neighbouring
+// lane's register, read as the DPP source (wave_shr/wave_shl) of the add that
+// consumes it.  Per pair per step (swar_device.hpp): 2 v_add_u32 horizontal
+// (pair sums X_j + X_{j+CH}, then P_{k-CH} + P_k), 2 vertical (rolling pair
+// sums), 2 truncation (v_lshrrev, v_and; 1.5 on average in the paired form) —
+// no VOP3 in the step, 2*CH of the horizontal adds per row with a DPP
+// operand; the byte shuffles (v_perm) happen only when a tile is loaded and
+// stored (profiles/r03/valu/).
 //
 // Tile: NW waves stacked vertically, wave w keeps rows [w*M, (w+1)*M); each
 // step the waves swap their boundary rows through LDS (double-buffered by step
@@ -915,9 +916,10 @@ double swar_launch_cycles(SwarShape s, int steps, int ch, int64_t rows, int64_t 
   const double per_cu = std::ceil(g / 256.0);
   const double rounds = std::ceil(per_cu / L);
   const double k = std::min<double>(per_cu, L) * s.nw / 4.0;  // waves per SIMD
-  // lane-crossing taps per row: separate DPP moves at 8-byte lanes, folded
-  // into the adds at 4-byte lanes (only the pairs with both taps outside cost one)
-  const double cross = np == 4 ? (ch == 1 ? 0.0 : ch == 3 ? 2.0 : 4.0) : 2.0 * ch;
+  // lane-crossing operands per row: 2 x ch pair sums take a DPP source (CH of
+  // the P_j, CH of the H_k, swar_device.hpp horiz); a DPP add issues at ~1.8x
+  // a plain v_add_u32 (tools/ubench/valu_issue.hip), so each costs 0.8 extra
+  const double cross = 1.6 * ch;
   const double stage = (s.m + 2) * (2.0 * np + cross) + s.m * 4.0 * np + 24.0;
   const double instr = steps * stage + 40.0 + 3.0 * s.m * np;
   const double round_cycles = instr * std::max(k * kCyclesMin, kCyclesOneWave) + steps * kStep + kRowLoad * s.m;

@@ -34,7 +34,7 @@ __device__ __forceinline__ u32 opaque(u32 v) {
 // v_perm_b32, v_bfe_u32, ...) and every DPP op issues at ~half the rate of a
 // VOP2 v_add_u32 / v_lshrrev_b32 / v_and_b32 (4.3-4.7 vs 2.4-2.7 cycles per
 // wave-instruction at 4 waves/SIMD, tools/ubench/valu_issue.hip,
-// profiles/r03/valu_issue.md).  keep() stops two dependent adds from fusing
+// profiles/r03/valu/README.md).  keep() stops two dependent adds from fusing
 // into a v_add3_u32 where the first one is also needed on its own (a fused
 // add3 beside the plain add costs 2.8 issue slots for what two adds do in 2),
 // and stops a lane-crossing add from becoming v_mov_b32_dpp + v_add3_u32 (VOP3
