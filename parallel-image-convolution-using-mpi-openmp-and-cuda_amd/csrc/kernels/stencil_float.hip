@@ -74,9 +74,9 @@ __device__ __forceinline__ void expand(const u32 (&X)[2], float w, f2 (&E)[4 + 2
   }
 }
 
-// Output bytes j and j + 4 (j < 4) as floats holding trunc(clamp(acc, 0,
-// 255)): integers, so v_cvt_pk_u8_f32 packs them exactly whatever its
-// rounding mode.  Reference order: row k (a: above, b: this row, c: below),
+// Output bytes j and j + 4 (j < 4) as floats holding trunc(acc): integers, so
+// v_cvt_pk_u8_f32 packs them exactly whatever its rounding mode, saturating
+// the ones outside [0, 255].  Reference order: row k (a: above, b: this row, c: below),
 // then column l.
 template <int CH, bool UNIFORM>
 __device__ __forceinline__ f2 out_pair(const f2 (&a)[4 + 2 * CH], const f2 (&b)[4 + 2 * CH],
@@ -103,9 +103,13 @@ __device__ __forceinline__ f2 out_pair(const f2 (&a)[4 + 2 * CH], const f2 (&b)[
     acc = acc + c[j + CH] * w[7];
     acc = acc + c[j + 2 * CH] * w[8];
   }
-  // reference store: float -> uint8 truncation (clamped like the CPU oracle)
-  return (f2){__builtin_truncf(__builtin_amdgcn_fmed3f(acc.x, 0.0f, 255.0f)),
-              __builtin_truncf(__builtin_amdgcn_fmed3f(acc.y, 0.0f, 255.0f))};
+  // reference store: float -> uint8 truncation, clamped like the CPU oracle.
+  // The clamp is the packer's: v_cvt_pk_u8_f32 saturates to [0, 255]
+  // (measured: -1e9, -5, -0.5 -> 0; 256, 300, 1e9 -> 255;
+  // tools/ubench/cvt_pk_u8.hip, profiles/r03/float/cvt_pk_u8.txt), and
+  // cvt(trunc(x)) == trunc(clamp(x, 0, 255)) for every finite x, so no
+  // v_med3_f32 (a VOP3, ~1.8 issue slots) per output.
+  return (f2){__builtin_truncf(acc.x), __builtin_truncf(acc.y)};
 }
 
 template <int CH, bool UNIFORM, int M, int NW>
