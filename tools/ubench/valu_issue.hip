@@ -43,6 +43,16 @@ constexpr int PER_BLOCK = 16;
 #define I_PERM(d, a, b) "v_perm_b32 " d ", " a ", " b ", %8\n"
 #define I_ADD_LSHL(d, a, b) "v_add_lshl_u32 " d ", " a ", " b ", 1\n"
 #define I_BFE(d, a, b) "v_bfe_u32 " d ", " a ", 4, 8\n"
+// float ops of the float temporal kernel (stencil_float.hip)
+#define I_ADD_F32(d, a, b) "v_add_f32_e32 " d ", " a ", " b "\n"
+#define I_MUL_F32(d, a, b) "v_mul_f32_e32 " d ", " a ", " b "\n"
+#define I_TRUNC_F32(d, a, b) "v_trunc_f32_e32 " d ", " a "\n"
+#define I_CVT_UBYTE(d, a, b) "v_cvt_f32_ubyte1_e32 " d ", " a "\n"
+#define I_CVT_PK_U8(d, a, b) "v_cvt_pk_u8_f32 " d ", " a ", 1, " b "\n"
+#define I_MED3_F32(d, a, b) "v_med3_f32 " d ", " a ", 0, " b "\n"
+// packed f32 on register pairs (%0..%7 are 64-bit operands here)
+#define I_PK_ADD_F32(d, a, b) "v_pk_add_f32 " d ", " a ", " b "\n"
+#define I_PK_MUL_F32(d, a, b) "v_pk_mul_f32 " d ", " a ", " b "\n"
 
 #define KERNEL(NAME, T)                                                                         \
   __global__ __launch_bounds__(256) void NAME(uint32_t* out, uint32_t seed) {                   \
@@ -69,6 +79,25 @@ KERNEL(k_and, I_AND)
 KERNEL(k_perm, I_PERM)
 KERNEL(k_add_lshl, I_ADD_LSHL)
 KERNEL(k_bfe, I_BFE)
+KERNEL(k_add_f32, I_ADD_F32)
+KERNEL(k_mul_f32, I_MUL_F32)
+KERNEL(k_trunc_f32, I_TRUNC_F32)
+KERNEL(k_cvt_ubyte, I_CVT_UBYTE)
+KERNEL(k_cvt_pk_u8, I_CVT_PK_U8)
+KERNEL(k_med3_f32, I_MED3_F32)
+
+#define KERNEL64(NAME, T)                                                                       \
+  __global__ __launch_bounds__(256) void NAME(uint32_t* out, uint32_t seed) {                   \
+    uint64_t r0 = seed + threadIdx.x, r1 = r0 * 3, r2 = r0 * 5, r3 = r0 * 7, r4 = r0 * 11,      \
+             r5 = r0 * 13, r6 = r0 * 17, r7 = r0 * 19;                                          \
+    for (int it = 0; it < ITERS; ++it) {                                                        \
+      asm volatile(R8(T) R8(T)                                                                  \
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7)); \
+    }                                                                                           \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = uint32_t(r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7); \
+  }
+KERNEL64(k_pk_add_f32, I_PK_ADD_F32)
+KERNEL64(k_pk_mul_f32, I_PK_MUL_F32)
 
 template <typename K>
 int run(const char* name, K kern, int per_cu) {
@@ -110,6 +139,14 @@ int main() {
     run("v_perm_b32", k_perm, w);
     run("v_add_lshl_u32", k_add_lshl, w);
     run("v_bfe_u32", k_bfe, w);
+    run("v_add_f32", k_add_f32, w);
+    run("v_mul_f32", k_mul_f32, w);
+    run("v_pk_add_f32", k_pk_add_f32, w);
+    run("v_pk_mul_f32", k_pk_mul_f32, w);
+    run("v_trunc_f32", k_trunc_f32, w);
+    run("v_cvt_f32_ubyte1", k_cvt_ubyte, w);
+    run("v_cvt_pk_u8_f32", k_cvt_pk_u8, w);
+    run("v_med3_f32", k_med3_f32, w);
   }
   return 0;
 }
