@@ -40,7 +40,10 @@ The JSON names the runtime actually loaded ("runtime": HIP runtime version
 and library path, RCCL version and library path): under torch, librccl and
 the HIP runtime resolve to torch's bundled copies.
 value = W*H*reps*steps / max-over-ranks elapsed / 1e6 (whole-job Mpix/s).
-Extra fields report the device-resident loop alone (no PCIe copies).
+Extra fields report the device-resident loop alone (no PCIe copies) and the
+box's PCIe floor: each copy alone and, as `copy_floor.pair_ms`, one pitched
+H2D + one pitched D2H of a step issued together — what a PCIe-bound step
+converges to (e.g. 0.309 ms per pair vs a 0.318 ms step at N=1).
 
 Data: synthetic random bytes (no image ships with the reference).
 """
@@ -443,6 +446,15 @@ def main():
     h2d_ms, d2h_ms = copy_floor_ms(blur.inputs[0].size, b.rows * blur.row_bytes, device)
     h2d_ms = max_over_ranks(h2d_ms / 1e3) * 1e3
     d2h_ms = max_over_ranks(d2h_ms / 1e3) * 1e3
+    # ... and both directions at once, pitched like the pipeline's copies: the
+    # floor a PCIe-bound step converges to (diagnostic only: never fatal)
+    try:
+        pair_ms = pconv.native.copy_pair_floor_ms(device, blur.row_bytes, blur.inputs[0].size // blur.row_bytes,
+                                                  b.rows, 8)
+    except Exception as e:  # noqa: BLE001
+        print(f"bench: copy pair floor not measured: {e}", file=sys.stderr)
+        pair_ms = -1.0
+    pair_ms = max_over_ranks(pair_ms / 1e3) * 1e3
     if a.emulate:
         world = 1
 
@@ -515,7 +527,10 @@ def main():
             },
             "latency_ms": round(latency_ms, 4),
             "copy_floor": {"h2d_ms": round(h2d_ms, 4), "d2h_ms": round(d2h_ms, 4),
-                           "floor_ms": round(max(h2d_ms, d2h_ms), 4)},
+                           "floor_ms": round(max(h2d_ms, d2h_ms), 4),
+                           # one pitched H2D + one pitched D2H of a step issued together (the PCIe-bound
+                           # pipeline's floor; null if the measurement failed)
+                           "pair_ms": round(pair_ms, 4) if pair_ms > 0 else None},
             "loop_only": {
                 "ms_per_step": round(loop_elapsed / ls * 1e3, 4) if ls else None,
                 "mpix_per_s": round(loop_value, 2) if loop_value else None,  # (reps 0: copy-only diagnostics)

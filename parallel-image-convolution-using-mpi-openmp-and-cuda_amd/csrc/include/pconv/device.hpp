@@ -46,6 +46,15 @@ HipRuntimeInfo hip_runtime_info();
 // PCONV_NUMA_BIND=0 disables.  Returns the CPUs kept, 0 if nothing changed.
 int bind_to_device_numa(int device);
 
+// PCIe floor of one pipelined step on this box: `iters` pitched (2-D) H2D
+// copies of `rows_in` rows and, concurrently on a second stream, `iters`
+// pitched D2H copies of `rows_out` rows — the copy shapes the serving
+// pipeline issues — timed together; returns ms per (H2D, D2H) pair.  With
+// both directions busy the link carries less than the sum of the solo rates
+// (~94 GB/s in both directions together on the measured boxes), so this, not
+// the slower solo copy, is what a PCIe-bound step converges to.
+double copy_pair_floor_ms(int device, int64_t row_bytes, int64_t rows_in, int64_t rows_out, int iters);
+
 class DeviceBuffer {
  public:
   DeviceBuffer() = default;

@@ -4,6 +4,7 @@
 #include <dlfcn.h>
 #include <sched.h>
 
+#include <algorithm>
 #include <cctype>
 #include <cstdlib>
 #include <fstream>
@@ -71,6 +72,36 @@ int bind_to_device_numa(int device) {
   const int n = CPU_COUNT(&keep);
   if (n == 0 || CPU_EQUAL(&keep, &allowed)) return 0;
   return sched_setaffinity(0, sizeof(keep), &keep) == 0 ? n : 0;
+}
+
+double copy_pair_floor_ms(int device, int64_t row_bytes, int64_t rows_in, int64_t rows_out, int iters) {
+  PCONV_CHECK(row_bytes > 0 && rows_in > 0 && rows_out > 0 && iters > 0, "copy_pair_floor_ms: empty copy");
+  set_device(device);
+  const int64_t pitch = (row_bytes + 16 + 127) / 128 * 128;  // a padded frame pitch like the engine's
+  DeviceBuffer din(static_cast<size_t>(pitch * rows_in)), dout(static_cast<size_t>(pitch * rows_out));
+  PinnedBuffer hin(static_cast<size_t>(row_bytes * rows_in)), hout(static_cast<size_t>(row_bytes * rows_out));
+  Stream s1 = Stream::create(0), s2 = Stream::create(0);
+  Event e0 = Event::create(true), a = Event::create(true), b = Event::create(true);
+  auto pairs = [&](int n) {
+    PCONV_HIP_CHECK(hipDeviceSynchronize());
+    e0.record(s1.get());
+    e0.wait_on(s2.get());
+    for (int i = 0; i < n; ++i) {
+      PCONV_HIP_CHECK(hipMemcpy2DAsync(din.data() + 16, static_cast<size_t>(pitch), hin.data(),
+                                       static_cast<size_t>(row_bytes), static_cast<size_t>(row_bytes),
+                                       static_cast<size_t>(rows_in), hipMemcpyHostToDevice, s1.get()));
+      PCONV_HIP_CHECK(hipMemcpy2DAsync(hout.data(), static_cast<size_t>(row_bytes), dout.data() + 16,
+                                       static_cast<size_t>(pitch), static_cast<size_t>(row_bytes),
+                                       static_cast<size_t>(rows_out), hipMemcpyDeviceToHost, s2.get()));
+    }
+    a.record(s1.get());
+    b.record(s2.get());
+    a.sync();
+    b.sync();
+    return std::max(Event::elapsed_ms(e0, a), Event::elapsed_ms(e0, b)) / n;
+  };
+  (void)pairs(2);  // warm: first-use queue / engine set-up
+  return std::min(pairs(iters), pairs(iters));
 }
 
 std::string device_name(int device) {

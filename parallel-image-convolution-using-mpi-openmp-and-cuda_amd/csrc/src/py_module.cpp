@@ -287,6 +287,9 @@ PYBIND11_MODULE(_pconv_native, m) {
   m.def("device_name", &device_name);
   m.def("set_device", &set_device);
   m.def("device_pci_bus_id", &device_pci_bus_id);
+  m.def("copy_pair_floor_ms", &copy_pair_floor_ms, py::arg("device"), py::arg("row_bytes"), py::arg("rows_in"),
+        py::arg("rows_out"), py::arg("iters") = 8,
+        "ms per pitched H2D + D2H pair issued concurrently on two streams (the pipeline's PCIe floor)");
   m.def("bind_to_device_numa", &bind_to_device_numa,
         "Restrict this process to the CPUs local to the GPU (0: unchanged; PCONV_NUMA_BIND=0 disables)");
 

@@ -318,3 +318,15 @@ def test_pipeline_split_d2h(pconv_mod, rng, slots, reps, world, rank):
     for k, img in enumerate(imgs):
         ref = pconv_mod.numpy_convolve(img, reps).reshape(h, -1)[b.y0:b.y0 + b.rows]
         assert np.array_equal(blur.outputs[k], ref), k
+
+
+def test_copy_pair_floor(native):
+    """The pipeline's PCIe floor (bench.py copy_floor.pair_ms): pitched H2D +
+    D2H issued together; positive, and a pair is no faster than either copy
+    alone could be at the link's one-way peak (64 GB/s for PCIe Gen5 x16)."""
+    rb, rows = 5760, 2520
+    ms = native.copy_pair_floor_ms(0, rb, rows, rows, 4)
+    assert 0 < ms < 100
+    assert ms >= rb * rows / 64e9 * 1e3
+    with pytest.raises(Exception):
+        native.copy_pair_floor_ms(0, rb, 0, rows, 4)
