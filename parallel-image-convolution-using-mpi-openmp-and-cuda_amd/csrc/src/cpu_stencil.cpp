@@ -26,15 +26,38 @@ inline uint8_t sat_trunc(float v) {
   return static_cast<uint8_t>(static_cast<int>(v));
 }
 
+// (Σ tap·p) >> 4 with taps [1,2,1]⊗[1,2,1]: the vertical sums of the row once
+// into a 16-bit scratch row (every sum <= 1020; the full sum <= 4080 < 2^16),
+// then the horizontal pass — two passes of 16-bit lanes the compiler
+// vectorises.  Built twice: the x86-64 baseline and an AVX2 clone picked at
+// run time (the GPU boxes' and this container's CPUs have AVX2; no -march
+// flag, so the binary still runs anywhere).
+#define PCONV_ROW_BINOMIAL_BODY                                                               \
+  for (int64_t x = -CH; x < n + CH; ++x) v[x + CH] = static_cast<uint16_t>(a[x] + 2 * b[x] + c[x]); \
+  for (int64_t x = 0; x < n; ++x)                                                             \
+    o[x] = static_cast<uint8_t>(static_cast<uint16_t>(v[x] + 2 * v[x + CH] + v[x + 2 * CH]) >> 4);
+
+template <int CH>
+void row_binomial_base(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* o, int64_t n, uint16_t* v) {
+  PCONV_ROW_BINOMIAL_BODY
+}
+
+template <int CH>
+__attribute__((target("avx2"))) void row_binomial_avx2(const uint8_t* a, const uint8_t* b, const uint8_t* c,
+                                                       uint8_t* o, int64_t n, uint16_t* v) {
+  PCONV_ROW_BINOMIAL_BODY
+}
+#undef PCONV_ROW_BINOMIAL_BODY
+
 template <int CH>
 void row_binomial(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* o, int64_t n) {
-  // (Σ tap·p) >> 4 with taps [1,2,1]⊗[1,2,1]: vertical then horizontal.
-  for (int64_t x = 0; x < n; ++x) {
-    const int l = a[x - CH] + 2 * b[x - CH] + c[x - CH];
-    const int m = a[x] + 2 * b[x] + c[x];
-    const int r = a[x + CH] + 2 * b[x + CH] + c[x + CH];
-    o[x] = static_cast<uint8_t>((l + 2 * m + r) >> 4);
-  }
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  thread_local std::vector<uint16_t> scratch;
+  if (scratch.size() < static_cast<size_t>(n + 2 * CH)) scratch.resize(static_cast<size_t>(n + 2 * CH));
+  if (avx2)
+    row_binomial_avx2<CH>(a, b, c, o, n, scratch.data());
+  else
+    row_binomial_base<CH>(a, b, c, o, n, scratch.data());
 }
 
 template <int CH>
@@ -48,20 +71,46 @@ void row_int(const Filter& f, const uint8_t* a, const uint8_t* b, const uint8_t*
   }
 }
 
+// Float filters: per output, acc = 0; acc += fl(p * w) over the nine taps in
+// row-major order (the reference's sequence, one rounding per op, no FMA:
+// -ffp-contract=off, and the AVX2 clone does not enable FMA).  Outputs are
+// independent, so vectorising across x keeps every output's order.
+#define PCONV_ROW_FLOAT_BODY                                                                  \
+  const float w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5], w6 = w[6], w7 = w[7], \
+              w8 = w[8];                                                                      \
+  for (int64_t x = 0; x < n; ++x) {                                                           \
+    float acc = 0.0f;                                                                         \
+    acc = acc + static_cast<float>(a[x - CH]) * w0;                                           \
+    acc = acc + static_cast<float>(a[x]) * w1;                                                \
+    acc = acc + static_cast<float>(a[x + CH]) * w2;                                           \
+    acc = acc + static_cast<float>(b[x - CH]) * w3;                                           \
+    acc = acc + static_cast<float>(b[x]) * w4;                                                \
+    acc = acc + static_cast<float>(b[x + CH]) * w5;                                           \
+    acc = acc + static_cast<float>(c[x - CH]) * w6;                                           \
+    acc = acc + static_cast<float>(c[x]) * w7;                                                \
+    acc = acc + static_cast<float>(c[x + CH]) * w8;                                           \
+    o[x] = sat_trunc(acc);                                                                    \
+  }
+
+template <int CH>
+void row_float_base(const float* w, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* o, int64_t n) {
+  PCONV_ROW_FLOAT_BODY
+}
+
+template <int CH>
+__attribute__((target("avx2"))) void row_float_avx2(const float* w, const uint8_t* a, const uint8_t* b,
+                                                    const uint8_t* c, uint8_t* o, int64_t n) {
+  PCONV_ROW_FLOAT_BODY
+}
+#undef PCONV_ROW_FLOAT_BODY
+
 template <int CH>
 void row_float(const Filter& f, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* o, int64_t n) {
-  const float* w = f.weights.data();
-  for (int64_t x = 0; x < n; ++x) {
-    const uint8_t* rows[3] = {a, b, c};
-    float acc = 0.0f;
-    for (int k = 0; k < 3; ++k)
-      for (int l = 0; l < 3; ++l) {
-        const float p = static_cast<float>(rows[k][x + (l - 1) * CH]);
-        const float prod = p * w[k * 3 + l];
-        acc = acc + prod;
-      }
-    o[x] = sat_trunc(acc);
-  }
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2)
+    row_float_avx2<CH>(f.weights.data(), a, b, c, o, n);
+  else
+    row_float_base<CH>(f.weights.data(), a, b, c, o, n);
 }
 
 template <int CH>
