@@ -60,15 +60,35 @@ void row_binomial(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t*
     row_binomial_base<CH>(a, b, c, o, n, scratch.data());
 }
 
+// Integer-exact custom filters (non-negative taps, power-of-two divisor).
+#define PCONV_ROW_INT_BODY                                                                          \
+  const int t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4], t5 = t[5], t6 = t[6], t7 = t[7], \
+            t8 = t[8];                                                                              \
+  for (int64_t x = 0; x < n; ++x) {                                                                 \
+    const int acc = t0 * a[x - CH] + t1 * a[x] + t2 * a[x + CH] + t3 * b[x - CH] + t4 * b[x] +       \
+                    t5 * b[x + CH] + t6 * c[x - CH] + t7 * c[x] + t8 * c[x + CH];                   \
+    o[x] = static_cast<uint8_t>(std::min(acc >> s, 255));                                            \
+  }
+
+template <int CH>
+void row_int_base(const int* t, int s, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* o, int64_t n) {
+  PCONV_ROW_INT_BODY
+}
+
+template <int CH>
+__attribute__((target("avx2"))) void row_int_avx2(const int* t, int s, const uint8_t* a, const uint8_t* b,
+                                                  const uint8_t* c, uint8_t* o, int64_t n) {
+  PCONV_ROW_INT_BODY
+}
+#undef PCONV_ROW_INT_BODY
+
 template <int CH>
 void row_int(const Filter& f, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* o, int64_t n) {
-  const int* t = f.taps.data();
-  const int s = f.shift;
-  for (int64_t x = 0; x < n; ++x) {
-    const int acc = t[0] * a[x - CH] + t[1] * a[x] + t[2] * a[x + CH] + t[3] * b[x - CH] + t[4] * b[x] +
-                    t[5] * b[x + CH] + t[6] * c[x - CH] + t[7] * c[x] + t[8] * c[x + CH];
-    o[x] = static_cast<uint8_t>(std::min(acc >> s, 255));
-  }
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2)
+    row_int_avx2<CH>(f.taps.data(), f.shift, a, b, c, o, n);
+  else
+    row_int_base<CH>(f.taps.data(), f.shift, a, b, c, o, n);
 }
 
 // Float filters: per output, acc = 0; acc += fl(p * w) over the nine taps in

@@ -117,3 +117,16 @@ def test_convolve_file_cpu(pconv_mod, tmp_path, rng):
     dst = pconv_mod.convolve_file(src, 23, 17, 4, "grey", backend="omp")
     assert dst.endswith("blur_g.raw")
     assert np.array_equal(pconv_mod.read_raw(dst, 23, 17, "grey"), pconv_mod.numpy_convolve(img, 4))
+
+
+def test_custom_int_filter_cpu_matches_oracle(pconv_mod, rng):
+    """The integer row path (int-exact custom filters, not the binomial) in
+    both CPU backends — each row kernel runs as its AVX2 clone where the CPU
+    has AVX2 — against the NumPy float32 oracle (exact for power-of-two
+    divisors)."""
+    filt = ((1, 1, 1, 1, 8, 1, 1, 1, 1), 16)
+    for shape in ((37, 53, 3), (29, 41), (16, 300, 4)):
+        img = rng.integers(0, 256, size=shape, dtype=np.uint8)
+        ref = pconv_mod.numpy_convolve(img, 3, filt)
+        for be in ("cpu", "omp"):
+            assert np.array_equal(pconv_mod.convolve(img, 3, filter=filt, backend=be), ref), (shape, be)
