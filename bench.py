@@ -112,6 +112,9 @@ def parse():
                    help="step graphs: the last fused launch stores packed rows into a device staging buffer and the "
                         "D2H is one contiguous copy (default off: a pitched 2-D copy from the frame; packed measured "
                         "slower on a box whose 2-D D2H runs at full rate, profiles/r02/raw/packed_d2h/)")
+    p.add_argument("--stream-chunks", type=int, default=0,
+                   help="rows streamed within each image: upload in this many row chunks, advance every level behind "
+                        "them, download finished rows meanwhile (H2D, reps and D2H of ONE image overlap; 0 = off)")
     p.add_argument("--d2h", choices=["sdma", "kernel"], default="sdma",
                    help="step graphs: the D2H by SDMA (pitched copy) or by a CU copy kernel")
     p.add_argument("--emulate", default=None, metavar="WORLD:RANK",
@@ -394,7 +397,7 @@ def main():
                                step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
                                zero_copy_out=a.zero_copy_out == "on", graph_capture=a.graph_capture == "on",
                                split_d2h=a.pipeline == "split", packed_out=a.packed_d2h == "on",
-                               kernel_d2h=a.d2h == "kernel")
+                               kernel_d2h=a.d2h == "kernel", stream_chunks=a.stream_chunks)
     blur.load_synthetic(a.seed)
     # --emulate-rccl: hold a (1-rank) RCCL communicator through the timed
     # region, as every real N>1 rank of the exchange path does.
@@ -521,6 +524,7 @@ def main():
                 "d2h": a.d2h,
                 "halo_depth": int(blur.engine.halo),
                 "fuse": int(blur.engine.fuse),
+                "stream_chunks": int(a.stream_chunks),
                 "preload_halo": bool(blur.preload_halo),
                 "launches_per_step": int(stats.launches),
                 "exchanges_per_step": int(stats.exchanges),

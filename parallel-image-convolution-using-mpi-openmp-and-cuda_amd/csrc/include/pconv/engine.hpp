@@ -86,6 +86,11 @@ struct EngineOptions {
   // between workgroups every `fuse` steps; kernels/stencil_resident.hip).
   // Needs the whole device: never with other kernels running concurrently.
   bool resident = false;
+  // Row streaming within one image (schedule.hpp, plan_streamed): a serving
+  // step's rows are uploaded in this many chunks and each level advances as
+  // far as the rows on the device allow, so H2D, launches and D2H of ONE
+  // image overlap on three streams.  0 / 1: whole-image chain.
+  int stream_chunks = 0;
 };
 
 struct RunStats {
@@ -164,6 +169,15 @@ class BandEngine {
   void process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps);
   // True when `reps` repetitions with / without pre-loaded ghost rows need no exchange.
   bool exchange_free(int reps, bool halo_preloaded) const;
+  // Row-streamed serving step (options().stream_chunks chunks): the plan of
+  // one image with input rows [in_r0, in_r1); empty chunks when the image
+  // cannot be streamed (exchanges, reps == 0, streaming off).
+  StreamPlan stream_plan(int reps, int64_t in_r0, int64_t in_r1) const;
+  // Enqueue a streamed image: chunk uploads on `up`, launches on the compute
+  // stream, downloads of the finished rows on `down` (cross-stream events per
+  // chunk).  The caller orders `up` after any earlier use of these frames.
+  void enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
+                        const StreamPlan& sp, hipStream_t up, hipStream_t down);
   // Phase-by-phase execution for multi-band emulation on one device.
   std::vector<Phase> plan(int reps) const;
   void exec_exchange(const Phase& p);
@@ -199,6 +213,8 @@ class BandEngine {
   Stream own_cs_, own_ms_;
   hipStream_t cs_ = nullptr, ms_ = nullptr;
   Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_;
+  Event ev_up_, ev_dn_;       // streamed images: chunk uploaded / chunk rows final
+  Stream cap_up_, cap_dn_;    // streamed step graphs: capture-only fork streams (never launched on)
   std::shared_ptr<HaloTransport> transport_;
   RunStats stats_;
   double wall_t0_ = 0;

@@ -62,6 +62,8 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
   ev_ready_ = Event::create();
   ev_halo_ = Event::create();
   ev_sync_ = Event::create();
+  ev_up_ = Event::create();
+  ev_dn_ = Event::create();
   ev_t0_ = Event::create(true);
   ev_t1_ = Event::create(true);
   PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
@@ -389,9 +391,113 @@ bool BandEngine::exchange_free(int reps, bool halo_preloaded) const {
   return true;
 }
 
+StreamPlan BandEngine::stream_plan(int reps, int64_t in_r0, int64_t in_r1) const {
+  StreamPlan sp;
+  if (opt_.stream_chunks < 2 || reps < 1) return sp;
+  PlanConfig c = engine_plan_config(geom_, band_, filter_, opt_);
+  c.halo_preloaded = input_preloaded(in_r0, in_r1);
+  const std::vector<Phase> ph = plan_band(band_, reps, c);
+  if (!streamable(ph)) return sp;
+  return plan_streamed(ph, in_r0, in_r1, band_.rows, stream_cuts(in_r0, in_r1, opt_.stream_chunks));
+}
+
+void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
+                                  const StreamPlan& sp, hipStream_t up, hipStream_t down) {
+  TraceRange tr("pconv.streamed_image");
+  PCONV_CHECK(!sp.chunks.empty(), "enqueue_streamed: empty stream plan");
+  PCONV_CHECK(sp.chunks.front().up_lo == in_r0 && sp.chunks.back().up_hi == in_r1,
+              "enqueue_streamed: plan does not match the input rows");
+  PCONV_CHECK(band_.y0 + in_r0 >= 0 && band_.y0 + in_r1 <= geom_.height && in_r0 >= -lay_.halo &&
+                  in_r1 <= lay_.rows + lay_.halo,
+              "enqueue_streamed: input rows outside frame / image");
+  const int64_t rb = lay_.row_bytes, p = lay_.pitch;
+  stats_ = RunStats{};
+  const int c0 = cur_;
+  uint8_t* in_frame = frame_at(c0);
+  const uint8_t* out_frame = frame_at(c0 + sp.levels);
+  bool joined = true;  // `down` already ordered after every launch issued so far
+  for (const auto& ch : sp.chunks) {
+    if (ch.up_hi > ch.up_lo) {
+      PCONV_HIP_CHECK(hipMemcpy2DAsync(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, rb,
+                                       ch.up_hi - ch.up_lo, hipMemcpyHostToDevice, up));
+      if (up != cs_) {
+        ev_up_.record(up);
+        ev_up_.wait_on(cs_);
+      }
+    }
+    for (size_t i = 0; i < ch.launches.size(); ++i) {
+      launch_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1, nullptr, 0),
+                     cs_, opt_.variant);
+      ++stats_.launches;
+      joined = false;
+    }
+    if (ch.down_hi > ch.down_lo && host_out) {
+      if (down != cs_) {
+        ev_dn_.record(cs_);
+        ev_dn_.wait_on(down);
+      }
+      joined = true;
+      PCONV_HIP_CHECK(hipMemcpy2DAsync(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, rb,
+                                       ch.down_hi - ch.down_lo, hipMemcpyDeviceToHost, down));
+    }
+  }
+  if (!joined && down != cs_) {
+    // Launches after the last download: `down` finishing must still mean the
+    // whole image is done (the next image of these frames waits on `down`).
+    ev_dn_.record(cs_);
+    ev_dn_.wait_on(down);
+  }
+  cur_ = (c0 + sp.levels) & 1;
+  halo_valid_ = false;
+}
+
 void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
   TraceRange tr("pconv.step_graph");
   PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
+  const StreamPlan sp = host_out ? stream_plan(reps, in_r0, in_r1) : StreamPlan{};
+  if (!sp.chunks.empty()) {
+    // Streamed image as ONE graph: uploads and downloads on two forked
+    // capture streams, launches on the compute stream, one edge per chunk
+    // between them; the graph runs on the compute stream.
+    const auto key = std::make_tuple(-reps - 1, cur_, host_in, in_r0, in_r1, host_out);
+    auto it = step_graphs_.find(key);
+    stats_ = RunStats{};
+    if (it == step_graphs_.end()) {
+      trim_graph_caches();
+      if (!cap_up_.get()) {
+        cap_up_ = Stream::create(0);
+        cap_dn_ = Stream::create(0);
+      }
+      const int c0 = cur_;
+      for (const auto& ch : sp.chunks)
+        for (size_t i = 0; i < ch.launches.size(); ++i)
+          prepare_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1, nullptr, 0),
+                          cs_, opt_.variant);
+      hipGraph_t g = nullptr;
+      PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
+      ev_ready_.record(cs_);
+      ev_ready_.wait_on(cap_up_.get());
+      ev_ready_.wait_on(cap_dn_.get());
+      enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, cap_up_.get(), cap_dn_.get());
+      ev_up_.record(cap_up_.get());
+      ev_up_.wait_on(cs_);
+      ev_dn_.record(cap_dn_.get());
+      ev_dn_.wait_on(cs_);
+      PCONV_HIP_CHECK(hipStreamEndCapture(cs_, &g));
+      StepGraph sg;
+      PCONV_HIP_CHECK(hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0));
+      PCONV_HIP_CHECK(hipGraphDestroy(g));
+      sg.end_cur = cur_;
+      sg.launches = stats_.launches;
+      it = step_graphs_.emplace(key, sg).first;
+    } else {
+      cur_ = it->second.end_cur;
+      stats_.launches = it->second.launches;
+    }
+    PCONV_HIP_CHECK(hipGraphLaunch(it->second.exec, cs_));
+    halo_valid_ = false;
+    return;
+  }
   halo_valid_ = input_preloaded(in_r0, in_r1);
   std::vector<Phase> ph = plan(reps);
   bool exchanges = false;
@@ -661,6 +767,19 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   const bool preloaded = e.input_preloaded(in_r0, in_r1);
   // H2D into slot k once its previous image has been downloaded.
   if (used_[k]) ev_free_[k].wait_on(h2d_.get());
+  if (e.options().stream_chunks > 1 && trace_ev_.empty()) {
+    // Rows streamed within the image: chunk uploads on the H2D stream,
+    // launches on the compute stream, finished rows downloaded on the D2H
+    // stream, one event pair per chunk (exchange-free images only).
+    const StreamPlan sp = e.stream_plan(reps, in_r0, in_r1);
+    if (!sp.chunks.empty()) {
+      e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, h2d_.get(), d2h_.get());
+      ev_free_[k].record(d2h_.get());
+      used_[k] = true;
+      ++count_;
+      return;
+    }
+  }
   trace_mark(0, h2d_.get());
   e.upload_rows(host_in, e.layout().row_bytes, in_r0, in_r1, h2d_.get());
   trace_mark(1, h2d_.get());

@@ -170,6 +170,20 @@ PYBIND11_MODULE(_pconv_native, m) {
       py::arg("halo_depth"), py::arg("fuse"), py::arg("min_band_rows"), py::arg("max_fuse") = kMaxFusedSteps);
   m.def("describe_plan", &describe_plan);
   m.attr("MAX_FUSED_STEPS") = kMaxFusedSteps;
+  py::class_<StreamChunk>(m, "StreamChunk")
+      .def_readonly("up_lo", &StreamChunk::up_lo)
+      .def_readonly("up_hi", &StreamChunk::up_hi)
+      .def_readonly("launches", &StreamChunk::launches)
+      .def_readonly("levels", &StreamChunk::levels)
+      .def_readonly("down_lo", &StreamChunk::down_lo)
+      .def_readonly("down_hi", &StreamChunk::down_hi);
+  py::class_<StreamPlan>(m, "StreamPlan")
+      .def_readonly("levels", &StreamPlan::levels)
+      .def_readonly("chunks", &StreamPlan::chunks);
+  m.def("streamable", &streamable, py::arg("plan"));
+  m.def("stream_cuts", &stream_cuts, py::arg("in_lo"), py::arg("in_hi"), py::arg("chunks"));
+  m.def("plan_streamed", &plan_streamed, py::arg("plan"), py::arg("in_lo"), py::arg("in_hi"), py::arg("owned_rows"),
+        py::arg("cuts"));
 
   // ---------------------------------------------------------------- CPU oracle
   m.def(
@@ -420,8 +434,9 @@ PYBIND11_MODULE(_pconv_native, m) {
   py::class_<BandEngine>(m, "BandEngine")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, bool graph, const std::string& variant,
-                       bool kernel_copies, bool resident) {
+                       bool kernel_copies, bool resident, int stream_chunks) {
              EngineOptions o;
+             o.stream_chunks = stream_chunks;
              o.kernel_copies = kernel_copies;
              o.resident = resident;
              o.device = device;
@@ -436,8 +451,9 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
            py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
            py::arg("overlap") = true, py::arg("graph") = false, py::arg("variant") = "auto",
-           py::arg("kernel_copies") = false, py::arg("resident") = false)
+           py::arg("kernel_copies") = false, py::arg("resident") = false, py::arg("stream_chunks") = 0)
       .def_property_readonly("band", &BandEngine::band)
+      .def("stream_plan", &BandEngine::stream_plan, py::arg("reps"), py::arg("in_r0"), py::arg("in_r1"))
       .def_property_readonly("halo", [](const BandEngine& e) { return e.layout().halo; })
       .def_property_readonly("fuse", [](const BandEngine& e) { return e.options().fuse; })
       .def_property_readonly("cached_graphs", &BandEngine::cached_graphs)
@@ -560,8 +576,9 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
                        int concurrent, bool graphs, bool zero_copy_out, bool step_graphs, bool split_d2h,
-                       bool packed_out, bool kernel_d2h, py::object band, bool slot_comm) {
+                       bool packed_out, bool kernel_d2h, py::object band, bool slot_comm, int stream_chunks) {
              EngineOptions o;
+             o.stream_chunks = stream_chunks;
              o.zero_copy_out = zero_copy_out;
              o.packed_out = packed_out;
              o.kernel_d2h = kernel_d2h;
@@ -581,7 +598,7 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1,
            py::arg("graphs") = false, py::arg("zero_copy_out") = false, py::arg("step_graphs") = true,
            py::arg("split_d2h") = false, py::arg("packed_out") = false, py::arg("kernel_d2h") = false,
-           py::arg("band") = py::none(), py::arg("slot_comm") = false)
+           py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",

@@ -62,6 +62,82 @@ std::vector<Phase> plan_band(const Band& band, int reps, const PlanConfig& cfg) 
   return plan;
 }
 
+bool streamable(const std::vector<Phase>& plan) {
+  if (plan.empty()) return false;
+  for (const auto& p : plan)
+    if (p.exchange_depth > 0 || p.launches.size() != 1) return false;
+  return true;
+}
+
+std::vector<int64_t> stream_cuts(int64_t in_lo, int64_t in_hi, int chunks) {
+  const int64_t n = in_hi - in_lo;
+  chunks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(chunks, n)));
+  std::vector<int64_t> cuts;
+  if (chunks <= 1) return cuts;
+  // weights 1, 2, ..., 2, 1 (two chunks: 1, 1)
+  const int64_t total = chunks == 2 ? 2 : 2 * (chunks - 1);
+  int64_t acc = 0;
+  for (int c = 0; c + 1 < chunks; ++c) {
+    acc += (c == 0 || chunks == 2) ? 1 : 2;
+    const int64_t cut = in_lo + (n * acc) / total;
+    if (cut > in_lo && cut < in_hi && (cuts.empty() || cut > cuts.back())) cuts.push_back(cut);
+  }
+  return cuts;
+}
+
+StreamPlan plan_streamed(const std::vector<Phase>& plan, int64_t in_lo, int64_t in_hi, int64_t owned_rows,
+                         const std::vector<int64_t>& cuts) {
+  PCONV_CHECK(streamable(plan), "plan_streamed: the plan must be exchange-free with one launch per phase");
+  PCONV_CHECK(in_lo <= 0 && in_hi >= owned_rows && in_lo < in_hi, "plan_streamed: input rows must cover the band");
+  for (size_t i = 0; i < cuts.size(); ++i)
+    PCONV_CHECK(cuts[i] > in_lo && cuts[i] < in_hi && (i == 0 || cuts[i] > cuts[i - 1]),
+                "plan_streamed: cuts must increase strictly inside the input rows");
+  const int L = static_cast<int>(plan.size());
+  std::vector<int64_t> lo(L + 1), hi(L + 1);
+  std::vector<int> s(L + 1, 0);
+  lo[0] = in_lo;
+  hi[0] = in_hi;
+  for (int j = 1; j <= L; ++j) {
+    const LaunchSpec& l = plan[j - 1].launches[0];
+    lo[j] = l.lo;
+    hi[j] = l.hi;
+    s[j] = l.steps;
+  }
+  PCONV_CHECK(lo[L] <= 0 && hi[L] >= owned_rows, "plan_streamed: the last level must cover the owned rows");
+  StreamPlan sp;
+  sp.levels = L;
+  std::vector<int64_t> front(lo);  // W_j(c-1): first row of level j not yet computed
+  front[0] = in_lo;
+  const size_t C = cuts.size() + 1;
+  for (size_t c = 0; c < C; ++c) {
+    const bool last = c + 1 == C;
+    StreamChunk ch;
+    ch.up_lo = front[0];
+    ch.up_hi = last ? in_hi : cuts[c];
+    std::vector<int64_t> w(L + 1);
+    w[0] = ch.up_hi;
+    for (int j = 1; j <= L; ++j) {
+      int64_t wj;
+      if (last || w[j - 1] >= hi[j - 1])
+        wj = hi[j];
+      else
+        wj = std::min(hi[j], w[j - 1] - std::max(s[j], s[j - 1]));
+      wj = std::max(wj, front[j]);
+      w[j] = wj;
+      if (wj > front[j]) {
+        ch.launches.push_back({s[j], front[j], wj, false});
+        ch.levels.push_back(j);
+      }
+    }
+    ch.down_lo = std::max<int64_t>(0, front[L]);
+    ch.down_hi = std::min(owned_rows, w[L]);
+    if (ch.down_hi < ch.down_lo) ch.down_hi = ch.down_lo;
+    for (int j = 0; j <= L; ++j) front[j] = w[j];
+    sp.chunks.push_back(std::move(ch));
+  }
+  return sp;
+}
+
 std::string describe_plan(const std::vector<Phase>& plan) {
   std::ostringstream os;
   for (size_t i = 0; i < plan.size(); ++i) {

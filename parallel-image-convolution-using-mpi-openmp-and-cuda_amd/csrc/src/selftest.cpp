@@ -27,6 +27,10 @@ constexpr int kCrashSignals[] = {SIGSEGV, SIGBUS, SIGILL, SIGFPE, SIGABRT};
 struct sigaction g_prev[sizeof(kCrashSignals) / sizeof(int)];
 bool g_installed = false;
 int g_fds[2] = {2, -1};  // stderr, and PCONV_CRASH_LOG when set (test runners capture fd 2)
+// PCONV_CRASH_LOG's path, copied at install time: the file is opened only
+// when a signal arrives (open(2) is async-signal-safe), so a process that
+// never crashes leaves no empty log behind.
+char g_log_path[1024] = {0};
 
 void write_str(const char* s) {
   for (int fd : g_fds)
@@ -57,6 +61,7 @@ const char* signal_name(int sig) {
 void on_fatal(int sig, siginfo_t* info, void* uctx) {
   // Only async-signal-safe calls up to backtrace (backtrace() itself may
   // allocate on first use: it is primed in install_crash_handler).
+  if (g_log_path[0] && g_fds[1] < 0) g_fds[1] = ::open(g_log_path, O_WRONLY | O_CREAT | O_APPEND, 0644);
   write_str("\n[pconv] fatal signal ");
   char num[8];
   int k = 0, v = sig;
@@ -98,7 +103,10 @@ void install_crash_handler() {
   if (g_installed) return;
   // A copy of the report to a file: a test runner that captures fd 2 drops
   // what a dying process wrote there (faulthandler writes to a saved fd).
-  if (const char* p = std::getenv("PCONV_CRASH_LOG")) g_fds[1] = ::open(p, O_WRONLY | O_CREAT | O_APPEND, 0644);
+  if (const char* p = std::getenv("PCONV_CRASH_LOG")) {
+    std::strncpy(g_log_path, p, sizeof(g_log_path) - 1);
+    g_log_path[sizeof(g_log_path) - 1] = '\0';
+  }
   void* prime[2];
   (void)backtrace(prime, 2);  // loads libgcc's unwinder outside the handler
   // An alternate stack: a stack overflow must still be reported.

@@ -59,7 +59,8 @@ class DistributedBlur:
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
                  step_graphs: Optional[bool] = None, zero_copy_out: bool = False, graph_capture: bool = True,
                  slot_exchange: bool = False, split_d2h: bool = False, packed_out: bool = False,
-                 kernel_d2h: bool = False, self_neighbours: bool = False, slot_comm: bool = False):
+                 kernel_d2h: bool = False, self_neighbours: bool = False, slot_comm: bool = False,
+                 stream_chunks: int = 0):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -72,8 +73,11 @@ class DistributedBlur:
             fuse = n.auto_fuse(nf, variant, self.width * ch * (self.height // max(1, self.world)), ch)
         if halo is None:
             halo = auto_halo(self.height, self.world, reps, fuse, preload=bool(preload_halo) and not slot_exchange)
+        # stream_chunks > 1: each exchange-free image's rows are uploaded in
+        # that many chunks and its levels advance behind them (H2D, launches
+        # and D2H of ONE image overlap; schedule.hpp plan_streamed)
         kw = dict(halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant, slots=int(slots),
-                  concurrent=int(concurrent))
+                  concurrent=int(concurrent), stream_chunks=int(stream_chunks))
         if self_neighbours:
             # One-GPU emulation of rank `rank` of a `world`-way split whose halos
             # really move: its neighbours are replaced by itself (a 1-rank

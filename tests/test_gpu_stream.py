@@ -1,0 +1,92 @@
+"""Row streaming within one image on the GPU (EngineOptions::stream_chunks).
+
+Each image's rows are uploaded in chunks and every level advances behind
+them (schedule.hpp plan_streamed); H2D, launches and D2H of one image run on
+three streams.  Both pipeline forms are checked bit-exact against the NumPy
+oracle (tests/test_stream_plan.py checks the plans themselves on the CPU):
+  * graph: every image ONE captured hipGraph (uploads / downloads on forked
+    capture streams), slots on their own streams;
+  * direct: shared H2D / compute / D2H streams, one event pair per chunk.
+Output buffers are pre-filled with junk so a row never downloaded shows up.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CH = {"grey": 1, "rgb": 3, "rgba": 4}
+
+
+def _blur(w, h, ch, filt, reps, chunks, graph, slots=2, **kw):
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    return DistributedBlur(w, h, ch, filt, reps, device=0, slots=slots, stream_chunks=chunks,
+                           step_graphs=graph, graph_capture=graph, **kw)
+
+
+def _run_images(pconv_mod, rng, blur, w, h, ch, filt, reps, rounds=2):
+    c = CH[ch]
+    b = blur.band
+    for rnd in range(rounds):
+        imgs = [rng.integers(0, 256, size=(h, w, c), dtype=np.uint8) for _ in range(blur.slots)]
+        ks = []
+        for img in imgs:
+            k = blur._next
+            blur.load_image(img, slot=k)
+            blur.outputs[k][:] = 0xAB
+            ks.append(blur.submit(reps))
+        blur.drain()
+        for img, k in zip(imgs, ks):
+            ref = pconv_mod.numpy_convolve(img if c > 1 else img[..., 0], reps, filt).reshape(h, -1)
+            got = blur.outputs[k].reshape(b.rows, -1)
+            assert np.array_equal(got, ref[b.y0:b.y0 + b.rows]), (rnd, k)
+
+
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("chunks", [2, 3, 5, 8])
+@pytest.mark.parametrize("w,h,ch,reps", [(67, 45, "rgb", 9), (64, 133, "grey", 40), (50, 71, "rgba", 13),
+                                         (1920, 252, "rgb", 40)])
+def test_streamed_pipeline_bit_exact(pconv_mod, rng, graph, chunks, w, h, ch, reps):
+    blur = _blur(w, h, ch, "gaussian", reps, chunks, graph)
+    assert blur.pipe.graphs == graph
+    sp = blur.engine.stream_plan(reps, 0, h)
+    assert len(sp.chunks) == min(chunks, h) and sp.levels == len(blur.plan(reps))
+    _run_images(pconv_mod, rng, blur, w, h, ch, "gaussian", reps)
+    assert blur.stats.launches >= sp.levels
+
+
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("filt", ["box", "edge"])
+def test_streamed_float_filters(pconv_mod, rng, graph, filt):
+    _run_images(pconv_mod, rng, _blur(59, 83, "rgb", filt, 11, 4, graph), 59, 83, "rgb", filt, 11)
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_streamed_reps_exceed_chunks(pconv_mod, rng, graph):
+    """More repetitions than rows per chunk (the last level lags several
+    chunks behind the uploads), an odd height and a last launch of 1 step."""
+    _run_images(pconv_mod, rng, _blur(33, 37, "grey", "gaussian", 41, 9, graph), 33, 37, "grey", "gaussian", 41)
+
+
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("world,rank", [(2, 0), (3, 1), (4, 3), (8, 5)])
+def test_streamed_preloaded_bands(pconv_mod, rng, graph, world, rank):
+    """A rank's band with pre-loaded ghost rows (the N>1 headline) streamed:
+    the ghost rows travel with the first / last chunks."""
+    w, h, reps = 61, 400, 40
+    blur = _blur(w, h, "rgb", "gaussian", reps, 3, graph, rank=rank, world=world, preload_halo=True,
+                 transport="none")
+    _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps)
+
+
+def test_streamed_step_and_reps_zero(pconv_mod, rng):
+    """blur.step (one image alone) and reps = 0 (nothing to stream: the
+    whole-image path) through a streaming pipeline."""
+    w, h = 40, 30
+    blur = _blur(w, h, "rgb", "gaussian", 7, 4, True)
+    img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+    blur.load_image(img)
+    assert np.array_equal(blur.step(7).reshape(h, w, 3), pconv_mod.numpy_convolve(img, 7))
+    assert len(blur.engine.stream_plan(0, 0, h).chunks) == 0
+    assert np.array_equal(blur.step(0).reshape(h, w, 3), img)
+    assert np.array_equal(blur.step(7).reshape(h, w, 3), pconv_mod.numpy_convolve(img, 7))
