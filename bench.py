@@ -149,30 +149,43 @@ def parse():
                    help="after the timed region, time the stages of IMAGES more images (needs a directly issued "
                         "pipeline: --graph-capture off or --step-graphs off) and write them to --trace-out")
     p.add_argument("--trace-out", default="gpurun_out/pipeline_trace.json")
-    p.add_argument("--check", action="store_true",
-                   help="after timing, verify every rank's band against the CPU oracle (not timed)")
+    p.add_argument("--check", dest="check", action="store_true", default=True,
+                   help="after timing (outside the timed region), compare every rank's newest image, and every halo "
+                        "mode's at N>1, with the CPU oracle; 'mismatches' in the JSON line (default on)")
+    p.add_argument("--no-check", dest="check", action="store_false", help="skip the oracle check (sweeps)")
     return p.parse_args()
 
 
-def check_bands(blur, a) -> int:
-    """Compare the newest image of every rank with the native OpenMP oracle on
-    the whole synthetic image; returns the total mismatching bytes (all ranks)."""
+def oracle_rows(a, band):
+    """The CPU oracle (native OpenMP stencil, bit-exact with the reference's
+    float32) for this rank's owned rows: the synthetic image rows of the
+    band's dependency cone [y0 - reps, y0 + rows + reps) (clipped to the
+    image) convolved `reps` times; an artificial edge of the cone moves one
+    row per repetition, so the owned rows are exact without convolving the
+    whole image on every rank."""
     import numpy as np
 
     from pconv._native import require_native
     from pconv.models.filters import get_filter
-    from pconv.parallel.bootstrap import sum_over_ranks
 
     n = require_native()
-    full = np.empty(a.width * a.height * {"grey": 1, "rgb": 3, "rgba": 4}[a.channels], np.uint8)
-    n.synth_rows(full, a.width, a.height, a.channels, int(a.seed), 0, a.height)
-    ref = np.empty_like(full)
-    n.cpu_convolve(full, ref, a.width, a.height, a.channels, a.reps, get_filter(a.filter).to_native(), True, 0)
-    ref = ref.reshape(a.height, -1)
-    b = blur.band
-    out = blur.step(a.reps)
-    bad = int(np.count_nonzero(out != ref[b.y0:b.y0 + b.rows]))
-    return int(sum_over_ranks(bad))
+    c = {"grey": 1, "rgb": 3, "rgba": 4}[a.channels]
+    lo, hi = max(0, band.y0 - a.reps), min(a.height, band.y0 + band.rows + a.reps)
+    sub = np.empty((hi - lo) * a.width * c, np.uint8)
+    n.synth_rows(sub, a.width, a.height, a.channels, int(a.seed), lo, hi - lo)
+    ref = np.empty_like(sub)
+    n.cpu_convolve(sub, ref, a.width, hi - lo, a.channels, a.reps, get_filter(a.filter).to_native(), True, 0)
+    return ref.reshape(hi - lo, -1)[band.y0 - lo:band.y0 - lo + band.rows]
+
+
+def mismatching_bytes(got, ref) -> int:
+    """Bytes of this rank's newest image that differ from the oracle, summed
+    over ranks (every rank must call it)."""
+    import numpy as np
+
+    from pconv.parallel.bootstrap import sum_over_ranks
+
+    return int(sum_over_ranks(int(np.count_nonzero(got.reshape(ref.shape) != ref))))
 
 
 def gather_floats(v: float):
@@ -222,11 +235,12 @@ def mode_kwargs(a, mode: str, fuse: int) -> dict:
     return kw
 
 
-def measure_mode(a, mode, ref_rows, world, rank, device, transport, fuse):
+def measure_mode(a, mode, ref_rows, world, rank, device, transport, fuse, oracle=None):
     """Time K steps of one halo mode exactly like the headline (barrier +
     device sync on both sides, max over ranks) and compare its newest image
-    with the headline's bytes.  Never raises: a failure is reported in the
-    returned dict (status), and every rank tears the pipeline down."""
+    with the headline's bytes and (when checking) with the CPU oracle.  Never
+    raises: a failure is reported in the returned dict (status), and every
+    rank tears the pipeline down."""
     import gc
 
     import numpy as np
@@ -248,6 +262,8 @@ def measure_mode(a, mode, ref_rows, world, rank, device, transport, fuse):
         elapsed, mine = timed_steps(xb, a.steps, a.reps, a.exchange_timeout)
         got = xb.step(a.reps)
         bad = sum_over_ranks(int(np.count_nonzero(got != ref_rows)))
+        if oracle is not None:
+            res["mismatches"] = mismatching_bytes(got, oracle)
         per_rank = gather_floats(mine)
         st = xb.stats
         px = a.width * a.height * a.reps
@@ -425,7 +441,13 @@ def main():
     elapsed = max_over_ranks(mine)
     per_rank = gather_floats(mine)  # diagnostics: load balance across ranks
     stats = blur.stats
-    mismatches = check_bands(blur, a) if a.check else None
+    # ---- oracle check of the newest image (not timed): every rank compares
+    # its owned rows with the CPU oracle of its dependency cone.  Not with
+    # --emulate-halo: a self-neighbour rank's ghost rows are its own rows.
+    oracle = None
+    if a.check and not (a.emulate and a.emulate_halo != "preload"):
+        oracle = oracle_rows(a, blur.band)
+    mismatches = mismatching_bytes(blur.step(a.reps), oracle) if oracle is not None else None
     if a.trace:
         blur.pipe.enable_trace(a.trace)
         for _ in range(a.trace):
@@ -550,6 +572,8 @@ def main():
         }
         if mismatches is not None:
             out["mismatches"] = mismatches
+            out["check"] = "newest image of every rank vs the CPU oracle (OpenMP, bit-exact float32 semantics), " \
+                           "after the timed region"
         if a.emulate:
             out["emulated"] = f"rank {rank} of a {a.emulate.split(':')[0]}-way split on one GPU; value = this " \
                               "rank's step rate x full-image pixels (proxy, not a multi-GPU measurement)"
@@ -588,6 +612,8 @@ def main():
                 "status": "ok", "transport": head_transport, "ms_per_step": out["ms_per_step"],
                 "value": out["value"], "halo_depth": out["config"]["halo_depth"],
                 "exchanges_per_step": out["config"]["exchanges_per_step"]}
+            if "mismatches" in out:
+                results[out["config"]["halo_mode"]]["mismatches"] = out["mismatches"]
 
         def expire():
             if state["out"] is not None:
@@ -596,10 +622,13 @@ def main():
                 if pending["mode"]:
                     hm[pending["mode"]] = {"transport": transport, "status": "watchdog timeout"}
                 line["halo_modes"] = hm
+                line["watchdog"] = "fired: a halo-mode measurement stalled (exit status 3)"
                 emit(line)
             sys.stdout.flush()
             sys.stderr.flush()
-            os._exit(0)
+            # the headline line is out, but a stalled exchange is a failure the
+            # caller must see: exit non-zero (no restart, no exec)
+            os._exit(3)
 
         dog = threading.Timer(a.watchdog if a.watchdog is not None else
                               len(modes) * (a.exchange_timeout + 10.0) + 30.0, expire)
@@ -608,7 +637,7 @@ def main():
         ref_rows = blur.step(a.reps).copy()
         for m in modes:
             pending["mode"] = m
-            r = measure_mode(a, m, ref_rows, world, rank, device, transport, int(blur.engine.fuse))
+            r = measure_mode(a, m, ref_rows, world, rank, device, transport, int(blur.engine.fuse), oracle)
             pending["mode"] = None
             if out is not None:
                 results[m] = r
@@ -616,8 +645,11 @@ def main():
         # numbers, so they agree; rank 0 reports.
         if out is not None:
             head_ms = out["ms_per_step"]
+            # a mode qualifies only when bit-exact: against the oracle when the
+            # check ran, and byte-equal with the headline pipeline in any case
             ok = {m: r for m, r in results.items()
-                  if m != head_mode and r.get("status") == "ok" and r.get("mismatches_vs_headline") == 0}
+                  if m != head_mode and r.get("status") == "ok" and r.get("mismatches_vs_headline") == 0
+                  and r.get("mismatches", 0) == 0}
             forced = a.halo_select if a.halo_select not in ("auto", "off") else None
             if forced == "exchange":
                 forced = "slot_exchange"
@@ -652,10 +684,8 @@ def main():
                 pre = results[head_mode]
                 for k in ("latency_ms", "loop_only"):
                     pre[k] = adopted.pop(k)
-                if "mismatches" in adopted:
-                    # oracle check of the pre-loaded pipeline + 0 bytes between the two pipelines
-                    adopted["mismatches"] = out["mismatches"]
-                    adopted["mismatches_basis"] = f"{head_mode} vs CPU oracle, {pick} vs {head_mode} byte-equal"
+                if "mismatches" in r:
+                    adopted["mismatches"] = r["mismatches"]  # the adopted mode's own oracle check
                 out = adopted
             out["halo_select"] = {"mode": pick or head_mode, "reason": why,
                                   "candidates": {m: results[m].get("ms_per_step") for m in results}}
