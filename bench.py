@@ -92,11 +92,7 @@ def parse():
     p.add_argument("--loop-steps", type=int, default=None, help="timed device-resident loops (default = --steps)")
     p.add_argument("--variant", default="auto")
     p.add_argument("--seed", type=int, default=1234)
-    p.add_argument("--slots", type=int, default=None,
-                   help="images in flight (default 3; 4 engines with --pipeline split)")
-    p.add_argument("--pipeline", choices=["slots", "split"], default="slots",
-                   help="slots: each image's H2D + reps + D2H is one graph on its slot's stream; split: H2D + reps "
-                        "on one of slots/2 compute streams, the D2H on a shared copy stream")
+    p.add_argument("--slots", type=int, default=None, help="images in flight (default 3)")
     p.add_argument("--concurrent", choices=["auto", "on", "off"], default="off",
                    help="one compute stream per image in flight (default: one shared compute stream)")
     p.add_argument("--transport", choices=["rccl", "gloo-host"], default="rccl",
@@ -105,18 +101,9 @@ def parse():
                    help="one hipGraph per image (H2D + reps + D2H) on per-slot streams (auto: when exchange-free)")
     p.add_argument("--graph-capture", choices=["on", "off"], default="on",
                    help="slot-stream pipeline: capture each image as a hipGraph (on) or issue directly (off)")
-    p.add_argument("--zero-copy-out", choices=["on", "off"], default="off",
-                   help="step graphs: the last fused launch stores the result straight into pinned host memory "
-                        "(measured slower than the SDMA D2H copy: 0.41 vs 0.32 ms/step at N=1)")
-    p.add_argument("--packed-d2h", choices=["on", "off"], default="off",
-                   help="step graphs: the last fused launch stores packed rows into a device staging buffer and the "
-                        "D2H is one contiguous copy (default off: a pitched 2-D copy from the frame; packed measured "
-                        "slower on a box whose 2-D D2H runs at full rate, profiles/r02/raw/packed_d2h/)")
     p.add_argument("--stream-chunks", type=int, default=0,
                    help="rows streamed within each image: upload in this many row chunks, advance every level behind "
                         "them, download finished rows meanwhile (H2D, reps and D2H of ONE image overlap; 0 = off)")
-    p.add_argument("--d2h", choices=["sdma", "kernel"], default="sdma",
-                   help="step graphs: the D2H by SDMA (pitched copy) or by a CU copy kernel")
     p.add_argument("--emulate", default=None, metavar="WORLD:RANK",
                    help="time ONE rank of a WORLD-way split on this GPU (pre-loaded halos, no peers): a "
                         "single-GPU proxy of the per-rank step; reported as emulated, never as the headline")
@@ -355,7 +342,7 @@ def copy_floor_ms(in_bytes: int, out_bytes: int, device: int, iters: int = 8):
 def main():
     a = parse()
     if a.slots is None:
-        a.slots = 4 if a.pipeline == "split" else 3
+        a.slots = 3
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not a.emulate:
         sys.exit(spawn_ranks(a))
     # One hardware queue per stream of the serving pipeline (H2D, D2H, comm and
@@ -411,9 +398,7 @@ def main():
                                preload_halo=a.preload_halo, slots=a.slots, variant=a.variant,
                                transport=head_transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
                                step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
-                               zero_copy_out=a.zero_copy_out == "on", graph_capture=a.graph_capture == "on",
-                               split_d2h=a.pipeline == "split", packed_out=a.packed_d2h == "on",
-                               kernel_d2h=a.d2h == "kernel", stream_chunks=a.stream_chunks)
+                               graph_capture=a.graph_capture == "on", stream_chunks=a.stream_chunks)
     blur.load_synthetic(a.seed)
     # --emulate-rccl: hold a (1-rank) RCCL communicator through the timed
     # region, as every real N>1 rank of the exchange path does.
@@ -540,10 +525,6 @@ def main():
                 "concurrent_images": bool(blur.pipe.concurrent),
                 "slot_streams": bool(blur.pipe.graphs),
                 "step_graphs": bool(blur.pipe.step_graphs),
-                "split_d2h": bool(blur.pipe.split_d2h),
-                "zero_copy_out": bool(blur.pipe.graphs) and a.zero_copy_out == "on",
-                "packed_d2h": bool(blur.pipe.step_graphs) and a.packed_d2h == "on" and a.zero_copy_out != "on",
-                "d2h": a.d2h,
                 "halo_depth": int(blur.engine.halo),
                 "fuse": int(blur.engine.fuse),
                 "stream_chunks": int(a.stream_chunks),
@@ -677,8 +658,7 @@ def main():
                                          launches_per_step=r["launches_per_step"],
                                          exchanges_per_step=r["exchanges_per_step"], images_in_flight=a.slots,
                                          slot_streams=r["slot_streams"], step_graphs=r["step_graphs"],
-                                         concurrent_images=r["concurrent_images"], zero_copy_out=False,
-                                         packed_d2h=False, split_d2h=False)
+                                         concurrent_images=r["concurrent_images"], stream_chunks=0)
                 # fields measured on the pre-loaded pipeline move under its entry: every top-level
                 # field describes the reported pipeline
                 pre = results[head_mode]

@@ -61,31 +61,11 @@ struct EngineOptions {
   // hipEvent loop timing around every run() (two event records, ~3 us of
   // host time each on ROCm 7: the serving pipeline turns it off).
   bool timing = true;
-  // process_graph(): the image's last launch stores its rows straight into
-  // the pinned host output (zero-copy D2H fused into the producing kernel)
-  // instead of a separate D2H copy — when the filter / row size allow it.
-  bool zero_copy_out = false;
-  // process_graph() without zero-copy: the image's last launch stores its
-  // rows PACKED (pitch = row bytes) into a device staging buffer and the D2H
-  // is one contiguous copy.  For boxes whose pitched (2-D) D2H is slow
-  // (12-35 GB/s against 45-54 contiguous on one measured box); on a box
-  // without that problem it measured slower (N=1 0.41-0.42 vs 0.33-0.38 ms,
-  // 8-way rank 0.069 vs 0.059 ms: profiles/r02/raw/packed_d2h/), so off.
-  bool packed_out = false;
   // Host <-> frame copies (upload_rows / download_rows) and the initial frame
   // zeroing by kernels of this library instead of SDMA / the runtime's blit
   // programs: a one-shot process (the `conv` CLI) skips their first-use
   // set-up; the serving pipeline keeps SDMA (faster per byte, frees the CUs).
   bool kernel_copies = false;
-  // D2H only by a CU copy kernel (H2D stays on SDMA): an SDMA H2D beside a
-  // kernel D2H keeps both directions at full rate even on boxes whose pitched
-  // SDMA D2H is slow (tools/ubench/copy_bw.hip "SDMA H2D + zero-copy D2H").
-  bool kernel_d2h = false;
-  // run() of a single-band gaussian frame small enough for one workgroup per
-  // CU: all repetitions in ONE register-resident launch (halo rings exchanged
-  // between workgroups every `fuse` steps; kernels/stencil_resident.hip).
-  // Needs the whole device: never with other kernels running concurrently.
-  bool resident = false;
   // Row streaming within one image (schedule.hpp, plan_streamed): a serving
   // step's rows are uploaded in this many chunks and each level advances as
   // far as the rows on the device allow, so H2D, launches and D2H of ONE
@@ -226,18 +206,7 @@ class BandEngine {
     int end_cur = 0;
     int launches = 0;
     int exchanges = 0;
-    bool zero_copy = false;
-    bool packed = false;
   };
-  DeviceBuffer stage_;  // packed_out: the last launch's packed rows
-  // resident run(): plan (once), per-workgroup flags, epoch, error word
-  bool run_resident(int reps);
-  bool rplan_done_ = false;
-  ResidentPlan rplan_;
-  DeviceBuffer rflags_;
-  PinnedBuffer rerr_;
-  uint32_t repoch_ = 1;
-  bool resident_pending_ = false;
   // (reps, start buffer, in, in_r0, in_r1, out) -> whole-step graph.  Keyed
   // on host pointers, so both caches are bounded: past kMaxCachedGraphs
   // entries the stream is drained and the cache is emptied.
@@ -261,14 +230,6 @@ class BandPipeline {
   // stream-ordered, no cross-stream events) — slots overlap each other; needs
   // exchange-free images.  step_graphs: each such image is one cached hipGraph
   // (one host call), otherwise its copies and launches are issued directly.
-  // split_d2h (needs slot_streams + step_graphs; `slots` engines, an even
-  // number): each image's graph holds only its H2D and repetitions, on one of
-  // slots/2 compute streams (two engines alternate on each); its D2H runs on
-  // a shared copy stream after an event.  A compute stream then uploads and
-  // computes the next image while the previous one still downloads — the
-  // per-stream serial chain is H2D + reps instead of H2D + reps + D2H, with
-  // one more busy queue (slots/2 + 1 in total).  Engine reuse waits for that
-  // engine's previous download (events), so no frame is overwritten early.
   // slot_comm (slot-stream mode): every slot also gets its own
   // communication stream and keeps opt.overlap, so an exchange phase splits
   // into the interior launch on the slot stream ‖ the exchange on its comm
@@ -276,8 +237,7 @@ class BandPipeline {
   // image (the reference's Isend/inner/Wait/edges loop for every phase) is
   // ONE graph with a fork/join per exchange.
   BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt, int slots,
-               int concurrent = -1, bool slot_streams = false, bool step_graphs = true, bool split_d2h = false,
-               bool slot_comm = false);
+               int concurrent = -1, bool slot_streams = false, bool step_graphs = true, bool slot_comm = false);
   ~BandPipeline();
   int slots() const { return static_cast<int>(slots_.size()); }
   BandEngine& slot(int i) { return *slots_.at(i); }
@@ -297,7 +257,6 @@ class BandPipeline {
   bool concurrent() const { return concurrent_; }
   bool graphs() const { return graphs_; }
   bool step_graphs() const { return graphs_ && step_graphs_; }
-  bool split_d2h() const { return split_d2h_; }
   // Stage timeline of the next `images` submits (not with captured step
   // graphs): per image {slot, H2D start, H2D end, reps end, D2H end} in ms
   // from the first image's H2D start, read after drain().  Timing events
@@ -313,8 +272,6 @@ class BandPipeline {
   bool concurrent_ = false;
   bool graphs_ = false;  // slot-stream mode
   bool step_graphs_ = true;
-  bool split_d2h_ = false;
-  std::vector<Event> ev_done_split_, ev_freed_;  // per engine: graph done / its D2H done
   std::vector<std::unique_ptr<BandEngine>> slots_;
   std::vector<Event> ev_up_, ev_done_, ev_free_, ev_halo_;
   std::vector<bool> used_;

@@ -52,7 +52,6 @@ enum class KernelVariant : int {
   Float9 = 4,    // generic float32 9-tap (reference rounding)
   TemporalPk = 5,  // packed-u16 (VOP3P) fused gaussian, kept for A/B measurements
   FloatTemporal = 6,  // any 3x3 filter, float32 reference rounding, `steps` fused in registers
-  Mfma = 7,           // prototype: one gaussian step on a grey frame as two banded f16 MFMA products
 };
 
 const char* kernel_variant_name(KernelVariant v);
@@ -76,8 +75,6 @@ void launch_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a,
 // graph capture); clear the cache of tuned shapes.
 void prepare_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream);
 void clear_float_tuning();
-// MFMA prototype (kernels/stencil_mfma.hip): one gaussian step, grey frames.
-void launch_mfma_grey_step(const StencilLaunch& a, hipStream_t stream);
 
 // Whether `v` (or Auto) can fuse `steps` > 1 for this filter.
 bool supports_fusion(const Filter& f, KernelVariant v);
@@ -104,32 +101,6 @@ void launch_fill_zero(uint8_t* p, int64_t bytes, hipStream_t stream);
 // Load the code object of the temporal / copy kernels now (a one-shot process
 // calls it from a helper thread while it creates its first hardware queue).
 void preload_kernel_module();
-// Register-resident fused gaussian (kernels/stencil_resident.hip): every
-// repetition of a single-band frame in ONE launch, tiles held in registers,
-// halo rings exchanged between workgroups through memory every K steps.
-struct ResidentGeom {
-  int hl = 0, vbytes = 0, vrows = 0, nstrips = 0, pair_stride = 0, row_tiles = 0;
-};
-struct ResidentPlan {
-  bool ok = false;  // false: frame too large for one workgroup per CU, or unsupported
-  int m = 0;        // register rows per wave (8 waves per workgroup)
-  int grid = 0;     // workgroups (<= CUs)
-  ResidentGeom geom;
-};
-struct ResidentLaunch {
-  uint8_t* f0 = nullptr;  // input frame at (row 0, byte 0); also a ring buffer
-  uint8_t* f1 = nullptr;  // the other frame
-  int64_t pitch = 0, row_bytes = 0, height = 0;
-  int reps = 0, K = 8;         // repetitions, steps per phase (halo depth)
-  uint32_t* flags = nullptr;   // one word per workgroup, device memory
-  uint32_t epoch = 0;          // flags reach epoch + phase; above every earlier launch's values
-  uint32_t* err = nullptr;     // pinned host word: set on a wait timeout
-  double timeout_s = 0.25;     // per wait
-  bool force_acquire = false;  // agent acquire even at one workgroup per CU (A/B)
-};
-ResidentPlan plan_resident(Channels ch, int64_t rows, int64_t row_bytes, int steps_per_phase);
-// The result lands in f1 for an odd number of phases ceil(reps / K), else f0.
-void launch_resident(const ResidentLaunch& a, Channels ch, const ResidentPlan& plan, hipStream_t stream);
 
 // Empirical tile-shape tuning on / off (off: the latency model's pick);
 // returns the previous setting.  A one-shot process turns it off: timing a

@@ -468,7 +468,6 @@ const char* kernel_variant_name(KernelVariant v) {
     case KernelVariant::Float9: return "float9";
     case KernelVariant::TemporalPk: return "temporal_pk";
     case KernelVariant::FloatTemporal: return "float_temporal";
-    case KernelVariant::Mfma: return "mfma";
   }
   return "?";
 }
@@ -529,13 +528,6 @@ void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hip
     v = f.binomial121 ? (a.steps > 1 || own_dst_pitch ? KernelVariant::Temporal : KernelVariant::Binomial)
                       : (a.steps > 1 ? KernelVariant::FloatTemporal
                                      : (f.int_exact ? KernelVariant::Int9 : KernelVariant::Float9));
-  if (v == KernelVariant::Mfma) {
-    PCONV_CHECK(f.binomial121 && ch == Channels::Grey && a.steps == 1,
-                "mfma prototype: gaussian, grey, one step per launch");
-    launch_mfma_grey_step(a, stream);
-    PCONV_HIP_CHECK(hipGetLastError());
-    return;
-  }
   if (v == KernelVariant::FloatTemporal) {
     launch_float_temporal(f, ch, a, stream);
     PCONV_HIP_CHECK(hipGetLastError());

@@ -287,164 +287,6 @@ __global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__
   }
 }
 
-// Row-streaming form of the same fused gaussian, for large frames.
-//
-// The tile kernel above pays for its independence with a trapezoid: a
-// 64-row tile advanced 8 steps keeps only 48 rows (25 % of its arithmetic is
-// halo), and every step ends at a workgroup barrier.  Here one wave owns a
-// column-strip pair (the same pair layout and DPP taps as k_swar) and walks
-// DOWN a segment of rows, holding T time levels as rolling row sums in
-// registers: each input row it loads climbs all T levels at once (level t
-// emits row i - 2t + 1, levels skewed by one row for ILP), and the last
-// level's row is stored.  Vertical redundancy
-// is only the 2T-row run-in/run-out of each segment (a few %), there is no
-// LDS and no barrier — waves are independent; loads are prefetched two rows
-// ahead.  Per pair per level: 2 ops horizontal, 2 vertical, 2 (or, with ALT,
-// 1.5 on average) truncation — the tile kernel's arithmetic without its halo
-// rows.  Chosen by the tuner where it wins (large frames; small bands leave
-// too few segments to fill the chip).
-template <int CH, int NP, int T, bool ALT>
-__global__ __launch_bounds__(256) void k_stream(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                int64_t pitch, int64_t dst_pitch, int row_bytes, int r0, int r1,
-                                                int g_row0, int height, int nstrips, int pair_stride, int seg_rows,
-                                                int nwaves) {
-  static_assert(!ALT || T % 2 == 0, "paired levels need an even level count");
-  using CT = typename Chunk<NP>::T;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + (static_cast<int>(threadIdx.x) >> 6));
-  if (wid >= nwaves) return;  // whole wave (uniform)
-  constexpr int hl = (T * CH + NP - 1) / NP;  // halo lanes per side
-  constexpr int vbytes = (64 - 2 * hl) * NP;
-  const int col = wid % pair_stride, seg = wid / pair_stride;
-  const int sA = col, sB = col + pair_stride;
-  const bool hasB = sB < nstrips;
-  const int baseA = sA * vbytes - hl * NP, baseB = sB * vbytes - hl * NP;
-  const int xA = baseA + lane * NP, xB = baseB + lane * NP;
-  const int validA = (xA >= 0) ? min(max(row_bytes - xA, 0), NP) : 0;
-  const int validB = (hasB && xB >= 0) ? min(max(row_bytes - xB, 0), NP) : 0;
-  const bool needs_mask = baseA < 0 || baseA + 64 * NP > row_bytes || !hasB || baseB + 64 * NP > row_bytes;
-  u32 cm[NP];
-#pragma unroll
-  for (int k = 0; k < NP; ++k) cm[k] = (k < validA ? 0xffffu : 0u) | (k < validB ? 0xffff0000u : 0u);
-
-  const int s0 = r0 + seg * seg_rows;
-  const int s1 = min(r1, s0 + seg_rows);
-  const int lo_ok = max(r0 - T, -g_row0), hi_ok = min(r1 + T, height - g_row0);
-  const int img_lo = -g_row0, img_hi = height - g_row0;  // frame rows inside the image
-  const int st_hi = min(s1, img_hi);
-  const bool lane_in = lane >= hl && lane < 64 - hl;
-  const bool stA = lane_in && validA > 0, stB = lane_in && validB > 0;
-
-  auto load = [&](int fr, CT& a, CT& b) {
-    a = Chunk<NP>::zero();
-    b = Chunk<NP>::zero();
-    if (fr >= lo_ok && fr < hi_ok) {
-      const uint8_t* rowp = src + static_cast<int64_t>(fr) * pitch;
-      if (validA > 0) a = *reinterpret_cast<const CT*>(rowp + xA);
-      if (validB > 0) b = *reinterpret_cast<const CT*>(rowp + xB);
-    }
-  };
-
-  // Rolling state per level: H = horizontal sum of the level's previous
-  // input row, S = that of the two previous rows, updated in place (the new
-  // values replace dead ones, so the register allocator renames instead of
-  // copying; a parity-double-buffered form cost 40-64 more VGPRs and one
-  // wave per SIMD).  Levels are SKEWED: level t consumes the row level t-1
-  // emitted in the PREVIOUS iteration (Y[t-1]), so the T levels of one
-  // iteration are independent (T x NP-way ILP instead of a T-long dependency
-  // chain); level t emits row i - 2t + 1 at iteration i.
-  u32 S[T][NP], H[T][NP], Y[T][NP];
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int k = 0; k < NP; ++k) S[t][k] = H[t][k] = Y[t][k] = 0u;
-  // Input rows are prefetched PF rows ahead (a ring of PF raw rows): one
-  // row's T levels are ~T x 6 x NP instructions, far less than a load's
-  // latency from HBM.
-  constexpr int PF = 8;
-  CT ra[PF], rb[PF];
-  const int i0 = s0 - T, iend = s1 + 2 * T - 1;
-#pragma unroll
-  for (int q = 0; q < PF; ++q) load(i0 + q, ra[q], rb[q]);
-
-  auto row = [&](auto slot_c, auto safe_c, int i) {
-    constexpr int Q = decltype(slot_c)::value;
-    constexpr bool SAFE = decltype(safe_c)::value;  // every emitted row inside the image, no edge columns
-    u32 X0[NP];
-    unpack<NP>(ra[Q], rb[Q], X0);
-    load(i + PF, ra[Q], rb[Q]);
-    // Highest level first: level t reads Y[t-1] before level t-1 replaces it.
-#pragma unroll
-    for (int t = T - 1; t >= 0; --t) {
-      u32 Hn[NP], X[NP];
-      if (t == 0)
-        horiz<CH, NP>(X0, Hn);
-      else
-        horiz<CH, NP>(Y[t - 1], Hn);
-      const int j = i - 2 * t - 1;  // row emitted by level t + 1
-#pragma unroll
-      for (int k = 0; k < NP; ++k) {
-        const u32 Sn = H[t][k] + Hn[k];
-        const u32 sum = S[t][k] + Sn;
-        if constexpr (!ALT)
-          X[k] = trunc_sum<0>(sum);
-        else  // unrolled: the level parity folds at compile time
-          X[k] = ((T - 1 - t) & 1) ? trunc_sum<1>(sum) /* keeps 16 x floor */ : trunc_sum<2>(sum);
-        S[t][k] = Sn;
-        H[t][k] = Hn[k];
-      }
-      if constexpr (!SAFE) {
-        if (j < img_lo || j >= img_hi) {
-#pragma unroll
-          for (int k = 0; k < NP; ++k) X[k] = 0u;
-        }
-        if (needs_mask) {
-#pragma unroll
-          for (int k = 0; k < NP; ++k) X[k] &= cm[k];
-        }
-      }
-      if (t < T - 1) {
-#pragma unroll
-        for (int k = 0; k < NP; ++k) Y[t][k] = X[k];
-      } else if (j >= s0 && j < st_hi) {  // the last level's row is finished
-        CT a, b;
-        pack<NP>(X, a, b);
-        uint8_t* rowq = dst + static_cast<int64_t>(j) * dst_pitch;
-        if (stA) {
-          if (validA == NP)
-            *reinterpret_cast<CT*>(rowq + xA) = a;
-          else
-            store_bytes<NP>(rowq + xA, a, validA);
-        }
-        if (stB) {
-          if (validB == NP)
-            *reinterpret_cast<CT*>(rowq + xB) = b;
-          else
-            store_bytes<NP>(rowq + xB, b, validB);
-        }
-      }
-    }
-  };
-  using Safe = std::true_type;
-  using Edge = std::false_type;
-  static_assert(PF == 8, "the block below unrolls 8 ring slots");
-  auto block = [&](auto safe_c, int i, bool partial) {
-    // PF consecutive rows, ring slots 0..PF-1 (compile-time indices)
-#define PCONV_STREAM_ROW(Q_) \
-  if (!partial || i + Q_ < iend) row(std::integral_constant<int, Q_>{}, safe_c, i + Q_);
-    PCONV_STREAM_ROW(0) PCONV_STREAM_ROW(1) PCONV_STREAM_ROW(2) PCONV_STREAM_ROW(3)
-    PCONV_STREAM_ROW(4) PCONV_STREAM_ROW(5) PCONV_STREAM_ROW(6) PCONV_STREAM_ROW(7)
-#undef PCONV_STREAM_ROW
-  };
-  int i = i0;
-  // Run-in near the image top / edge strips: per-level zero rows and masks.
-  for (; i < iend && (needs_mask || i - 2 * T + 1 < img_lo); i += PF) block(Edge{}, i, true);
-  // Body: every level's row inside the image (rows i - 2T + 1 .. i + PF - 1).
-  const int safe_end = min(iend, img_hi);
-  for (; i + PF <= safe_end; i += PF) block(Safe{}, i, false);
-  for (; i < iend; i += PF) block(Edge{}, i, true);
-}
-
 // Instantiated tile shapes (LW, M, NW).
 constexpr SwarShape kShapes[] = {
     {8, 8, 8}, {8, 8, 4}, {8, 16, 4}, {8, 4, 8},              // 8-byte lanes: large images
@@ -474,24 +316,6 @@ int alt_mode() {
     const char* e = std::getenv("PCONV_SWAR_ALT");
     v = !e ? -1 : e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
     g_alt_mode.store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
-
-// Timed by the tuner against the tile kernel (where its segments are long
-// enough).  At 8 levels it lost everywhere (~190 VGPRs, 2 waves per SIMD;
-// docs/PERFORMANCE.md); at 6 levels (~150 VGPRs) it beats the 6-step tile
-// launches of frames beyond the Infinity Cache (32768^2 grey 128.8 vs 158
-// us/rep) but not the taller 8-step tiles (121).  PCONV_STREAM=0 keeps it
-// out of the tuning, =1 forces it (tests / A-B).
-std::atomic<int> g_stream_mode{-2};  // -2: PCONV_STREAM on first use; -1 tune, 0 off, 1 forced
-
-int stream_mode() {
-  int v = g_stream_mode.load(std::memory_order_relaxed);
-  if (v == -2) {
-    const char* e = std::getenv("PCONV_STREAM");
-    v = !e ? -1 : e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
-    g_stream_mode.store(v, std::memory_order_relaxed);
   }
   return v;
 }
@@ -672,93 +496,6 @@ void launch_pf_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh, bool alt)
   PCONV_FAIL("swar prefetch kernel: unsupported tile shape");
 }
 
-// Row-streaming launches: (NP, T) instantiations, T = the launch's steps.
-struct StreamCfg {
-  int np = 0;    // 0: tile kernel
-  int segf = 1;  // waves per resident slot (segments = resident waves x segf / strip pairs)
-};
-
-template <int CH, int NP, int T>
-const void* stream_fn(bool alt) {
-  return alt ? reinterpret_cast<const void*>(&k_stream<CH, NP, T, true>)
-             : reinterpret_cast<const void*>(&k_stream<CH, NP, T, false>);
-}
-
-// Resident waves per SIMD of one instantiation (VGPR-bound; no LDS).
-int stream_occupancy(const void* fn) {
-  static std::mutex mu;
-  static std::map<const void*, int> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find(fn);
-  if (it != cache.end()) return it->second;
-  hipFuncAttributes at{};
-  int occ = 4;
-  if (hipFuncGetAttributes(&at, fn) == hipSuccess && at.numRegs > 0) {
-    occ = std::max(1, std::min(8, 512 / round_up(at.numRegs, 8)));
-    cache.emplace(fn, occ);
-  } else {
-    (void)hipGetLastError();
-  }
-  return occ;
-}
-
-struct StreamGrid {
-  int nstrips = 0, pair_stride = 0, seg_rows = 0, nseg = 0, nwaves = 0;
-};
-
-StreamGrid stream_grid(int ch, int np, int t, int64_t rows, int64_t row_bytes, int occ, int segf) {
-  StreamGrid g;
-  const int hl = (t * ch + np - 1) / np;
-  const int vbytes = (64 - 2 * hl) * np;
-  if (vbytes <= 0 || rows <= 0) return g;
-  g.nstrips = static_cast<int>(ceil_div<int64_t>(row_bytes, vbytes));
-  g.pair_stride = (g.nstrips + 1) / 2;
-  const int64_t target = int64_t(1024) * occ * std::max(1, segf);  // 256 CUs x 4 SIMDs x resident waves
-  const int64_t nseg_want = std::max<int64_t>(1, target / g.pair_stride);
-  g.seg_rows = static_cast<int>(std::max<int64_t>(ceil_div<int64_t>(rows, nseg_want), 2 * t));
-  g.nseg = static_cast<int>(ceil_div<int64_t>(rows, g.seg_rows));
-  g.nwaves = g.pair_stride * g.nseg;
-  return g;
-}
-
-template <int CH, int NP, int T>
-void launch_stream_one(const StencilLaunch& a, hipStream_t s, bool alt, int segf) {
-  PCONV_CHECK(a.steps == T, "stream kernel: steps must equal its level count");
-  const int occ = stream_occupancy(stream_fn<CH, NP, T>(alt));
-  const StreamGrid g = stream_grid(CH, NP, T, a.r1 - a.r0, a.row_bytes, occ, segf);
-  PCONV_CHECK(g.nwaves > 0, "stream kernel: empty launch");
-  const dim3 grid(static_cast<unsigned>(ceil_div(g.nwaves, 4)));
-  const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
-  const int64_t dp = a.dst_pitch ? a.dst_pitch : a.pitch;
-  if (alt)
-    k_stream<CH, NP, T, true><<<grid, dim3(256), 0, s>>>(a.src, a.dst, a.pitch, dp, static_cast<int>(a.row_bytes),
-                                                         static_cast<int>(a.r0), static_cast<int>(a.r1),
-                                                         static_cast<int>(a.g_row0), static_cast<int>(hmax), g.nstrips,
-                                                         g.pair_stride, g.seg_rows, g.nwaves);
-  else
-    k_stream<CH, NP, T, false><<<grid, dim3(256), 0, s>>>(a.src, a.dst, a.pitch, dp, static_cast<int>(a.row_bytes),
-                                                          static_cast<int>(a.r0), static_cast<int>(a.r1),
-                                                          static_cast<int>(a.g_row0), static_cast<int>(hmax), g.nstrips,
-                                                          g.pair_stride, g.seg_rows, g.nwaves);
-}
-
-// Instantiated (NP, T): 4-byte lanes, 4 / 6 / 8 levels.  The rolling state
-// is 2 x T x 4 pairs double-buffered plus T x 4 skewed rows and an 8-row load
-// ring: ~190 VGPRs at T = 8 (2 waves/SIMD), ~150 at 6, ~110 at 4 (4
-// waves/SIMD) — fewer levels per launch, more launches, but no vertical
-// redundancy at all, which matters most for frames beyond the Infinity Cache
-// (the tile kernel's fixed cost per launch is its trapezoid and its load/store
-// phases).  16 levels or 8-byte lanes do not fit the register file.
-bool stream_supported(int ch, int np, int steps) { return np >= ch && np == 4 && (steps == 4 || steps == 6 || steps == 8); }
-
-template <int CH>
-void launch_stream_ch(const StencilLaunch& a, hipStream_t s, StreamCfg c, bool alt) {
-  if (c.np == 4 && a.steps == 8) return launch_stream_one<CH, 4, 8>(a, s, alt, c.segf);
-  if (c.np == 4 && a.steps == 6) return launch_stream_one<CH, 4, 6>(a, s, alt, c.segf);
-  if (c.np == 4 && a.steps == 4) return launch_stream_one<CH, 4, 4>(a, s, alt, c.segf);
-  PCONV_FAIL("stream kernel: unsupported (lanes, steps)");
-}
-
 bool known_shape(const SwarShape& s) {
   for (const auto& k : kShapes)
     if (k.lw == s.lw && k.m == s.m && k.nw == s.nw) return true;
@@ -887,7 +624,6 @@ KernelRes kernel_res(SwarShape sh, int ch, bool alt) {
 // best shape in 6 of 6 configurations of the current kernel.
 void set_xcd_swizzle(bool on) { g_xcd_swizzle.store(on ? 1 : 0, std::memory_order_relaxed); }
 void set_swar_alt(int mode) { g_alt_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
-void set_stream_mode(int mode) { g_stream_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
 void set_prefetch_mode(int mode, int grid_cap) {
   g_pf_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed);
   g_pf_grid_cap.store(grid_cap, std::memory_order_relaxed);
@@ -948,8 +684,7 @@ namespace {
 struct SwarChoice {
   SwarShape shape;
   bool alt = true;
-  StreamCfg stream;  // np > 0: row-streaming kernel instead of the tile kernel
-  bool pf = false;   // persistent prefetching tile kernel (k_swar_pf)
+  bool pf = false;  // buffer-op tile kernel (k_swar_pf)
 };
 
 void launch_choice(const StencilLaunch& a, Channels ch, hipStream_t stream, SwarChoice c) {
@@ -958,14 +693,6 @@ void launch_choice(const StencilLaunch& a, Channels ch, hipStream_t stream, Swar
       case Channels::Grey: launch_pf_ch<1>(a, stream, c.shape, c.alt); break;
       case Channels::Rgb: launch_pf_ch<3>(a, stream, c.shape, c.alt); break;
       case Channels::Rgba: launch_pf_ch<4>(a, stream, c.shape, c.alt); break;
-    }
-    return;
-  }
-  if (c.stream.np > 0) {
-    switch (ch) {
-      case Channels::Grey: launch_stream_ch<1>(a, stream, c.stream, c.alt); break;
-      case Channels::Rgb: launch_stream_ch<3>(a, stream, c.stream, c.alt); break;
-      case Channels::Rgba: launch_stream_ch<4>(a, stream, c.stream, c.alt); break;
     }
     return;
   }
@@ -1017,11 +744,6 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   const int mode = alt_mode();
   SwarChoice fallback;
   fallback.alt = default_alt();
-  if (stream_mode() == 1 && !autotune_enabled() && stream_supported(c, 4, a.steps)) {
-    fallback.shape = pick_swar_shape(a.steps, c, rows, a.row_bytes);
-    fallback.stream = StreamCfg{4, 1};  // forced streaming kernel, untuned
-    return fallback;
-  }
   if (pf_mode() == 1 && pf_launch_ok(a, a.steps) && (override_shape(fallback.shape) || !autotune_enabled())) {
     // forced prefetch kernel, untuned: the overridden shape if it has a
     // prefetch instantiation, else the first prefetch shape that runs
@@ -1070,10 +792,7 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   std::vector<SwarChoice> cands;
   for (const auto& r : ranked)
     for (int alt = 0; alt <= 1; ++alt)
-      if (mode < 0 || mode == alt) cands.push_back(SwarChoice{r.second, alt == 1, StreamCfg{}, false});
-  // Row-streaming candidates where the segments stay long against their
-  // 2T-row run-in (large frames / bands): 8 segments' worth of rows per
-  // strip pair at least.
+      if (mode < 0 || mode == alt) cands.push_back(SwarChoice{r.second, alt == 1, false});
   // Buffer-op tile kernel (k_swar_pf, one workgroup per tile) for the
   // model's candidate shapes it instantiates: hardware zero-fill of rows and
   // lanes outside the frame instead of branches (measured 2-6 % faster on RGB
@@ -1083,26 +802,9 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
     for (const auto& r : ranked)
       if (known_pf_shape(r.second))
         for (int alt = 0; alt <= 1; ++alt)
-          if (mode < 0 || mode == alt) pfs.push_back(SwarChoice{r.second, alt == 1, StreamCfg{}, true});
+          if (mode < 0 || mode == alt) pfs.push_back(SwarChoice{r.second, alt == 1, true});
     if (pf_mode() == 1 && !pfs.empty()) cands.clear();  // forced: only these candidates
     cands.insert(cands.end(), pfs.begin(), pfs.end());
-  }
-  if (stream_mode() != 0) {
-    for (int np : {4}) {
-      if (!stream_supported(c, np, a.steps)) continue;
-      for (int segf : {1, 2}) {
-        const StreamGrid g = stream_grid(c, np, a.steps, rows, a.row_bytes, 4, segf);
-        if (g.nwaves == 0 || (stream_mode() != 1 && g.seg_rows < 8 * a.steps)) continue;
-        for (int alt = 0; alt <= 1; ++alt)
-          if (mode < 0 || mode == alt) cands.push_back(SwarChoice{fallback.shape, alt == 1, StreamCfg{np, segf}, false});
-      }
-    }
-    if (stream_mode() == 1) {  // forced: only streaming candidates (tests / A-B)
-      std::vector<SwarChoice> only;
-      for (const auto& x : cands)
-        if (x.stream.np > 0) only.push_back(x);
-      if (!only.empty()) cands.swap(only);
-    }
   }
   SwarChoice best = cands.front();
   if (cands.size() > 1) {
@@ -1153,7 +855,7 @@ std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned() {
   std::vector<std::pair<std::vector<int64_t>, SwarShape>> out;
   for (const auto& kv : g_tuned)
     out.push_back({{kv.first.ch, kv.first.steps, kv.first.rows, kv.first.row_bytes, kv.second.alt ? 1 : 0,
-                    kv.second.stream.np, kv.second.stream.segf, kv.second.pf ? 1 : 0},
+                    kv.second.pf ? 1 : 0},
                    kv.second.shape});
   return out;
 }

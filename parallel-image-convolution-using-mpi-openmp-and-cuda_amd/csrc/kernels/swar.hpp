@@ -29,8 +29,8 @@ void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
 void prepare_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
 void set_autotune(bool on);
 void clear_swar_tuning();
-// Tuned entries: ({channels, steps, rows, row_bytes, paired_form, stream_lanes, stream_segf, prefetch}, shape);
-// stream_lanes > 0: the row-streaming kernel won (shape unused); prefetch = 1: k_swar_pf won.
+// Tuned entries: ({channels, steps, rows, row_bytes, paired_form, prefetch}, shape); prefetch = 1: the
+// buffer-op tile kernel k_swar_pf won.
 std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned();
 
 // Force a tile shape (lw = 0 restores the model) and list the instantiated ones.
@@ -49,9 +49,6 @@ void set_xcd_swizzle(bool on);
 // Step form: -1 tuned per launch geometry (default), 0 truncate every step,
 // 1 steps in pairs with a scale-16 intermediate (PCONV_SWAR_ALT=0/1).
 void set_swar_alt(int mode);
-// Row-streaming kernel: -1 among the tuned candidates, 0 never (default:
-// measured slower), 1 forced where it applies (PCONV_STREAM=-1/0/1).
-void set_stream_mode(int mode);
 // Buffer-op tile kernel (k_swar_pf): -1 among the tuned candidates
 // (default), 0 never, 1 forced (PCONV_PREFETCH=-1/0/1); with the mode forced,
 // a shape set by set_swar_shape that it instantiates is used as is (tests).

@@ -1,5 +1,4 @@
-// Device helpers of the SWAR-32 gaussian shared by the tile kernel
-// (stencil_swar.hip) and the register-resident kernel (stencil_resident.hip):
+// Device helpers of the SWAR-32 gaussian tile kernels (stencil_swar.hip):
 // the byte-pair layout, the horizontal [1,2,1] with DPP lane crossing, and one
 // interior-first repetition of a wave's register rows.  See stencil_swar.hip
 // for the layout and the measurements behind these forms.

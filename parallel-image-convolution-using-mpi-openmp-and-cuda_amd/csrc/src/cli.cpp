@@ -38,7 +38,7 @@ std::string help_text(const std::string& prog) {
          "  --fuse T                  repetitions fused per kernel launch (default: auto)\n"
          "  --no-overlap              do not overlap halo exchange with interior compute\n"
          "  --graph                   capture the repetition loop in a hipGraph (1 GPU)\n"
-         "  --kernel {auto,binomial,temporal,int9,float9,float_temporal,mfma}\n"
+         "  --kernel {auto,binomial,temporal,int9,float9,float_temporal}\n"
          "  --out PATH                output file (default: blur_<image> next to the input)\n"
          "  --synthetic SEED          use a deterministic random image instead of reading the file\n"
          "  --check                   verify the result against the CPU oracle\n"
@@ -110,7 +110,6 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       else if (v == "int9") c.variant = KernelVariant::Int9;
       else if (v == "float9") c.variant = KernelVariant::Float9;
       else if (v == "float_temporal") c.variant = KernelVariant::FloatTemporal;
-      else if (v == "mfma") c.variant = KernelVariant::Mfma;
       else PCONV_FAIL("invalid --kernel '" + v + "'");
     } else if (a == "--out") {
       c.out = next("--out");

@@ -130,7 +130,7 @@ void BandEngine::download_rows(uint8_t* host, int64_t host_pitch, int64_t r_begi
                                hipStream_t stream) {
   PCONV_CHECK(r_begin >= 0 && r_end <= lay_.rows && r_begin <= r_end, "download_rows: rows outside band");
   if (r_end == r_begin) return;
-  if (opt_.kernel_copies || opt_.kernel_d2h) {
+  if (opt_.kernel_copies) {
     launch_copy_rows(src_frame() + r_begin * lay_.pitch, lay_.pitch, host, host_pitch, lay_.row_bytes, r_end - r_begin,
                      stream ? stream : cs_);
     return;
@@ -303,14 +303,6 @@ void BandEngine::run(int reps) {
   pre_exchanges_ = 0;
   wall_t0_ = wall_seconds();
   if (opt_.timing) ev_t0_.record(cs_);
-  if (opt_.resident && run_resident(reps)) {
-    if (opt_.timing) {
-      ev_t1_.record(cs_);
-      timing_pending_ = true;
-    }
-    halo_valid_ = false;
-    return;
-  }
   bool graph = opt_.use_graph && !ph.empty();
   for (const auto& p : ph) graph = graph && p.exchange_depth == 0;
   if (graph) {
@@ -342,45 +334,6 @@ void BandEngine::run(int reps) {
     timing_pending_ = true;
   }
   halo_valid_ = false;
-}
-
-bool BandEngine::run_resident(int reps) {
-  if (reps < 1 || band_.up >= 0 || band_.down >= 0 || !filter_.binomial121 ||
-      !(opt_.variant == KernelVariant::Auto || opt_.variant == KernelVariant::Temporal))
-    return false;
-  if (!rplan_done_) {
-    rplan_ = plan_resident(geom_.channels, band_.rows, lay_.row_bytes, std::max(1, opt_.fuse));
-    rplan_done_ = true;
-    if (rplan_.ok) {
-      rflags_ = DeviceBuffer(static_cast<size_t>(round_up(rplan_.grid, 4)) * 4);
-      PCONV_HIP_CHECK(hipMemsetAsync(rflags_.data(), 0, rflags_.size(), cs_));
-      rerr_ = PinnedBuffer(64);
-      std::memset(rerr_.data(), 0, 64);
-    }
-  }
-  if (!rplan_.ok) return false;
-  const int K = std::max(1, opt_.fuse);
-  const int phases = (reps + K - 1) / K;
-  ResidentLaunch a;
-  a.f0 = frame_at(cur_);
-  a.f1 = frame_at(cur_ ^ 1);
-  a.pitch = lay_.pitch;
-  a.row_bytes = lay_.row_bytes;
-  a.height = band_.rows;
-  a.reps = reps;
-  a.K = K;
-  a.flags = reinterpret_cast<uint32_t*>(rflags_.data());
-  a.epoch = repoch_;
-  a.err = reinterpret_cast<uint32_t*>(rerr_.data());
-  const char* fa = std::getenv("PCONV_RESIDENT_ACQUIRE");  // A/B: keep the acquire at one workgroup per CU
-  a.force_acquire = fa && fa[0] == '1';
-  if (const char* ts = std::getenv("PCONV_RESIDENT_TIMEOUT_S")) a.timeout_s = std::atof(ts);  // tests: abort path
-  repoch_ += static_cast<uint32_t>(phases) + 1;
-  launch_resident(a, geom_.channels, rplan_, cs_);
-  ++stats_.launches;
-  if (phases & 1) cur_ ^= 1;
-  resident_pending_ = true;
-  return true;
 }
 
 bool BandEngine::exchange_free(int reps, bool halo_preloaded) const {
@@ -522,20 +475,6 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     trim_graph_caches();
     const int64_t rb = lay_.row_bytes;
     hipGraph_t g = nullptr;
-    // Zero-copy output: the last launch must produce exactly the owned rows
-    // with the SWAR kernel (gaussian) into a 4-byte-aligned packed row pitch.
-    // The last launch can store its rows straight to another pointer (the
-    // SWAR kernel takes a destination pitch) when it alone produces exactly
-    // the owned rows.
-    const bool last_whole = host_out && !ph.empty() && ph.back().exchange_depth == 0 &&
-                            ph.back().launches.size() == 1 && ph.back().launches[0].lo == 0 &&
-                            ph.back().launches[0].hi == band_.rows && filter_.binomial121 &&
-                            (opt_.variant == KernelVariant::Auto || opt_.variant == KernelVariant::Temporal) &&
-                            rb % 4 == 0;
-    const bool zc = last_whole && opt_.zero_copy_out && reinterpret_cast<uintptr_t>(host_out) % 16 == 0;
-    const bool packed = last_whole && !zc && opt_.packed_out;
-    if (packed && stage_.size() < static_cast<size_t>(rb * band_.rows))
-      stage_ = DeviceBuffer(static_cast<size_t>(rb * band_.rows));
     prepare(ph);  // tile-shape tuning cannot run inside the capture
     PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
     upload_rows(host_in, rb, in_r0, in_r1, cs_);
@@ -543,20 +482,10 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
       transport_->exchange(*this, lay_.halo, cs_);  // stream order: after the upload, before the launches
       ++stats_.exchanges;
     }
-    for (size_t i = 0; i + (zc || packed ? 1 : 0) < ph.size(); ++i) enqueue_phase(ph[i]);
-    if (zc || packed) {
-      launch(ph.back().launches[0], cs_, zc ? host_out : stage_.data(), rb);
-      cur_ ^= 1;  // frame state as after the phase (its rows now live outside the frames)
-      if (packed)
-        PCONV_HIP_CHECK(hipMemcpyAsync(host_out, stage_.data(), static_cast<size_t>(rb * band_.rows),
-                                       hipMemcpyDeviceToHost, cs_));
-    } else if (host_out) {
-      download_rows(host_out, rb, 0, band_.rows, cs_);
-    }  // host_out == nullptr: the caller downloads the result frame itself
+    for (const auto& p : ph) enqueue_phase(p);
+    if (host_out) download_rows(host_out, rb, 0, band_.rows, cs_);  // nullptr: the caller downloads itself
     PCONV_HIP_CHECK(hipStreamEndCapture(cs_, &g));
     StepGraph sg;
-    sg.zero_copy = zc;
-    sg.packed = packed;
     PCONV_HIP_CHECK(hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0));
     PCONV_HIP_CHECK(hipGraphDestroy(g));
     sg.end_cur = cur_;
@@ -587,15 +516,6 @@ void BandEngine::exec_compute(const Phase& p) {
 void BandEngine::synchronize() {
   PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
   if (ms_ != cs_) PCONV_HIP_CHECK(hipStreamSynchronize(ms_));
-  if (resident_pending_) {
-    resident_pending_ = false;
-    volatile uint32_t* e = reinterpret_cast<volatile uint32_t*>(rerr_.data());
-    if (*e != 0) {
-      *e = 0;
-      PCONV_FAIL("resident kernel: a workgroup timed out waiting for its neighbours (grid not co-resident: "
-                 "another kernel on the device?); the frames hold garbage");
-    }
-  }
   if (timing_pending_) {
     stats_.loop_ms = Event::elapsed_ms(ev_t0_, ev_t1_);
     stats_.wall_ms = (wall_seconds() - wall_t0_) * 1e3;
@@ -606,34 +526,9 @@ void BandEngine::synchronize() {
 // --------------------------------------------------------------- BandPipeline
 
 BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter& filter, const EngineOptions& opt,
-                           int slots, int concurrent, bool graphs, bool step_graphs, bool split_d2h, bool slot_comm) {
+                           int slots, int concurrent, bool graphs, bool step_graphs, bool slot_comm) {
   PCONV_CHECK(slots >= 1 && slots <= 8, "pipeline slots must be in [1, 8]");
   set_device(opt.device);
-  if (split_d2h) {
-    PCONV_CHECK(graphs && step_graphs, "split_d2h needs whole-step graphs on slot streams");
-    PCONV_CHECK(slots >= 2 && slots % 2 == 0, "split_d2h needs an even number of engines (two per stream)");
-    graphs_ = true;
-    step_graphs_ = true;
-    split_d2h_ = true;
-    concurrent_ = true;
-    EngineOptions o = opt;
-    o.use_graph = false;
-    o.timing = false;
-    o.overlap = false;
-    for (int i = 0; i < slots / 2; ++i) computes_.push_back(Stream::create(0));
-    d2h_ = Stream::create(0);
-    for (int i = 0; i < slots; ++i) {
-      // engines 2j and 2j+1 share compute stream j: consecutive images
-      // alternate streams, and each stream alternates its two engines
-      o.compute_stream = computes_[static_cast<size_t>(i % (slots / 2))].get();
-      o.comm_stream = o.compute_stream;
-      slots_.push_back(std::make_unique<BandEngine>(geom, band, filter, o));
-      ev_done_split_.push_back(Event::create());
-      ev_freed_.push_back(Event::create());
-    }
-    used_.assign(slots, false);
-    return;
-  }
   if (graphs) {
     // One stream per slot carries that slot's whole image (H2D, reps, D2H) as
     // one graph: slots overlap each other without cross-stream events.
@@ -739,20 +634,6 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
     trace_mark(2, cs);
     e.download_rows(host_out, e.layout().row_bytes, 0, e.band().rows);
     trace_mark(3, cs);
-    used_[k] = true;
-    ++count_;
-    return;
-  }
-  if (split_d2h_) {
-    PCONV_CHECK(trace_ev_.empty(), "pipeline trace needs directly issued images (graph capture off)");
-    hipStream_t cs = e.compute_stream();
-    // This engine's frames may still be read by its previous image's D2H.
-    if (used_[k]) ev_freed_[k].wait_on(cs);
-    e.process_graph(host_in, in_r0, in_r1, nullptr, reps);  // H2D + repetitions only
-    ev_done_split_[k].record(cs);
-    ev_done_split_[k].wait_on(d2h_.get());
-    e.download_rows(host_out, e.layout().row_bytes, 0, e.band().rows, d2h_.get());
-    ev_freed_[k].record(d2h_.get());
     used_[k] = true;
     ++count_;
     return;

@@ -60,7 +60,6 @@ KernelVariant parse_variant(const std::string& s) {
   if (s == "int9") return KernelVariant::Int9;
   if (s == "float9") return KernelVariant::Float9;
   if (s == "float_temporal") return KernelVariant::FloatTemporal;
-  if (s == "mfma") return KernelVariant::Mfma;
   PCONV_FAIL("unknown kernel variant '" + s + "'");
 }
 
@@ -364,9 +363,6 @@ PYBIND11_MODULE(_pconv_native, m) {
       out.append(py::make_tuple(py::cast(kv.first), py::make_tuple(kv.second.lw, kv.second.m, kv.second.nw)));
     return out;
   });
-  m.def("set_stream_mode", &set_stream_mode, py::arg("mode"),
-        "Row-streaming temporal kernel: -1 tuned against the tile kernel, 0 never (default), 1 forced where it "
-        "applies (8-step launches)");
   m.def("set_prefetch_mode", &set_prefetch_mode, py::arg("mode"), py::arg("grid_cap") = 0,
         "Buffer-op tile kernel: -1 tuned against the others (default), 0 never, 1 forced (with a set_swar_shape "
         "shape it instantiates, that shape); grid_cap 0: one workgroup per tile, < 0: persistent resident "
@@ -434,11 +430,10 @@ PYBIND11_MODULE(_pconv_native, m) {
   py::class_<BandEngine>(m, "BandEngine")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, bool graph, const std::string& variant,
-                       bool kernel_copies, bool resident, int stream_chunks) {
+                       bool kernel_copies, int stream_chunks) {
              EngineOptions o;
              o.stream_chunks = stream_chunks;
              o.kernel_copies = kernel_copies;
-             o.resident = resident;
              o.device = device;
              o.halo_depth = halo;
              o.fuse = fuse;
@@ -451,7 +446,7 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
            py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
            py::arg("overlap") = true, py::arg("graph") = false, py::arg("variant") = "auto",
-           py::arg("kernel_copies") = false, py::arg("resident") = false, py::arg("stream_chunks") = 0)
+           py::arg("kernel_copies") = false, py::arg("stream_chunks") = 0)
       .def_property_readonly("band", &BandEngine::band)
       .def("stream_plan", &BandEngine::stream_plan, py::arg("reps"), py::arg("in_r0"), py::arg("in_r1"))
       .def_property_readonly("halo", [](const BandEngine& e) { return e.layout().halo; })
@@ -575,13 +570,10 @@ PYBIND11_MODULE(_pconv_native, m) {
   py::class_<BandPipeline>(m, "BandPipeline")
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
-                       int concurrent, bool graphs, bool zero_copy_out, bool step_graphs, bool split_d2h,
-                       bool packed_out, bool kernel_d2h, py::object band, bool slot_comm, int stream_chunks) {
+                       int concurrent, bool graphs, bool step_graphs, py::object band, bool slot_comm,
+                       int stream_chunks) {
              EngineOptions o;
              o.stream_chunks = stream_chunks;
-             o.zero_copy_out = zero_copy_out;
-             o.packed_out = packed_out;
-             o.kernel_d2h = kernel_d2h;
              o.device = device;
              o.halo_depth = halo;
              o.fuse = fuse;
@@ -591,13 +583,12 @@ PYBIND11_MODULE(_pconv_native, m) {
              // band: an explicit Band (tests: a self-neighbour band on a 1-rank communicator)
              const Band b = band.is_none() ? row_band(h, world, rank) : band.cast<Band>();
              return std::make_unique<BandPipeline>(g, b, make_filter(filter), o, slots, concurrent, graphs,
-                                                   step_graphs, split_d2h, slot_comm);
+                                                   step_graphs, slot_comm);
            }),
            py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter") = "gaussian",
            py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
            py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1,
-           py::arg("graphs") = false, py::arg("zero_copy_out") = false, py::arg("step_graphs") = true,
-           py::arg("split_d2h") = false, py::arg("packed_out") = false, py::arg("kernel_d2h") = false,
+           py::arg("graphs") = false, py::arg("step_graphs") = true,
            py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
@@ -626,7 +617,6 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_property_readonly("concurrent", &BandPipeline::concurrent)
       .def_property_readonly("graphs", &BandPipeline::graphs)
       .def_property_readonly("step_graphs", &BandPipeline::step_graphs)
-      .def_property_readonly("split_d2h", &BandPipeline::split_d2h)
       .def("enable_trace", &BandPipeline::enable_trace, py::arg("images"),
            "Time the stages of the next `images` submits (directly issued pipelines only)")
       .def("trace", &BandPipeline::trace, py::call_guard<py::gil_scoped_release>(),

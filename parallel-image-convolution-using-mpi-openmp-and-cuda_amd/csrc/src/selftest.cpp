@@ -277,7 +277,7 @@ std::string rccl_selftest_multicomm(int device, int slots, int images, double ti
     o.halo_depth = c.halo;
     o.fuse = c.fuse;
     BandPipeline pipe(g, self_band(y0, rows), f, o, slots, -1, /*slot_streams=*/true, /*step_graphs=*/captured,
-                      /*split_d2h=*/false, slot_comm);
+                      slot_comm);
     std::vector<std::shared_ptr<RcclComm>> comms;
     for (int k = 0; k < slots; ++k) {
       comms.push_back(std::make_shared<RcclComm>(rccl_unique_id(), 0, 1, device));

@@ -57,10 +57,8 @@ class DistributedBlur:
                  device: Optional[int] = None, halo: Optional[int] = None, fuse: Optional[int] = None,
                  overlap: bool = True, preload_halo: bool = False, comm=None, slots: int = 2,
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
-                 step_graphs: Optional[bool] = None, zero_copy_out: bool = False, graph_capture: bool = True,
-                 slot_exchange: bool = False, split_d2h: bool = False, packed_out: bool = False,
-                 kernel_d2h: bool = False, self_neighbours: bool = False, slot_comm: bool = False,
-                 stream_chunks: int = 0):
+                 step_graphs: Optional[bool] = None, graph_capture: bool = True, slot_exchange: bool = False,
+                 self_neighbours: bool = False, slot_comm: bool = False, stream_chunks: int = 0):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -111,22 +109,14 @@ class DistributedBlur:
         # With RCCL, an exchange image is ONE captured graph (upload, ncclSend/
         # ncclRecv of the ghost zone, launches, download): one host call per
         # image instead of the transport's group calls + launches + copies.
-        # split_d2h: each image's graph = H2D + repetitions on one of slots/2
-        # compute streams (two engines alternate on each), its D2H on a shared
-        # copy stream — exchange-free images only.
-        split = bool(split_d2h) and free and not self.slot_exchange
-        if split and (slots < 2 or slots % 2):
-            raise ValueError("split_d2h needs an even number of slots (two engines per compute stream)")
-        if self.slot_exchange or split or (free if step_graphs is None else bool(step_graphs)):
+        if self.slot_exchange or (free if step_graphs is None else bool(step_graphs)):
             del self.pipe
             # slot_comm (exchange images): each slot also gets a communication
             # stream, so an exchange phase runs beside the interior launch and
             # the edges follow the halo event — captured, the reference's per-
             # phase loop becomes ONE graph per image.
             self.pipe = n.BandPipeline(self.width, self.height, channels, nf, self.rank, self.world, self.device,
-                                       graphs=True, zero_copy_out=bool(zero_copy_out), packed_out=bool(packed_out),
-                                       kernel_d2h=bool(kernel_d2h),
-                                       step_graphs=bool(graph_capture) or split, split_d2h=split,
+                                       graphs=True, step_graphs=bool(graph_capture),
                                        slot_comm=bool(slot_comm) and self.slot_exchange, **kw)
         self.engine = self.pipe.slot(0)
         self.band = self.engine.band

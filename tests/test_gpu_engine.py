@@ -169,34 +169,6 @@ def test_pipeline_step_graphs_preloaded_band(pconv_mod, rng):
     assert np.array_equal(out, pconv_mod.numpy_convolve(img, reps)[b.y0:b.y0 + b.rows])
 
 
-@pytest.mark.parametrize("w,h,ch,reps,fuse", [(67, 45, "rgb", 9, 8), (64, 33, "grey", 13, 8), (40, 50, "rgba", 8, 4),
-                                              (61, 20, "rgb", 3, 8), (1920, 64, "rgb", 40, 8)])
-@pytest.mark.parametrize("mode", ["zero_copy", "packed", "kernel_d2h"])
-def test_pipeline_zero_copy_out(pconv_mod, rng, w, h, ch, reps, fuse, mode):
-    """The last fused launch writes packed rows straight into pinned host
-    memory (zero_copy) or into a device staging buffer followed by one
-    contiguous D2H (packed), or a CU copy kernel does the D2H (kernel_d2h):
-    every byte rewritten (pre-filled with 0xAB) and
-    exact — a partial last chunk spilling into the next packed row would show
-    as a mismatch."""
-    from pconv.parallel.dist_engine import DistributedBlur
-
-    c = {"grey": 1, "rgb": 3, "rgba": 4}[ch]
-    blur = DistributedBlur(w, h, ch, "gaussian", reps, rank=0, world=1, device=0, fuse=fuse, slots=2,
-                           step_graphs=True, zero_copy_out=mode == "zero_copy", packed_out=mode == "packed",
-                           kernel_d2h=mode == "kernel_d2h")
-    for rnd in range(2):
-        img = rng.integers(0, 256, size=(h, w, c), dtype=np.uint8)
-        blur.load_image(img)
-        for k in range(2):
-            blur.outputs[k][:] = 0xAB
-        ks = [blur.submit(reps) for _ in range(2)]
-        blur.drain()
-        ref = pconv_mod.numpy_convolve(img if c > 1 else img[..., 0], reps).reshape(h, -1)
-        for k in ks:
-            assert np.array_equal(blur.outputs[k].reshape(h, -1), ref), (rnd, k)
-
-
 @pytest.mark.parametrize("capture", [True, False])
 def test_pipeline_slot_streams_direct_and_graph(pconv_mod, rng, capture):
     """Slot-stream pipeline with and without whole-step graph capture."""
@@ -294,20 +266,21 @@ def test_step_graph_cache_bounded_across_host_buffers(pconv_mod, rng):
     assert eng.cached_graphs - eng.cached_step_graphs == loop_graphs
 
 
-@pytest.mark.parametrize("slots,reps,world,rank", [(2, 9, 1, 0), (4, 13, 1, 0), (4, 12, 8, 3), (6, 7, 3, 1)])
-def test_pipeline_split_d2h(pconv_mod, rng, slots, reps, world, rank):
-    """Split pipeline (graph = H2D + reps on slots/2 compute streams, D2H on a
-    shared copy stream).  Three rings of images over the same slot inputs with
-    no host synchronisation in between: an engine reused before its previous
-    download finished would have its result frame overwritten by the next
-    upload (the raw input would come back), so every output must equal the
-    oracle of its slot's input."""
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("slots,reps,world,rank", [(2, 9, 1, 0), (3, 13, 1, 0), (2, 12, 8, 3), (3, 7, 3, 1)])
+def test_pipeline_streamed_rings(pconv_mod, rng, graph, slots, reps, world, rank):
+    """Row-streamed images (stream_chunks=4): three rings of images over the
+    same slot inputs with no host synchronisation in between.  A slot reused
+    before its previous image's last download finished would have its result
+    frame overwritten by the next image's first chunk (the raw input or a
+    partial level would come back), so every output must equal the oracle of
+    its slot's input."""
     from pconv.parallel.dist_engine import DistributedBlur
 
     w, h = 83, 120
     blur = DistributedBlur(w, h, "rgb", "gaussian", reps, rank=rank, world=world, device=0, slots=slots,
-                           preload_halo=True, transport="none", split_d2h=True)
-    assert blur.pipe.split_d2h
+                           preload_halo=True, transport="none", stream_chunks=4, step_graphs=graph,
+                           graph_capture=graph)
     b = blur.band
     imgs = [rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for _ in range(slots)]
     for k, img in enumerate(imgs):

@@ -287,33 +287,6 @@ def test_prefetch_kernel_tuned_large_frame(native, rng):
         torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("steps", [4, 6, 8])
-@pytest.mark.parametrize("form", [0, 1])
-def test_row_streaming_kernel_bit_exact(native, rng, form, steps):
-    """The row-streaming form of the fused gaussian (forced; off by default):
-    whole images and band regions with ghost rows / image edges, guard-band
-    canaries and untouched rows outside [r0, r1) (checked by _run_fused)."""
-    try:
-        native.set_swar_alt(form)
-        native.set_stream_mode(1)
-        native.clear_swar_tuning()
-        for channels in ("grey", "rgb", "rgba"):
-            c = CH[channels]
-            for (h, w) in [(1, 7), (9, 5), (71, 301), (200, 1000)]:
-                img = rng.integers(0, 256, size=(h, w, c) if c > 1 else (h, w), dtype=np.uint8)
-                gpu, cpu = _run_fused(native, img, steps, 0, h, steps, 0, h, variant="temporal")
-                assert np.array_equal(gpu, cpu), (channels, h, w)
-            img = rng.integers(0, 256, size=(40, 301, c) if c > 1 else (40, 301), dtype=np.uint8)
-            for g_row0, H in ((30, 200), (0, 45), (160, 200)):
-                gpu, cpu = _run_fused(native, img, steps, -5, 45, 16, g_row0, H, variant="temporal")
-                assert np.array_equal(gpu[11:61], cpu[11:61]), (channels, g_row0, "band")
-        assert any(k[5] > 0 for k, _ in native.swar_tuned()), "streaming kernel was not used"
-    finally:
-        native.set_stream_mode(0)
-        native.clear_swar_tuning()
-        native.set_swar_alt(-1)
-
-
 def test_frame_beyond_2gib_offsets(pconv_mod, native):
     """64-bit offsets end to end: a 2.16 GB grey frame
     (65536 x 33000) through the fused kernel; rows near the top, the middle
@@ -334,24 +307,3 @@ def test_frame_beyond_2gib_offsets(pconv_mod, native):
         got = out[y0:y0 + 8, :2048 - reps]
         exp = ref[y0 - lo:y0 - lo + 8, :2048 - reps]
         assert np.array_equal(got, exp), y0
-
-
-def test_mfma_prototype_bit_exact(native, rng):
-    """The MFMA prototype (two banded f16 16x16x16 products per tile, opt-in
-    `--kernel mfma`) is bit-exact on grey frames: odd sizes, partial row
-    ranges, bands inside a taller image (zero rows outside it)."""
-    from pconv.ops.reference import numpy_convolve
-
-    for (h, w) in [(1, 1), (5, 3), (17, 16), (31, 100), (64, 65), (130, 257), (300, 1500)]:
-        img = rng.integers(0, 256, size=(h, w), dtype=np.uint8)
-        got = _run_kernel(native, img, "gaussian", "mfma")
-        assert np.array_equal(got, numpy_convolve(img, 1)), (h, w)
-    img = rng.integers(0, 256, size=(40, 37), dtype=np.uint8)
-    ref = numpy_convolve(img, 1)
-    for r0, r1 in [(0, 1), (5, 6), (3, 29), (39, 40), (13, 27)]:
-        got = _run_kernel(native, img, "gaussian", "mfma", r0=r0, r1=r1)
-        assert np.array_equal(got[r0:r1], ref[r0:r1])
-    img = np.zeros((60, 45), np.uint8)
-    for g_row0, H in ((0, 300), (100, 300), (240, 300)):
-        gpu, cpu = _run_fused(native, img, 1, -3, 63, 8, g_row0, H, variant="mfma")
-        assert np.array_equal(gpu[5:71], cpu[5:71]), g_row0

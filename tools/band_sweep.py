@@ -70,7 +70,7 @@ def main():
             for sh, t in res.items():
                 print(json.dumps({"world": world, "band_rows": b.rows, "halo": halo, "fuse": f, "ch": a.channels,
                                   "shape": "auto" if sh is None else "%d,%d,%d" % sh,
-                                  "launches": e.stats.launches, "stream_mode": os.environ.get("PCONV_STREAM", "0"),
+                                  "launches": e.stats.launches,
                                   "tuned_keys": tuned,
                                   "us_per_rep": None if t is None else round(t / a.reps * 1e6, 3)}), flush=True)
 

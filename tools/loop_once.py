@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Run one device-resident loop (for profilers): W H channels reps fuse iters.
-Environment knobs of the kernels apply (PCONV_STREAM, PCONV_SWAR_SHAPE, ...)."""
+Environment knobs of the kernels apply (PCONV_SWAR_SHAPE, PCONV_PREFETCH, ...)."""
 import os
 import sys
 
