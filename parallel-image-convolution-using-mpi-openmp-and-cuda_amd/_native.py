@@ -16,15 +16,20 @@ import os
 
 import torch  # noqa: F401  -- see module docstring
 
-# OpenMP workers of the CPU stencil (system libgomp, loaded with the
-# extension below) sleep between parallel regions instead of spinning: CPU
-# ranks of the MPI+OpenMP analog share a node's CPU quota, and spinning
-# workers of one rank burn the quota the others' compute needs (a throttled
-# cgroup stalls every rank for the rest of its 100 ms period: the round-2
-# hybrid table had 0.1-0.2 s outliers and got slower with more ranks;
-# profiles/r03/hybrid/).  An explicit setting (OMP_WAIT_POLICY or
-# GOMP_SPINCOUNT) wins.
-if "OMP_WAIT_POLICY" not in os.environ and "GOMP_SPINCOUNT" not in os.environ:
+# OpenMP workers of the CPU stencil sleep between parallel regions instead of
+# spinning: CPU ranks of the MPI+OpenMP analog share a node's CPU quota, and
+# spinning workers of one rank burn the quota the others' compute needs (a
+# throttled cgroup stalls every rank for the rest of its 100 ms period: the
+# round-2 hybrid table had 0.1-0.2 s outliers and got slower with more ranks;
+# profiles/r03/hybrid/).  libgomp reads OMP_WAIT_POLICY once, when it is
+# initialised, so the variable is set only around the extension's import and
+# the caller's environment is restored right after: child processes and
+# OpenMP runtimes initialised later keep the user's setting.  It takes effect
+# only when the extension's import is what initialises the system libgomp
+# (a libgomp already mapped by an earlier import keeps its own policy).  An
+# explicit OMP_WAIT_POLICY or GOMP_SPINCOUNT wins.
+_SET_POLICY = "OMP_WAIT_POLICY" not in os.environ and "GOMP_SPINCOUNT" not in os.environ
+if _SET_POLICY:
     os.environ["OMP_WAIT_POLICY"] = "passive"
 
 _ERR = None
@@ -33,6 +38,9 @@ try:
 except ImportError as e:  # pragma: no cover - exercised only on broken builds
     native = None
     _ERR = e
+finally:
+    if _SET_POLICY:
+        os.environ.pop("OMP_WAIT_POLICY", None)
 
 
 def native_available() -> bool:

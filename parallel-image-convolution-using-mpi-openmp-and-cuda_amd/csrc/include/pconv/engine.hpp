@@ -317,12 +317,15 @@ class NullTransport : public HaloTransport {
 };
 
 // Transport used by LocalCluster (neighbour engines live on the same device).
+// Not capturable: its D2D copies read a peer engine's frame, and only
+// LocalCluster's per-phase events order them after the peer's work — a
+// captured graph would carry no dependency on the peer's stream.
 class LocalTransport : public HaloTransport {
  public:
   explicit LocalTransport(std::vector<BandEngine*> peers) : peers_(std::move(peers)) {}
   void exchange(BandEngine& e, int64_t depth, hipStream_t stream) override;
   const char* name() const override { return "local-d2d"; }
-  bool capturable() const override { return true; }
+  bool capturable() const override { return false; }
 
  private:
   std::vector<BandEngine*> peers_;

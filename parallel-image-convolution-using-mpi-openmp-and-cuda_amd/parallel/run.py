@@ -40,6 +40,28 @@ from ..utils.raw_io import output_path_for
 _CH = {"grey": 1, "rgb": 3, "rgba": 4}
 
 
+def omp_team_size(threads: int, cpus, default_threads: int, local_world: int, env=None) -> int:
+    """OpenMP team of one CPU rank (the OpenMP program's threads per MPI
+    process, open-mp/omp_convolution.c:292,297).  Precedence: --threads; an
+    explicit OMP_NUM_THREADS; the CPUs the rank is bound to; the node's budget
+    split over the local ranks.  torch.distributed.run exports
+    OMP_NUM_THREADS=1 to every worker of a multi-process launch when the user
+    did not set it, so "1" under such a launch is taken as injected (and the
+    override reported on stderr); any other value is the user's and wins."""
+    env = os.environ if env is None else env
+    if threads:
+        return int(threads)
+    v = env.get("OMP_NUM_THREADS", "")
+    injected = v.strip() == "1" and local_world > 1 and "TORCHELASTIC_RUN_ID" in env
+    if v.strip().isdigit() and int(v) > 0 and not injected:
+        return int(v)
+    n = len(cpus) if cpus else max(1, default_threads // max(1, local_world))
+    if injected and n != 1:
+        print(f"pconv: OMP_NUM_THREADS=1 set by torch.distributed.run ignored: {n} OpenMP threads per rank "
+              "(--threads sets the team)", file=sys.stderr)
+    return n
+
+
 def usage(prog: str) -> str:
     # Same text as the reference (mpi/mpi_convolution.c:344) and the native CLI.
     return f"Error Input!\n{prog} image_name width height repetitions [rgb/grey].\n"
@@ -197,14 +219,7 @@ def main(argv: Optional[List[str]] = None) -> int:
             local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
             cpus = bind_cpu_rank(ctx.local_rank, local_world)
             if a.backend == "omp":
-                # OMP_NUM_THREADS is not a user choice here: torch.distributed.run
-                # exports 1 to every worker of a multi-process launch
-                if a.threads:
-                    n.set_cpu_threads(a.threads)
-                elif cpus is not None:
-                    n.set_cpu_threads(len(cpus))
-                else:
-                    n.set_cpu_threads(max(1, n.default_cpu_threads() // local_world))
+                n.set_cpu_threads(omp_team_size(a.threads, cpus, n.default_cpu_threads(), local_world))
             runner = _CpuBand(a, rank, world, omp=a.backend == "omp")
         b = runner.band
         rb = a.width * _CH[a.channels]

@@ -205,3 +205,33 @@ def test_bench_halo_mode_kwargs():
     assert kw["overlap"]["halo"] == 8 and kw["overlap"]["overlap"]  # T-deep halo, split phases
     with pytest.raises(ValueError):
         bench.mode_kwargs(a, "nope", 8)
+
+
+def test_omp_team_size_precedence():
+    """--threads > a user's OMP_NUM_THREADS > bound CPUs > node budget / ranks;
+    torchrun's injected OMP_NUM_THREADS=1 does not shrink the team."""
+    from pconv.parallel.run import omp_team_size
+
+    tr = {"TORCHELASTIC_RUN_ID": "x"}
+    assert omp_team_size(5, {0, 1}, 16, 2, env=dict(tr, OMP_NUM_THREADS="3")) == 5
+    assert omp_team_size(0, {0, 1}, 16, 2, env=dict(tr, OMP_NUM_THREADS="3")) == 3
+    assert omp_team_size(0, {0, 1, 2}, 16, 2, env=dict(tr, OMP_NUM_THREADS="1")) == 3  # injected
+    assert omp_team_size(0, None, 16, 4, env=dict(tr, OMP_NUM_THREADS="1")) == 4
+    assert omp_team_size(0, None, 16, 1, env={"OMP_NUM_THREADS": "1"}) == 1  # a single process: the user's 1
+    assert omp_team_size(0, None, 16, 2, env={"OMP_NUM_THREADS": "1"}) == 1  # not under torchrun: the user's
+    assert omp_team_size(0, None, 16, 4, env={}) == 4
+    assert omp_team_size(0, None, 2, 4, env={}) == 1
+
+
+def test_import_leaves_omp_wait_policy_unset():
+    """The passive wait policy is set only around the extension's import."""
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    code = f"import os, sys; sys.path.insert(0, {ROOT!r}); import pconv; print(os.environ.get('OMP_WAIT_POLICY'))"
+    env = {k: v for k, v in __import__("os").environ.items() if k not in ("OMP_WAIT_POLICY", "GOMP_SPINCOUNT")}
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "None"
