@@ -200,16 +200,25 @@ def gather_floats(v: float):
 #       Isend/Irecv, inner compute, Wait, edges) with a T-deep halo: an
 #       exchange every fused launch on the comm stream, the interior launch
 #       concurrently on the compute stream, the edge strips after the halo
-#       event.
-HALO_MODES = ("slot_exchange", "slot_exchange_direct", "event", "overlap")
+#       event;
+#   ipc: slot_exchange's pipeline with the HIP-IPC transport instead of RCCL
+#       (ipc_halo.hpp): each rank pulls its neighbours' boundary rows straight
+#       out of their frames (opened once with hipIpcOpenMemHandle), ordered by
+#       device-side flag kernels — no communication-library kernel; every
+#       image ONE captured graph.
+HALO_MODES = ("slot_exchange", "slot_exchange_direct", "event", "overlap", "ipc")
+
+
+def mode_transport(mode: str, transport: str) -> str:
+    return "ipc" if mode == "ipc" else transport
 
 
 def mode_kwargs(a, mode: str, fuse: int) -> dict:
     kw = dict(preload_halo=False, slots=a.slots, variant=a.variant, fuse=a.fuse, overlap=not a.no_overlap,
               halo=a.halo, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent])
-    if mode in ("slot_exchange", "slot_exchange_direct"):
+    if mode in ("slot_exchange", "slot_exchange_direct", "ipc"):
         kw["slot_exchange"] = True
-        kw["graph_capture"] = mode == "slot_exchange"
+        kw["graph_capture"] = mode != "slot_exchange_direct"
     elif mode == "overlap":
         # T-deep ghost zone: one exchange per fused launch on the comm stream
         # beside the interior launch, edges after the halo event (event-ordered
@@ -235,6 +244,7 @@ def measure_mode(a, mode, ref_rows, world, rank, device, transport, fuse, oracle
     from pconv.parallel.bootstrap import barrier, sum_over_ranks
     from pconv.parallel.dist_engine import DistributedBlur
 
+    transport = mode_transport(mode, transport)
     res = {"status": "ok", "transport": transport}
     xb = None
     try:
@@ -379,7 +389,8 @@ def main():
         world, rank = (int(v) for v in a.emulate.split(":"))
         a.preload_halo, transport, head_transport = True, "none", "none"
         if a.emulate_halo != "preload":
-            a.preload_halo, transport, head_transport = False, "rccl", "rccl"
+            t = mode_transport(a.emulate_halo, "rccl")
+            a.preload_halo, transport, head_transport = False, t, t
     device = ctx.local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     # host thread + first-touch pinned buffers on the GPU's own socket
@@ -390,8 +401,8 @@ def main():
             a.width, a.height, a.channels, a.filter, a.reps, rank=rank, world=world, device=device,
             preload_halo=True, slots=1, transport="none").engine.fuse
         blur = DistributedBlur(a.width, a.height, a.channels, a.filter, a.reps, rank=rank, world=world,
-                               device=device, transport="rccl", self_neighbours=True,
-                               **mode_kwargs(a, a.emulate_halo, fuse0))
+                               device=device, transport=mode_transport(a.emulate_halo, "rccl"),
+                               self_neighbours=True, **mode_kwargs(a, a.emulate_halo, fuse0))
     else:
         blur = DistributedBlur(a.width, a.height, a.channels, a.filter, a.reps, rank=rank, world=world,
                                device=device, halo=a.halo, fuse=a.fuse, overlap=not a.no_overlap,
@@ -560,8 +571,9 @@ def main():
                               "rank's step rate x full-image pixels (proxy, not a multi-GPU measurement)"
             out["config"]["halo_mode"] = a.emulate_halo
             if a.emulate_halo != "preload":
-                out["emulated"] += "; halos exchanged with the rank itself (RCCL send/recv to self): real " \
-                                   "exchange costs, ghost contents not those of its neighbours"
+                how = "IPC pulls of its own rows" if a.emulate_halo == "ipc" else "RCCL send/recv to self"
+                out["emulated"] += f"; halos exchanged with the rank itself ({how}): real exchange costs, ghost " \
+                                   "contents not those of its neighbours"
 
     import threading
 

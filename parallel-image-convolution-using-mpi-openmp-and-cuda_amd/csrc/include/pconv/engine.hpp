@@ -103,6 +103,8 @@ class BandEngine {
   uint8_t* dst_frame() const { return frame_[cur_ ^ 1].data() + lay_.offset(0); }
   // Frame `which` (0/1) at (owned row 0, data column 0); cur() = the source frame.
   uint8_t* frame_at(int which) const { return frame_[which & 1].data() + lay_.offset(0); }
+  // Base of frame `which`'s allocation (hipIpcGetMemHandle needs it).
+  uint8_t* frame_base(int which) const { return frame_[which & 1].data(); }
   int cur() const { return cur_; }
 
   // Copy frame-local rows [r_begin, r_end) from host (pointer at row r_begin).

@@ -1,0 +1,156 @@
+// HIP-IPC halo transport (see ipc_halo.hpp).
+#include "pconv/ipc_halo.hpp"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstring>
+
+#include "pconv/trace.hpp"
+
+namespace pconv {
+
+namespace {
+
+size_t segment_bytes(int world, int slots) {
+  return static_cast<size_t>(world) * static_cast<size_t>(slots) * sizeof(IpcFlags);
+}
+
+std::string shm_path(const std::string& name) { return name.empty() || name[0] != '/' ? "/" + name : name; }
+
+}  // namespace
+
+void ipc_create_segment(const std::string& name, int world, int slots) {
+  PCONV_CHECK(world >= 1 && slots >= 1, "ipc segment: bad world / slots");
+  const std::string p = shm_path(name);
+  const int fd = ::shm_open(p.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+  PCONV_CHECK(fd >= 0, "ipc segment: shm_open(" + p + ") failed: " + std::strerror(errno));
+  const size_t n = segment_bytes(world, slots);
+  const bool ok = ::ftruncate(fd, static_cast<off_t>(n)) == 0;  // zero-filled
+  ::close(fd);
+  if (!ok) {
+    ::shm_unlink(p.c_str());
+    PCONV_FAIL("ipc segment: ftruncate failed: " + std::string(std::strerror(errno)));
+  }
+}
+
+void ipc_unlink_segment(const std::string& name) { (void)::shm_unlink(shm_path(name).c_str()); }
+
+IpcHaloTransport::IpcHaloTransport(BandEngine& e, const std::string& segment, int slot, int slots, double timeout_s)
+    : eng_(&e), rank_(e.band().rank), world_(e.band().world), slot_(slot), slots_(slots), segment_(segment) {
+  PCONV_CHECK(slot >= 0 && slot < slots, "ipc transport: slot out of range");
+  seg_bytes_ = segment_bytes(world_, slots_);
+  const std::string p = shm_path(segment);
+  const int fd = ::shm_open(p.c_str(), O_RDWR, 0600);
+  PCONV_CHECK(fd >= 0, "ipc transport: shm_open(" + p + ") failed: " + std::strerror(errno));
+  struct stat st {};
+  PCONV_CHECK(::fstat(fd, &st) == 0 && static_cast<size_t>(st.st_size) >= seg_bytes_,
+              "ipc transport: flag segment smaller than world x slots blocks");
+  host_ = ::mmap(nullptr, seg_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  ::close(fd);
+  PCONV_CHECK(host_ != MAP_FAILED, "ipc transport: mmap failed");
+  set_device(e.options().device);
+  PCONV_HIP_CHECK(hipHostRegister(host_, seg_bytes_, hipHostRegisterMapped));
+  void* d = nullptr;
+  PCONV_HIP_CHECK(hipHostGetDevicePointer(&d, host_, 0));
+  dflags_ = static_cast<IpcFlags*>(d);
+  int khz = 0;
+  PCONV_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e.options().device));
+  timeout_ticks_ = static_cast<uint64_t>(timeout_s * static_cast<double>(khz > 0 ? khz : 100000) * 1000.0);
+  handles_.resize(2 * sizeof(hipIpcMemHandle_t));
+  for (int i = 0; i < 2; ++i) {
+    hipIpcMemHandle_t h;
+    own_base_[i] = e.frame_base(i);
+    PCONV_HIP_CHECK(hipIpcGetMemHandle(&h, own_base_[i]));
+    std::memcpy(handles_.data() + i * sizeof(h), &h, sizeof(h));
+  }
+}
+
+IpcHaloTransport::~IpcHaloTransport() {
+  for (uint8_t** side : {peer_up_, peer_down_})
+    for (int i = 0; i < 2; ++i)
+      if (side[i] && side[i] != own_base_[i]) (void)hipIpcCloseMemHandle(side[i]);
+  if (host_ && host_ != MAP_FAILED) {
+    (void)hipHostUnregister(host_);
+    ::munmap(host_, seg_bytes_);
+  }
+}
+
+void IpcHaloTransport::connect(const std::vector<uint8_t>& up_handles, const std::vector<uint8_t>& down_handles) {
+  PCONV_CHECK(!connected_, "ipc transport: already connected");
+  const Band& b = eng_->band();
+  const FrameLayout& L = eng_->layout();
+  auto open = [&](const std::vector<uint8_t>& hs, uint8_t** out) {
+    PCONV_CHECK(hs.size() == 2 * sizeof(hipIpcMemHandle_t), "ipc transport: bad handle blob");
+    if (hs == handles_) {
+      // This engine is its own neighbour (one-process emulation of a rank
+      // whose halos move: the band's own rows come back as its ghost rows,
+      // like RCCL send/recv to self).  A process cannot open its own handle.
+      for (int i = 0; i < 2; ++i) out[i] = own_base_[i];
+      own_ = true;
+      return;
+    }
+    for (int i = 0; i < 2; ++i) {
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, hs.data() + i * sizeof(h), sizeof(h));
+      void* p = nullptr;
+      PCONV_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+      out[i] = static_cast<uint8_t*>(p);
+    }
+  };
+  if (b.up >= 0) {
+    PCONV_CHECK(!up_handles.empty(), "ipc transport: band has an upper neighbour but no handles");
+    open(up_handles, peer_up_);
+    lay_up_ = FrameLayout::make(L.row_bytes, row_band(eng_->geom().height, world_, b.up).rows, L.halo);
+    PCONV_CHECK(lay_up_.pitch == L.pitch, "ipc transport: neighbour pitch differs");
+  }
+  if (b.down >= 0) {
+    PCONV_CHECK(!down_handles.empty(), "ipc transport: band has a lower neighbour but no handles");
+    open(down_handles, peer_down_);
+    lay_down_ = FrameLayout::make(L.row_bytes, row_band(eng_->geom().height, world_, b.down).rows, L.halo);
+    PCONV_CHECK(lay_down_.pitch == L.pitch, "ipc transport: neighbour pitch differs");
+  }
+  connected_ = true;
+}
+
+void IpcHaloTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream) {
+  TraceRange tr("pconv.halo.ipc");
+  PCONV_CHECK(connected_ && &e == eng_, "ipc transport: not connected to this engine");
+  const FrameLayout& L = e.layout();
+  const Band& b = e.band();
+  PCONV_CHECK(depth >= 1 && depth <= L.halo && depth <= b.rows, "ipc halo: bad depth");
+  const int me = rank_ * slots_ + slot_;
+  const int up = b.up >= 0 ? b.up * slots_ + slot_ : -1;
+  const int down = b.down >= 0 ? b.down * slots_ + slot_ : -1;
+  const int par = e.cur();  // neighbours hold the same time level in the frame of the same parity
+  const size_t n = static_cast<size_t>(depth * L.pitch);
+  uint8_t* mine = e.frame_base(par);
+  launch_ipc_signal_wait(dflags_, me, up, down, timeout_ticks_, stream);
+  // up: its last `depth` owned rows -> my ghost rows [-depth, 0); down: its
+  // first `depth` owned rows -> my ghost rows [rows, rows + depth).  Whole
+  // pitch-aligned rows (pads included: zero in every frame).
+  const uint8_t* src_up = up >= 0 ? peer_up_[par] + lay_up_.offset(lay_up_.rows - depth) - kPadLeft : nullptr;
+  const uint8_t* src_down = down >= 0 ? peer_down_[par] + lay_down_.offset(0) - kPadLeft : nullptr;
+  launch_ipc_pull(dflags_, me, mine + L.offset(-depth) - kPadLeft, src_up, mine + L.offset(b.rows) - kPadLeft,
+                  src_down, static_cast<int64_t>(n), stream);
+  launch_ipc_ack_wait(dflags_, me, up, down, timeout_ticks_, stream);
+  ++enqueued_;
+}
+
+uint32_t IpcHaloTransport::device_count() const {
+  const auto* f = static_cast<const volatile IpcFlags*>(host_);
+  return f[rank_ * slots_ + slot_].count;
+}
+
+void IpcHaloTransport::check() const {
+  const auto* f = static_cast<const volatile IpcFlags*>(host_);
+  const uint32_t err = f[rank_ * slots_ + slot_].err;
+  PCONV_CHECK(err == 0, std::string("ipc halo: rank ") + std::to_string(rank_) + " slot " + std::to_string(slot_) +
+                            (err == 1 ? ": timed out waiting for a neighbour's rows"
+                                      : ": timed out waiting for a neighbour to copy this rank's rows"));
+}
+
+}  // namespace pconv

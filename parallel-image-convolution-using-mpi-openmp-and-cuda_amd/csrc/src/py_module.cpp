@@ -13,6 +13,7 @@
 #include "pconv/cpu_stencil.hpp"
 #include "pconv/device.hpp"
 #include "pconv/engine.hpp"
+#include "pconv/ipc_halo.hpp"
 #include "pconv/kernels.hpp"
 #include "pconv/partition.hpp"
 #include "pconv/selftest.hpp"
@@ -647,6 +648,32 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def("download", [](LocalCluster& c, py::buffer host) { c.download(host_view(host, true).ptr); })
       .def("exchanges", [](LocalCluster& c) { return c.engine(0).last_stats().exchanges; })
       .def_property_readonly("size", &LocalCluster::size);
+
+  // ---------------------------------------------------------------- HIP IPC halos
+  m.def("ipc_create_segment", &ipc_create_segment, py::arg("name"), py::arg("world"), py::arg("slots"),
+        "create the zeroed shared flag segment of an IPC halo job (one rank)");
+  m.def("ipc_unlink_segment", &ipc_unlink_segment, py::arg("name"),
+        "remove the segment's name (mappings stay valid; call once every rank has mapped it)");
+  py::class_<IpcHaloTransport, HaloTransport, std::shared_ptr<IpcHaloTransport>>(m, "IpcHaloTransport")
+      .def(py::init([](BandEngine& e, const std::string& segment, int slot, int slots, double timeout_s) {
+             return std::make_shared<IpcHaloTransport>(e, segment, slot, slots, timeout_s);
+           }),
+           py::arg("engine"), py::arg("segment"), py::arg("slot") = 0, py::arg("slots") = 1,
+           py::arg("timeout_s") = 30.0, py::keep_alive<1, 2>())
+      .def("local_handles", [](const IpcHaloTransport& t) {
+        const auto v = t.local_handles();
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+      })
+      .def("connect",
+           [](IpcHaloTransport& t, py::bytes up, py::bytes down) {
+             const std::string u = up, d = down;
+             t.connect(std::vector<uint8_t>(u.begin(), u.end()), std::vector<uint8_t>(d.begin(), d.end()));
+           },
+           py::arg("up"), py::arg("down"))
+      .def_property_readonly("connected", &IpcHaloTransport::connected)
+      .def_property_readonly("enqueued", &IpcHaloTransport::enqueued)
+      .def_property_readonly("device_count", &IpcHaloTransport::device_count)
+      .def("check", &IpcHaloTransport::check, "raise if a wait of this rank timed out (after the stream drained)");
 
   // ---------------------------------------------------------------- RCCL
   m.def("rccl_unique_id", []() {

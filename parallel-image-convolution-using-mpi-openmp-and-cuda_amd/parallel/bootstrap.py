@@ -89,6 +89,49 @@ def make_rccl_comm(device: int, group=None):
     return n.RcclComm(uid, rank, world, device)
 
 
+def make_ipc_transports(engines, timeout_s: float = 30.0, group=None):
+    """HIP-IPC halo transports for this rank's pipeline slots (collective).
+
+    Rank 0 creates the job's shared flag segment and broadcasts its name;
+    every rank maps it, exports its slot engines' frames with
+    hipIpcGetMemHandle, the handles of all ranks are gathered, and each slot
+    opens its neighbours' frames (slot k of rank r exchanges with slot k of
+    ranks r-1 and r+1).  Once every rank has mapped the segment its name is
+    unlinked, so nothing is left in /dev/shm whatever happens later.
+    Replaces the reference's MPI_Isend/Irecv set-up of neighbour ranks
+    (mpi/mpi_convolution.c:142-149) for ranks on one node."""
+    import secrets
+
+    n = require_native()
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    slots = len(engines)
+    name = None
+    if rank == 0:
+        name = f"/pconv_ipc_{os.getpid()}_{secrets.token_hex(4)}"
+        n.ipc_create_segment(name, world, slots)
+    try:
+        name = broadcast_bytes(name.encode() if name else None, 0, group).decode()
+        ts = [n.IpcHaloTransport(e, name, k, slots, float(timeout_s)) for k, e in enumerate(engines)]
+    finally:
+        barrier(group)
+        if rank == 0:
+            n.ipc_unlink_segment(name)
+    mine = [t.local_handles() for t in ts]
+    if dist.is_initialized() and world > 1:
+        every = [None] * world
+        dist.all_gather_object(every, mine, group=group)
+    else:
+        every = [mine]
+    for k, (t, e) in enumerate(zip(ts, engines)):
+        b = e.band
+        up = every[b.up][k] if b.up >= 0 else b""
+        down = every[b.down][k] if b.down >= 0 else b""
+        t.connect(up, down)
+    barrier(group)
+    return ts
+
+
 def max_over_ranks(value: float, group=None) -> float:
     """Max of a float over ranks (the reference's Send/Recv max-gather,
     ``mpi/mpi_convolution.c:264-275``)."""

@@ -58,7 +58,8 @@ class DistributedBlur:
                  overlap: bool = True, preload_halo: bool = False, comm=None, slots: int = 2,
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
                  step_graphs: Optional[bool] = None, graph_capture: bool = True, slot_exchange: bool = False,
-                 self_neighbours: bool = False, slot_comm: bool = False, stream_chunks: int = 0):
+                 self_neighbours: bool = False, slot_comm: bool = False, stream_chunks: int = 0,
+                 ipc_timeout_s: float = 30.0):
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -104,7 +105,9 @@ class DistributedBlur:
         # exchange in stream order between upload and launches — slots overlap
         # each other instead of the exchange overlapping its own image.
         self.slot_exchange = bool(slot_exchange) and self.world > 1
-        if self.slot_exchange and transport != "rccl":
+        if transport == "ipc" and self.world > 1 and not free and not self.slot_exchange:
+            raise ValueError("transport 'ipc' exchanges per slot: use slot_exchange=True (one transport per slot)")
+        if self.slot_exchange and transport not in ("rccl", "ipc"):
             graph_capture = False  # host-staged transports synchronise: they cannot be captured
         # With RCCL, an exchange image is ONE captured graph (upload, ncclSend/
         # ncclRecv of the ghost zone, launches, download): one host call per
@@ -139,7 +142,16 @@ class DistributedBlur:
         self.transport = None
         self.slot_comms = []
         self.slot_transports = []
-        if self.slot_exchange:
+        self.ipc = []
+        if self.slot_exchange and transport == "ipc":
+            # device-side pulls of the neighbours' rows through HIP IPC, ordered
+            # by flag kernels (ipc_halo.hpp); one transport per slot
+            from .bootstrap import make_ipc_transports
+
+            self.ipc = make_ipc_transports([self.pipe.slot(k) for k in range(self.slots)], ipc_timeout_s)
+            for k, t in enumerate(self.ipc):
+                self.pipe.attach_slot_transport(k, t)
+        elif self.slot_exchange:
             for k in range(self.slots):
                 if transport == "rccl":
                     c = make_rccl_comm(self.device)
@@ -152,9 +164,9 @@ class DistributedBlur:
                     self.slot_transports.append(t)
                     self.pipe.attach_slot_transport(k, t)
                 else:
-                    raise ValueError(f"slot_exchange needs transport rccl or gloo-host, not {transport!r}")
+                    raise ValueError(f"slot_exchange needs transport rccl, ipc or gloo-host, not {transport!r}")
             self.comm = self.slot_comms[0] if self.slot_comms else None
-        elif self.world > 1 and transport != "none":  # "none": exchange-free images only
+        elif self.world > 1 and transport not in ("none", "ipc"):  # exchange-free images need none
             if transport == "rccl":
                 self.comm = comm if comm is not None else make_rccl_comm(self.device)
                 self.pipe.attach_rccl(self.comm)
@@ -164,7 +176,7 @@ class DistributedBlur:
                 self.transport = GlooHostTransport()
                 self.pipe.attach_transport(self.transport)
             else:
-                raise ValueError(f"unknown transport {transport!r} (rccl|gloo-host|none)")
+                raise ValueError(f"unknown transport {transport!r} (rccl|ipc|gloo-host|none)")
 
     # ------------------------------------------------------------ inputs
     @property
@@ -219,6 +231,8 @@ class DistributedBlur:
             for k, c in enumerate(self.slot_comms):
                 c.wait(self.pipe.slot(k).compute_stream, float(timeout_s))
         self.pipe.drain()
+        for t in self.ipc:
+            t.check()  # a timed-out device-side wait (a stalled neighbour) raises here
         self._pending = False
 
     def step(self, reps: int) -> np.ndarray:

@@ -185,16 +185,16 @@ def test_bench_metric_names():
 
 
 def test_bench_halo_mode_kwargs():
-    """The five N>1 pipelines bench.py times (slot_exchange, slot_exchange_direct,
-    event, overlap after the pre-loaded headline) map to the intended
-    DistributedBlur configurations."""
+    """The N>1 pipelines bench.py times after the pre-loaded headline
+    (slot_exchange, slot_exchange_direct, event, overlap, ipc) map to the
+    intended DistributedBlur configurations and transports."""
     import importlib.util
     from types import SimpleNamespace
 
     spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(ROOT, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    assert bench.HALO_MODES == ("slot_exchange", "slot_exchange_direct", "event", "overlap")
+    assert bench.HALO_MODES == ("slot_exchange", "slot_exchange_direct", "event", "overlap", "ipc")
     a = SimpleNamespace(slots=3, variant="auto", fuse=None, no_overlap=False, halo=None, concurrent="off")
     kw = {m: bench.mode_kwargs(a, m, 8) for m in bench.HALO_MODES}
     for m, k in kw.items():
@@ -203,6 +203,8 @@ def test_bench_halo_mode_kwargs():
     assert kw["slot_exchange_direct"]["slot_exchange"] and not kw["slot_exchange_direct"]["graph_capture"]
     assert not kw["event"].get("slot_exchange") and kw["event"]["halo"] is None  # deep auto halo
     assert kw["overlap"]["halo"] == 8 and kw["overlap"]["overlap"]  # T-deep halo, split phases
+    assert kw["ipc"]["slot_exchange"] and kw["ipc"]["graph_capture"]  # one captured graph per image
+    assert bench.mode_transport("ipc", "rccl") == "ipc" and bench.mode_transport("event", "rccl") == "rccl"
     with pytest.raises(ValueError):
         bench.mode_kwargs(a, "nope", 8)
 

@@ -1,0 +1,120 @@
+"""On-device, cross-process halo exchange on ONE GPU: HIP IPC (ipc_halo.hpp).
+
+N processes share the gpurun box's single GPU (RCCL refuses two ranks on one
+device; IPC does not).  Each rank exports its slot frames with
+hipIpcGetMemHandle, opens its neighbours' frames, and every exchange pulls the
+neighbours' boundary rows device-to-device, ordered by flag kernels on the
+rank's own stream — the path the 8-GPU node takes over xGMI, with no host
+staging.  Every image of every rank is compared with the NumPy oracle, for
+N = 2..8, ghost zones shallower than the repetitions (several exchanges per
+image), with and without the interior || exchange split, captured graphs and
+direct issue, grey / RGB and a float filter.  The reference's algorithm being
+replaced: Isend/Irecv of boundary rows, inner compute, Wait, edges
+(mpi/mpi_convolution.c:157-234).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cfg, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    from pconv.parallel.bootstrap import barrier, init_distributed, shutdown
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    ctx = init_distributed("gloo")
+    try:
+        blur = DistributedBlur(cfg["w"], cfg["h"], cfg["ch"], cfg["filter"], cfg["reps"], rank=rank, world=world,
+                               device=0, halo=cfg["halo"], fuse=cfg["fuse"], slots=cfg["slots"], transport="ipc",
+                               slot_exchange=True, graph_capture=cfg["graph"], slot_comm=cfg["overlap"],
+                               overlap=cfg["overlap"], ipc_timeout_s=cfg.get("timeout", 30.0))
+        if cfg.get("stall") and rank == world - 1:
+            barrier()  # set-up done; this rank then never exchanges
+            q.put((rank, None, None, 0))
+            barrier()
+            return
+        barrier()
+        blur.load_synthetic(cfg["seed"])
+        ks = [blur.submit(cfg["reps"]) for _ in range(cfg["images"])]
+        err = None
+        try:
+            blur.drain()
+        except Exception as e:  # noqa: BLE001 - reported to the test
+            err = str(e)
+        outs = [blur.outputs[k].copy() for k in ks[-cfg["slots"]:]]
+        q.put((rank, blur.band.y0, outs if err is None else err, sum(t.enqueued for t in blur.ipc)))
+        barrier()  # every rank done with its neighbours' frames before any exits
+        del blur
+    finally:
+        shutdown(ctx)
+
+
+def _run(pconv_mod, world, cfg, timeout=300):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=timeout) for _ in range(world)], key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return res
+
+
+@pytest.mark.parametrize("world,ch,filt,halo,fuse,reps,graph,overlap", [
+    (2, "rgb", "gaussian", 8, 8, 40, True, False),     # one zone exchange per image, captured
+    (2, "grey", "gaussian", 4, 4, 19, True, True),     # 5 exchanges per image, split phases, captured
+    (3, "rgb", "gaussian", 6, 3, 19, False, True),     # direct issue, interior || exchange
+    (4, "rgb", "box", 4, 4, 13, True, False),          # float filter
+    (4, "grey", "edge", 3, 3, 11, False, False),
+    (8, "rgb", "gaussian", 8, 8, 40, True, False),     # the 8-way split of the headline's shape
+    (8, "grey", "gaussian", 5, 5, 23, True, True),
+])
+def test_ipc_halo_bit_exact(pconv_mod, world, ch, filt, halo, fuse, reps, graph, overlap):
+    w, h, slots = 57, 160, 2
+    cfg = dict(w=w, h=h, ch=ch, filter=filt, reps=reps, halo=halo, fuse=fuse, slots=slots, graph=graph,
+               overlap=overlap, seed=11, images=slots + 2)
+    res = _run(pconv_mod, world, cfg)
+    img = pconv_mod.synthetic_image(w, h, ch, seed=11)
+    ref = pconv_mod.numpy_convolve(img, reps, filt).reshape(h, -1)
+    per_image = -(-reps // halo)  # exchanges per image (ghost zone of `halo` rows)
+    for rank, y0, outs, n_exch in res:
+        assert not isinstance(outs, str), f"rank {rank}: {outs}"
+        for o in outs:
+            assert np.array_equal(o, ref[y0:y0 + o.shape[0]]), (rank, world)
+        assert n_exch >= per_image * cfg["images"] - 1, (rank, n_exch)
+
+
+def test_ipc_stalled_neighbour_times_out(pconv_mod):
+    """A neighbour that never exchanges: the waiting rank's flag kernel gives
+    up after its timeout (no wave spins forever) and drain() raises."""
+    cfg = dict(w=40, h=64, ch="grey", filter="gaussian", reps=8, halo=8, fuse=8, slots=1, graph=True,
+               overlap=False, seed=3, images=1, stall=True, timeout=2.0)
+    res = _run(pconv_mod, 2, cfg, timeout=200)
+    r0 = res[0]
+    assert isinstance(r0[2], str) and "timed out" in r0[2], r0

@@ -97,7 +97,7 @@ def test_bench_torchrun_rehearsal(world, extra):
     assert meta["runtime"]["hip_runtime_version"] > 0 and meta["runtime"]["hip_runtime_path"]
     modes = meta["halo_modes"]
     head = "event" if "--halo-mode" in extra else "preload"
-    assert set(modes) == {head, "slot_exchange", "slot_exchange_direct", "event", "overlap"}, modes
+    assert set(modes) == {head, "slot_exchange", "slot_exchange_direct", "event", "overlap", "ipc"}, modes
     for m, r in modes.items():
         assert r["status"] == "ok", (m, r)
         assert r["ms_per_step"] > 0
