@@ -140,6 +140,9 @@ def parse():
                    help="after timing (outside the timed region), compare every rank's newest image, and every halo "
                         "mode's at N>1, with the CPU oracle; 'mismatches' in the JSON line (default on)")
     p.add_argument("--no-check", dest="check", action="store_false", help="skip the oracle check (sweeps)")
+    p.add_argument("--native", action="store_true",
+                   help="run the same serving step on the native stack: the in-tree `conv --bench` (ROCm's HIP "
+                        "runtime, no torch; its fork launcher for N > 1) and print its JSON line")
     return p.parse_args()
 
 
@@ -349,10 +352,45 @@ def copy_floor_ms(in_bytes: int, out_bytes: int, device: int, iters: int = 8):
     return h2d, d2h
 
 
+def run_native(a) -> int:
+    """`bench.py --native`: the serving step of the `conv` binary (C++ fork
+    launcher + BandPipeline on the HIP runtime it links) instead of this
+    torch process; its single JSON line is passed through.  Nothing here
+    touches the GPU (the child is started before any HIP call)."""
+    import subprocess
+
+    if int(os.environ.get("RANK", "0")) != 0:
+        return 0  # under torchrun: rank 0 runs the native launcher for all ranks
+    conv = os.path.join(ROOT, "parallel-image-convolution-using-mpi-openmp-and-cuda_amd", "bin", "conv")
+    cmd = [conv, "synthetic.raw", str(a.width), str(a.height), str(a.reps), a.channels, "--synthetic", str(a.seed),
+           "--gpus", str(a.gpus), "--bench", str(a.steps), "--warmup", str(min(a.warmup, 100)), "--slots",
+           str(a.slots), "--stream-chunks", str(a.stream_chunks), "--filter", a.filter]
+    if a.fuse:
+        cmd += ["--fuse", str(a.fuse)]
+    if a.check:
+        cmd.append("--check")
+    if a.transport == "gloo-host":
+        cmd += ["--transport", "shm"]  # rehearsal: ranks may share one GPU
+    env = dict(os.environ)
+    want = a.hw_queues if a.hw_queues else max(8, a.slots + 3)  # as for the torch pipeline below
+    if a.hw_queues or int(env.get("GPU_MAX_HW_QUEUES", "4")) < want:
+        env["GPU_MAX_HW_QUEUES"] = str(min(want, 32))
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env)
+    sys.stderr.write(r.stderr)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or len(lines) != 1:
+        sys.stderr.write(r.stdout)
+        return r.returncode or 1
+    print(lines[0], flush=True)
+    return 0
+
+
 def main():
     a = parse()
     if a.slots is None:
         a.slots = 3
+    if a.native:
+        sys.exit(run_native(a))
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not a.emulate:
         sys.exit(spawn_ranks(a))
     # One hardware queue per stream of the serving pipeline (H2D, D2H, comm and

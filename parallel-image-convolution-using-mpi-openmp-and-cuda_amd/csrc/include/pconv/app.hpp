@@ -52,4 +52,8 @@ AppReport run_app(const CliConfig& cfg, JobCache* cache = nullptr);
 
 std::string report_json(const CliConfig& cfg, const AppReport& r);
 
+// `--bench K`: bench.py's serving step on the native stack (fork launcher for
+// N > 1); returns bench.py's JSON line.
+std::string run_bench(const CliConfig& cfg);
+
 }  // namespace pconv

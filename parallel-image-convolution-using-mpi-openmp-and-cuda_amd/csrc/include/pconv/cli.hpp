@@ -50,6 +50,11 @@ struct CliConfig {
   int warmup = 1;                  // untimed runs of the whole schedule on the zeroed frames first
   std::string server;              // client mode: run the job on the resident server at this socket
   int copies = -1;                 // host<->device copies: -1 auto, 0 SDMA (hipMemcpy2DAsync), 1 CU kernels
+  // Serving bench (bench.py's step on the native stack): K timed images, each
+  // H2D + reps + D2H, `slots` in flight; 0 = off (a normal run).
+  int bench_steps = 0;
+  int slots = 3;
+  int stream_chunks = 0;  // rows streamed within each image (EngineOptions::stream_chunks)
 };
 
 // Parse argv.  Throws pconv::Error with the message to print on bad input.

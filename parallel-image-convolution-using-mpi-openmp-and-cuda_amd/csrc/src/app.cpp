@@ -580,7 +580,215 @@ AppReport run_multi(const CliConfig& c) {
   return r;
 }
 
+
+// ------------------------------------------------------------------ bench
+// `conv ... --bench K`: bench.py's serving step (H2D + reps + D2H per image,
+// `slots` images in flight, one BandPipeline per rank, pre-loaded ghost
+// rows) on the NATIVE stack — the HIP runtime this binary links (ROCm), no
+// torch, no Python — with the same K-step timing between barriers, the max
+// over ranks, the single-image latency, the box's PCIe pair floor and an
+// oracle check of every rank's newest image.  Ranks are forked before any
+// HIP call (like run_multi); N = 1 runs in this process.
+struct BenchShared {
+  SharedState st;            // barrier + error reporting (run_multi's)
+  double sec[kMaxRanks];     // timed region per rank
+  double lat_ms[kMaxRanks];  // median single-image latency per rank
+  double pair_ms[kMaxRanks];
+  int launches, halo, fuse, hip_version;
+  char hip_path[512];
+};
+
+constexpr double kBaselineMpix = 190.3;  // CUDA 1920x2520 RGB 40 reps end to end, GTX 970
+
+void bench_rank(const CliConfig& c, BenchShared* sh, uint8_t* image, int rank) {
+  set_error_rank(rank);
+  const ImageGeom g = geom_of(c);
+  const int world = c.gpus;
+  const int ndev = device_count();
+  PCONV_CHECK(c.transport == "shm" || ndev >= world,
+              "need " + std::to_string(world) + " GPUs, " + std::to_string(ndev) + " visible (--transport shm lets "
+              "bench ranks share one GPU)");
+  const int device = rank % ndev;
+  set_device(device);
+  if (world > 1) (void)bind_to_device_numa(device);
+  const Filter f = Filter::by_name(c.filter);
+  const Band b = row_band(g.height, world, rank);
+  EngineOptions o = engine_options(c, g, world, device);
+  // Pre-loaded ghost zone deep enough for every repetition (exchange-free
+  // images, like bench.py's headline): rows of the band's dependency cone.
+  if (world > 1 && c.halo == 0 && c.reps <= g.height / world) o.halo_depth = std::max(c.reps, o.fuse);
+  o.stream_chunks = c.stream_chunks;
+  BandPipeline pipe(g, b, f, o, c.slots, -1, /*slot_streams=*/true, /*step_graphs=*/true, /*slot_comm=*/false);
+  BandEngine& e0 = pipe.slot(0);
+  const int64_t d = e0.layout().halo;
+  const int64_t above = world > 1 ? std::min<int64_t>(d, b.y0) : 0;
+  const int64_t below = world > 1 ? std::min<int64_t>(d, g.height - (b.y0 + b.rows)) : 0;
+  PCONV_CHECK(e0.exchange_free(c.reps, world > 1),
+              "--bench needs exchange-free images: " + std::to_string(c.reps) + " repetitions with a " +
+                  std::to_string(d) + "-row ghost zone");
+  const int64_t rb = g.row_bytes(), in_rows = b.rows + above + below;
+  std::vector<PinnedBuffer> ins, outs;
+  for (int k = 0; k < c.slots; ++k) {
+    ins.emplace_back(static_cast<size_t>(in_rows * rb));
+    outs.emplace_back(static_cast<size_t>(b.rows * rb));
+  }
+  load_rows(c, g, b.y0 - above, in_rows, ins[0].data(), rb);
+  for (int k = 1; k < c.slots; ++k) std::memcpy(ins[k].data(), ins[0].data(), ins[0].size());
+  int64_t n = 0;
+  auto submit = [&]() {
+    const int k = static_cast<int>(n++ % c.slots);
+    pipe.submit(ins[k].data(), -above, b.rows + below, outs[k].data(), c.reps);
+    return k;
+  };
+  for (int i = 0; i < c.warmup; ++i) submit();
+  pipe.drain();
+  shm_barrier(&sh->st, world, c.timeout_s);
+  const double t0 = wall_seconds();
+  for (int i = 0; i < c.bench_steps; ++i) submit();
+  pipe.drain();
+  const double t1 = wall_seconds();
+  shm_barrier(&sh->st, world, c.timeout_s);
+  sh->sec[rank] = t1 - t0;
+  // one image alone (nothing else queued): the reference GPU_convolution() scope
+  std::vector<double> lat;
+  int last = 0;
+  for (int i = 0; i < 7; ++i) {
+    const double a = wall_seconds();
+    last = submit();
+    pipe.drain();
+    lat.push_back((wall_seconds() - a) * 1e3);
+  }
+  std::sort(lat.begin(), lat.end());
+  sh->lat_ms[rank] = lat[lat.size() / 2];
+  std::memcpy(image + b.y0 * rb, outs[last].data(), static_cast<size_t>(b.rows * rb));
+  sh->pair_ms[rank] = copy_pair_floor_ms(device, rb, in_rows, b.rows, 8);
+  if (rank == 0) {
+    sh->launches = e0.last_stats().launches;
+    sh->halo = static_cast<int>(d);
+    sh->fuse = e0.options().fuse;
+    const HipRuntimeInfo h = hip_runtime_info();
+    sh->hip_version = h.runtime_version;
+    std::snprintf(sh->hip_path, sizeof(sh->hip_path), "%s", h.runtime_path.c_str());
+  }
+  shm_barrier(&sh->st, world, c.timeout_s);
+}
+
+std::string bench_metric(const CliConfig& c) {
+  const bool head = c.width == 1920 && c.height == 2520 && c.channels == Channels::Rgb && c.reps == 40 &&
+                    c.filter == "gaussian";
+  if (head) return "Mpixels/sec (and wall-time) for 1920x2520 RGB, 40 reps at 1/2/4/8 MI355X";
+  std::string ch = channels_name(c.channels);
+  for (auto& x : ch) x = static_cast<char>(std::toupper(static_cast<unsigned char>(x)));
+  return "Mpixels/sec (and wall-time) for " + std::to_string(c.width) + "x" + std::to_string(c.height) + " " + ch +
+         ", " + std::to_string(c.reps) + " reps" + (c.filter == "gaussian" ? "" : " " + c.filter) +
+         " at 1/2/4/8 MI355X";
+}
+
+std::string run_bench_impl(const CliConfig& c) {
+  const ImageGeom g = geom_of(c);
+  PCONV_CHECK(c.backend == Backend::Hip, "--bench needs --backend hip");
+  PCONV_CHECK(c.gpus >= 1 && c.gpus <= kMaxRanks && g.height >= c.gpus, "--bench: bad rank count");
+  if (!c.synthetic) validate_input_file(c.image, g);
+  void* mem = mmap(nullptr, sizeof(BenchShared), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+  PCONV_CHECK(mem != MAP_FAILED, "mmap bench state failed");
+  auto* sh = new (mem) BenchShared();
+  sh->st.arrived = 0;
+  sh->st.generation = 0;
+  sh->st.failed = 0;
+  void* im = mmap(nullptr, static_cast<size_t>(g.bytes()), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+  PCONV_CHECK(im != MAP_FAILED, "mmap bench image failed");
+  auto* image = static_cast<uint8_t*>(im);
+  bool ok = true;
+  std::string err;
+  if (c.gpus == 1) {
+    try {
+      bench_rank(c, sh, image, 0);
+    } catch (const std::exception& e) {
+      ok = false;
+      err = e.what();
+    }
+  } else {
+    std::fflush(stdout);
+    std::fflush(stderr);
+    std::vector<pid_t> kids;
+    for (int r = 0; r < c.gpus; ++r) {
+      const pid_t pid = fork();
+      PCONV_CHECK(pid >= 0, "fork failed");
+      if (pid == 0) {
+        int code = 0;
+        try {
+          bench_rank(c, sh, image, r);
+        } catch (const std::exception& e) {
+          std::fprintf(stderr, "%s\n", e.what());
+          if (!sh->st.failed.exchange(1)) std::snprintf(sh->st.error, sizeof(sh->st.error), "%s", e.what());
+          code = 1;
+        }
+        std::fflush(stdout);
+        std::fflush(stderr);
+        _exit(code);
+      }
+      kids.push_back(pid);
+    }
+    for (pid_t p : kids) {
+      int st = 0;
+      waitpid(p, &st, 0);
+      ok = ok && WIFEXITED(st) && WEXITSTATUS(st) == 0;
+    }
+    if (!ok) err = sh->st.error[0] ? sh->st.error : "a bench rank died";
+  }
+  if (!ok) {
+    munmap(im, static_cast<size_t>(g.bytes()));
+    munmap(mem, sizeof(BenchShared));
+    PCONV_FAIL("bench failed: " + err);
+  }
+  double sec = 0, lat = 0, pair = 0;
+  std::ostringstream per;
+  for (int r = 0; r < c.gpus; ++r) {
+    sec = std::max(sec, sh->sec[r]);
+    lat = std::max(lat, sh->lat_ms[r]);
+    pair = std::max(pair, sh->pair_ms[r]);
+    per << (r ? ", " : "") << sh->sec[r] / c.bench_steps * 1e3;
+  }
+  const int64_t mism = c.check ? compare_with_oracle(c, g, image) : -1;
+  const double px = static_cast<double>(c.width) * static_cast<double>(c.height) * c.reps;
+  const double value = px * c.bench_steps / sec / 1e6;
+  const bool head = c.width == 1920 && c.height == 2520 && c.channels == Channels::Rgb && c.reps == 40 &&
+                    c.filter == "gaussian";
+  std::ostringstream os;
+  os.setf(std::ios::fixed);
+  os.precision(4);
+  os << "{\"metric\": \"" << bench_metric(c) << "\", \"value\": " << value << ", \"unit\": \"Mpix/s\", \"n_gpus\": "
+     << c.gpus << ", \"steps\": " << c.bench_steps << ", \"warmup\": " << c.warmup
+     << ", \"ms_per_step\": " << sec / c.bench_steps * 1e3 << ", \"higher_is_better\": true, \"scaling\": \"strong\""
+     << ", \"vs_baseline\": ";
+  if (head)
+    os << value / kBaselineMpix;
+  else
+    os << "null";
+  os << ", \"vs_baseline_basis\": \"pipelined throughput vs reference single-run end-to-end (CUDA, GTX 970)\""
+     << ", \"dtype\": \"fp32-exact (packed 16-bit integer, bit-identical to the reference float32)\""
+     << ", \"data\": \"" << (c.synthetic ? "synthetic random bytes" : "file") << "\", \"config\": {\"model\": \"3x3 "
+     << c.filter << " convolution, " << c.width << "x" << c.height << " " << channels_name(c.channels) << ", "
+     << c.reps << " reps\", \"global_batch\": 1, \"seq_len\": " << c.height << ", \"parallelism\": \"rowband"
+     << c.gpus << "\", \"step\": \"H2D + reps + D2H per image (reference GPU_convolution scope)\", \"halo_mode\": \""
+     << (c.gpus > 1 ? "preload" : "none") << "\", \"images_in_flight\": " << c.slots
+     << ", \"stream_chunks\": " << c.stream_chunks << ", \"halo_depth\": " << sh->halo << ", \"fuse\": " << sh->fuse
+     << ", \"launches_per_step\": " << sh->launches << "}, \"latency_ms\": " << lat
+     << ", \"copy_floor\": {\"pair_ms\": " << pair << "}";
+  if (mism >= 0)
+    os << ", \"mismatches\": " << mism
+       << ", \"check\": \"newest image of every rank vs the CPU oracle (OpenMP), after the timed region\"";
+  os << ", \"runtime\": {\"stack\": \"native conv (no torch)\", \"hip_runtime_version\": " << sh->hip_version
+     << ", \"hip_runtime_path\": \"" << json_escape(sh->hip_path) << "\", \"rccl_version\": null}"
+     << ", \"per_rank_ms_per_step\": [" << per.str() << "]}";
+  munmap(im, static_cast<size_t>(g.bytes()));
+  munmap(mem, sizeof(BenchShared));
+  return os.str();
+}
+
 }  // namespace
+
+std::string run_bench(const CliConfig& c) { return run_bench_impl(c); }
 
 AppReport run_app(const CliConfig& c, JobCache* cache) {
   AppReport r;
@@ -735,6 +943,15 @@ int conv_main(int argc, char** argv) {
   if (!c.server.empty()) {
     try {
       return run_client(prog, args, c);
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "%s: %s\n", prog.c_str(), e.what());
+      return EXIT_FAILURE;
+    }
+  }
+  if (c.bench_steps > 0) {
+    try {
+      std::printf("%s\n", run_bench(c).c_str());
+      return EXIT_SUCCESS;
     } catch (const std::exception& e) {
       std::fprintf(stderr, "%s: %s\n", prog.c_str(), e.what());
       return EXIT_FAILURE;

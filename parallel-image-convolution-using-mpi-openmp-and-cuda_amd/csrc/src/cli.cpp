@@ -57,6 +57,10 @@ std::string help_text(const std::string& prog) {
          "  --server SOCKET           run the job on a resident `conv --serve SOCKET` (warm GPU context)\n"
          "  --copies {auto,sdma,kernel}  1-GPU host<->device copies: SDMA engines or CU kernels (auto:\n"
          "                            kernels in a one-shot process, SDMA in a resident server)\n"
+         "  --bench K                 serving bench: K timed images (H2D + reps + D2H each) per rank after\n"
+         "                            --warmup untimed ones; prints bench.py's JSON line (native stack)\n"
+         "  --slots S                 --bench: images in flight (default 3)\n"
+         "  --stream-chunks C         --bench: rows of each image streamed in C chunks (0 = off)\n"
          "\n"
          "       " + prog + " --serve SOCKET [--device D] [--idle-timeout S] [--max-engines N]\n"
          "                            resident service: initialise the GPU once, then run jobs sent by\n"
@@ -150,6 +154,12 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       else PCONV_FAIL("invalid --copies '" + v + "' (auto|sdma|kernel)");
     } else if (a == "--server") {
       c.server = next("--server");
+    } else if (a == "--bench") {
+      c.bench_steps = static_cast<int>(parse_int(next("--bench"), "--bench", 1, 1 << 24));
+    } else if (a == "--slots") {
+      c.slots = static_cast<int>(parse_int(next("--slots"), "--slots", 1, 8));
+    } else if (a == "--stream-chunks") {
+      c.stream_chunks = static_cast<int>(parse_int(next("--stream-chunks"), "--stream-chunks", 0, 4096));
     } else if (a == "--warmup") {
       c.warmup = static_cast<int>(parse_int(next("--warmup"), "--warmup", 0, 100));
     } else {

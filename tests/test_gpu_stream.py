@@ -90,3 +90,29 @@ def test_streamed_step_and_reps_zero(pconv_mod, rng):
     assert len(blur.engine.stream_plan(0, 0, h).chunks) == 0
     assert np.array_equal(blur.step(0).reshape(h, w, 3), img)
     assert np.array_equal(blur.step(7).reshape(h, w, 3), pconv_mod.numpy_convolve(img, 7))
+
+
+@pytest.mark.parametrize("gpus,extra", [(1, []), (1, ["--stream-chunks", "4"]), (2, ["--transport", "gloo-host"])])
+def test_native_bench_line(gpus, extra):
+    """`bench.py --native`: the same serving step in the `conv` binary (ROCm's
+    HIP runtime, no torch; fork launcher for N > 1, here two ranks sharing the
+    GPU), one JSON line with the bench contract's fields, oracle-checked."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--native", "--gpus", str(gpus), "--steps", "12",
+           "--warmup", "3"] + extra
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["metric"] == "Mpixels/sec (and wall-time) for 1920x2520 RGB, 40 reps at 1/2/4/8 MI355X"
+    assert d["n_gpus"] == gpus and d["steps"] == 12 and d["value"] > 0 and d["mismatches"] == 0
+    assert d["runtime"]["stack"].startswith("native") and "torch" not in d["runtime"]["hip_runtime_path"]
+    assert d["config"]["parallelism"] == f"rowband{gpus}" and len(d["per_rank_ms_per_step"]) == gpus
+    assert d["latency_ms"] > 0 and d["copy_floor"]["pair_ms"] > 0

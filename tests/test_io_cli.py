@@ -112,3 +112,16 @@ def test_python_module_cli(tmp_path, pconv_mod):
                        timeout=300, env=dict(os.environ, PYTHONPATH=ROOT))
     assert r.returncode == 0, r.stderr
     assert "Execution time:" in r.stdout
+
+
+def test_cli_bench_flags(tmp_path):
+    """`conv --bench K` (bench.py's serving step on the native stack) flags are
+    validated like every other option; --help documents them."""
+    r = _run(["a.raw", "64", "64", "4", "rgb", "--synthetic", "1", "--bench", "0"], tmp_path)
+    assert r.returncode == 1 and "invalid --bench" in r.stderr
+    r = _run(["a.raw", "64", "64", "4", "rgb", "--synthetic", "1", "--bench", "5", "--slots", "9"], tmp_path)
+    assert r.returncode == 1 and "invalid --slots" in r.stderr
+    r = _run(["a.raw", "64", "64", "4", "rgb", "--bench", "5", "--stream-chunks", "x"], tmp_path)
+    assert r.returncode == 1 and "invalid --stream-chunks" in r.stderr
+    r = _run(["--help"], tmp_path)
+    assert "--bench K" in r.stdout and "--stream-chunks" in r.stdout
