@@ -69,7 +69,10 @@ struct EngineOptions {
   // Row streaming within one image (schedule.hpp, plan_streamed): a serving
   // step's rows are uploaded in this many chunks and each level advances as
   // far as the rows on the device allow, so H2D, launches and D2H of ONE
-  // image overlap on three streams.  0 / 1: whole-image chain.
+  // image overlap on three streams.  0 / 1: whole-image chain.  Issued
+  // directly (BandPipeline's event-ordered mode): captured as one graph with
+  // fork/join branches it measured 1.4-4.3x slower per image
+  // (profiles/r04/stream_a/).
   int stream_chunks = 0;
 };
 
@@ -196,7 +199,6 @@ class BandEngine {
   hipStream_t cs_ = nullptr, ms_ = nullptr;
   Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_;
   Event ev_up_, ev_dn_;       // streamed images: chunk uploaded / chunk rows final
-  Stream cap_up_, cap_dn_;    // streamed step graphs: capture-only fork streams (never launched on)
   std::shared_ptr<HaloTransport> transport_;
   RunStats stats_;
   double wall_t0_ = 0;

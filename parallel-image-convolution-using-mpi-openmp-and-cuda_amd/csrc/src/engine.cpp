@@ -407,50 +407,13 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
 void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
   TraceRange tr("pconv.step_graph");
   PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
-  const StreamPlan sp = host_out ? stream_plan(reps, in_r0, in_r1) : StreamPlan{};
-  if (!sp.chunks.empty()) {
-    // Streamed image as ONE graph: uploads and downloads on two forked
-    // capture streams, launches on the compute stream, one edge per chunk
-    // between them; the graph runs on the compute stream.
-    const auto key = std::make_tuple(-reps - 1, cur_, host_in, in_r0, in_r1, host_out);
-    auto it = step_graphs_.find(key);
-    stats_ = RunStats{};
-    if (it == step_graphs_.end()) {
-      trim_graph_caches();
-      if (!cap_up_.get()) {
-        cap_up_ = Stream::create(0);
-        cap_dn_ = Stream::create(0);
-      }
-      const int c0 = cur_;
-      for (const auto& ch : sp.chunks)
-        for (size_t i = 0; i < ch.launches.size(); ++i)
-          prepare_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1, nullptr, 0),
-                          cs_, opt_.variant);
-      hipGraph_t g = nullptr;
-      PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
-      ev_ready_.record(cs_);
-      ev_ready_.wait_on(cap_up_.get());
-      ev_ready_.wait_on(cap_dn_.get());
-      enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, cap_up_.get(), cap_dn_.get());
-      ev_up_.record(cap_up_.get());
-      ev_up_.wait_on(cs_);
-      ev_dn_.record(cap_dn_.get());
-      ev_dn_.wait_on(cs_);
-      PCONV_HIP_CHECK(hipStreamEndCapture(cs_, &g));
-      StepGraph sg;
-      PCONV_HIP_CHECK(hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0));
-      PCONV_HIP_CHECK(hipGraphDestroy(g));
-      sg.end_cur = cur_;
-      sg.launches = stats_.launches;
-      it = step_graphs_.emplace(key, sg).first;
-    } else {
-      cur_ = it->second.end_cur;
-      stats_.launches = it->second.launches;
-    }
-    PCONV_HIP_CHECK(hipGraphLaunch(it->second.exec, cs_));
-    halo_valid_ = false;
-    return;
-  }
+  // The whole input is uploaded by every step, so the step always starts in
+  // frame 0: one cached graph per (reps, buffers) instead of one per start
+  // frame (an odd number of launches per image flips the frames, and a step
+  // whose start frame was not seen before paid a capture + instantiate
+  // inside the first timed images).  All ranks follow the same rule, so
+  // neighbours still hold the same time level in the frame of equal parity.
+  cur_ = 0;
   halo_valid_ = input_preloaded(in_r0, in_r1);
   std::vector<Phase> ph = plan(reps);
   bool exchanges = false;

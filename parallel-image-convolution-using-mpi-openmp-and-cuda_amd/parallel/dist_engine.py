@@ -112,7 +112,11 @@ class DistributedBlur:
         # With RCCL, an exchange image is ONE captured graph (upload, ncclSend/
         # ncclRecv of the ghost zone, launches, download): one host call per
         # image instead of the transport's group calls + launches + copies.
-        if self.slot_exchange or (free if step_graphs is None else bool(step_graphs)):
+        # Row-streamed images are issued directly on shared H2D / compute / D2H
+        # streams (the event-ordered pipeline): captured as one graph with
+        # fork/join branches they measured 1.4-4.3x slower (profiles/r04/stream_a/).
+        streamed = int(stream_chunks) > 1 and free and not self.slot_exchange
+        if not streamed and (self.slot_exchange or (free if step_graphs is None else bool(step_graphs))):
             del self.pipe
             # slot_comm (exchange images): each slot also gets a communication
             # stream, so an exchange phase runs beside the interior launch and

@@ -2,11 +2,9 @@
 
 Each image's rows are uploaded in chunks and every level advances behind
 them (schedule.hpp plan_streamed); H2D, launches and D2H of one image run on
-three streams.  Both pipeline forms are checked bit-exact against the NumPy
-oracle (tests/test_stream_plan.py checks the plans themselves on the CPU):
-  * graph: every image ONE captured hipGraph (uploads / downloads on forked
-    capture streams), slots on their own streams;
-  * direct: shared H2D / compute / D2H streams, one event pair per chunk.
+three streams (shared H2D / compute / D2H streams, one event pair per chunk;
+the pipeline's event-ordered mode), checked bit-exact against the NumPy
+oracle (tests/test_stream_plan.py checks the plans themselves on the CPU).
 Output buffers are pre-filled with junk so a row never downloaded shows up.
 """
 import numpy as np
@@ -17,11 +15,12 @@ pytestmark = pytest.mark.gpu
 CH = {"grey": 1, "rgb": 3, "rgba": 4}
 
 
-def _blur(w, h, ch, filt, reps, chunks, graph, slots=2, **kw):
+def _blur(w, h, ch, filt, reps, chunks, slots=2, **kw):
     from pconv.parallel.dist_engine import DistributedBlur
 
-    return DistributedBlur(w, h, ch, filt, reps, device=0, slots=slots, stream_chunks=chunks,
-                           step_graphs=graph, graph_capture=graph, **kw)
+    b = DistributedBlur(w, h, ch, filt, reps, device=0, slots=slots, stream_chunks=chunks, **kw)
+    assert not b.pipe.graphs  # streamed images are issued directly (event-ordered streams)
+    return b
 
 
 def _run_images(pconv_mod, rng, blur, w, h, ch, filt, reps, rounds=2):
@@ -42,40 +41,37 @@ def _run_images(pconv_mod, rng, blur, w, h, ch, filt, reps, rounds=2):
             assert np.array_equal(got, ref[b.y0:b.y0 + b.rows]), (rnd, k)
 
 
-@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("slots", [1, 3])
 @pytest.mark.parametrize("chunks", [2, 3, 5, 8])
 @pytest.mark.parametrize("w,h,ch,reps", [(67, 45, "rgb", 9), (64, 133, "grey", 40), (50, 71, "rgba", 13),
                                          (1920, 252, "rgb", 40)])
-def test_streamed_pipeline_bit_exact(pconv_mod, rng, graph, chunks, w, h, ch, reps):
-    blur = _blur(w, h, ch, "gaussian", reps, chunks, graph)
-    assert blur.pipe.graphs == graph
+def test_streamed_pipeline_bit_exact(pconv_mod, rng, slots, chunks, w, h, ch, reps):
+    blur = _blur(w, h, ch, "gaussian", reps, chunks, slots=slots)
     sp = blur.engine.stream_plan(reps, 0, h)
     assert len(sp.chunks) == min(chunks, h) and sp.levels == len(blur.plan(reps))
     _run_images(pconv_mod, rng, blur, w, h, ch, "gaussian", reps)
     assert blur.stats.launches >= sp.levels
 
 
-@pytest.mark.parametrize("graph", [True, False])
 @pytest.mark.parametrize("filt", ["box", "edge"])
-def test_streamed_float_filters(pconv_mod, rng, graph, filt):
-    _run_images(pconv_mod, rng, _blur(59, 83, "rgb", filt, 11, 4, graph), 59, 83, "rgb", filt, 11)
+def test_streamed_float_filters(pconv_mod, rng, filt):
+    _run_images(pconv_mod, rng, _blur(59, 83, "rgb", filt, 11, 4), 59, 83, "rgb", filt, 11)
 
 
-@pytest.mark.parametrize("graph", [True, False])
-def test_streamed_reps_exceed_chunks(pconv_mod, rng, graph):
+@pytest.mark.parametrize("fuse", [8, 16])
+def test_streamed_reps_exceed_chunks(pconv_mod, rng, fuse):
     """More repetitions than rows per chunk (the last level lags several
     chunks behind the uploads), an odd height and a last launch of 1 step."""
-    _run_images(pconv_mod, rng, _blur(33, 37, "grey", "gaussian", 41, 9, graph), 33, 37, "grey", "gaussian", 41)
+    blur = _blur(33, 37, "grey", "gaussian", 41, 9, fuse=fuse, halo=fuse)
+    _run_images(pconv_mod, rng, blur, 33, 37, "grey", "gaussian", 41)
 
 
-@pytest.mark.parametrize("graph", [True, False])
 @pytest.mark.parametrize("world,rank", [(2, 0), (3, 1), (4, 3), (8, 5)])
-def test_streamed_preloaded_bands(pconv_mod, rng, graph, world, rank):
+def test_streamed_preloaded_bands(pconv_mod, rng, world, rank):
     """A rank's band with pre-loaded ghost rows (the N>1 headline) streamed:
     the ghost rows travel with the first / last chunks."""
     w, h, reps = 61, 400, 40
-    blur = _blur(w, h, "rgb", "gaussian", reps, 3, graph, rank=rank, world=world, preload_halo=True,
-                 transport="none")
+    blur = _blur(w, h, "rgb", "gaussian", reps, 3, rank=rank, world=world, preload_halo=True, transport="none")
     _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps)
 
 
@@ -83,7 +79,7 @@ def test_streamed_step_and_reps_zero(pconv_mod, rng):
     """blur.step (one image alone) and reps = 0 (nothing to stream: the
     whole-image path) through a streaming pipeline."""
     w, h = 40, 30
-    blur = _blur(w, h, "rgb", "gaussian", 7, 4, True)
+    blur = _blur(w, h, "rgb", "gaussian", 7, 4)
     img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
     blur.load_image(img)
     assert np.array_equal(blur.step(7).reshape(h, w, 3), pconv_mod.numpy_convolve(img, 7))
