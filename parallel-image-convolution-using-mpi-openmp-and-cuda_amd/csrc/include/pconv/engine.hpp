@@ -198,7 +198,7 @@ class BandEngine {
   Stream own_cs_, own_ms_;
   hipStream_t cs_ = nullptr, ms_ = nullptr;
   Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_;
-  Event ev_up_, ev_dn_;       // streamed images: chunk uploaded / chunk rows final
+  std::vector<Event> up_evs_, dn_evs_;  // streamed images: per chunk, uploaded / rows final
   std::shared_ptr<HaloTransport> transport_;
   RunStats stats_;
   double wall_t0_ = 0;

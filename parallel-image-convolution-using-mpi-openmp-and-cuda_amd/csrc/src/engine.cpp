@@ -62,8 +62,6 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
   ev_ready_ = Event::create();
   ev_halo_ = Event::create();
   ev_sync_ = Event::create();
-  ev_up_ = Event::create();
-  ev_dn_ = Event::create();
   ev_t0_ = Event::create(true);
   ev_t1_ = Event::create(true);
   PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
@@ -368,38 +366,46 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
   const int c0 = cur_;
   uint8_t* in_frame = frame_at(c0);
   const uint8_t* out_frame = frame_at(c0 + sp.levels);
-  bool joined = true;  // `down` already ordered after every launch issued so far
-  for (const auto& ch : sp.chunks) {
-    if (ch.up_hi > ch.up_lo) {
-      PCONV_HIP_CHECK(hipMemcpy2DAsync(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, rb,
-                                       ch.up_hi - ch.up_lo, hipMemcpyHostToDevice, up));
-      if (up != cs_) {
-        ev_up_.record(up);
-        ev_up_.wait_on(cs_);
-      }
-    }
+  const size_t nc = sp.chunks.size();
+  while (up_evs_.size() < nc) up_evs_.push_back(Event::create());
+  while (dn_evs_.size() < nc + 1) dn_evs_.push_back(Event::create());
+  // Host issue order: every upload first (the H2D stream then runs them back
+  // to back instead of waiting for the host to issue the next one behind the
+  // previous chunk's launches), then each chunk's launches behind its
+  // upload's event, then each download behind its chunk's event.  One event
+  // per chunk and direction (no re-recorded event is waited on).
+  for (size_t c = 0; c < nc; ++c) {
+    const StreamChunk& ch = sp.chunks[c];
+    PCONV_HIP_CHECK(hipMemcpy2DAsync(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, rb,
+                                     ch.up_hi - ch.up_lo, hipMemcpyHostToDevice, up));
+    if (up != cs_) up_evs_[c].record(up);
+  }
+  bool pending = false;  // launches not yet covered by a download-side event
+  for (size_t c = 0; c < nc; ++c) {
+    const StreamChunk& ch = sp.chunks[c];
+    if (up != cs_) up_evs_[c].wait_on(cs_);
     for (size_t i = 0; i < ch.launches.size(); ++i) {
       launch_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1, nullptr, 0),
                      cs_, opt_.variant);
       ++stats_.launches;
-      joined = false;
+      pending = true;
     }
-    if (ch.down_hi > ch.down_lo && host_out) {
-      if (down != cs_) {
-        ev_dn_.record(cs_);
-        ev_dn_.wait_on(down);
-      }
-      joined = true;
-      PCONV_HIP_CHECK(hipMemcpy2DAsync(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, rb,
-                                       ch.down_hi - ch.down_lo, hipMemcpyDeviceToHost, down));
+    if (ch.down_hi > ch.down_lo && host_out && down != cs_) {
+      dn_evs_[c].record(cs_);
+      pending = false;
     }
   }
-  if (!joined && down != cs_) {
-    // Launches after the last download: `down` finishing must still mean the
-    // whole image is done (the next image of these frames waits on `down`).
-    ev_dn_.record(cs_);
-    ev_dn_.wait_on(down);
+  // `down` finishing must mean the whole image is done (the next image of
+  // these frames waits on it), also when launches follow the last download.
+  if (pending && down != cs_) dn_evs_[nc].record(cs_);
+  for (size_t c = 0; c < nc; ++c) {
+    const StreamChunk& ch = sp.chunks[c];
+    if (!(ch.down_hi > ch.down_lo && host_out)) continue;
+    if (down != cs_) dn_evs_[c].wait_on(down);
+    PCONV_HIP_CHECK(hipMemcpy2DAsync(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, rb,
+                                     ch.down_hi - ch.down_lo, hipMemcpyDeviceToHost, down));
   }
+  if (pending && down != cs_) dn_evs_[nc].wait_on(down);
   cur_ = (c0 + sp.levels) & 1;
   halo_valid_ = false;
 }
