@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <string>
 #include <utility>
+#include <vector>
 
 #include "pconv/common.hpp"
 
@@ -93,6 +94,9 @@ class Stream {
  public:
   Stream() = default;
   static Stream create(int priority = 0);
+  // A stream on its own hardware queue restricted to the CUs set in `mask`
+  // (bit i of word w = CU 32*w + i); all-ones = every CU.
+  static Stream create_cu_masked(const std::vector<uint32_t>& mask);
   ~Stream();
   Stream(Stream&& o) noexcept : s_(o.s_) { o.s_ = nullptr; }
   Stream& operator=(Stream&& o) noexcept {

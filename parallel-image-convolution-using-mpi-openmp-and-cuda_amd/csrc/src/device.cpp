@@ -152,6 +152,12 @@ Stream Stream::create(int priority) {
   return s;
 }
 
+Stream Stream::create_cu_masked(const std::vector<uint32_t>& mask) {
+  Stream s;
+  PCONV_HIP_CHECK(hipExtStreamCreateWithCUMask(&s.s_, static_cast<uint32_t>(mask.size()), mask.data()));
+  return s;
+}
+
 Stream::~Stream() {
   if (s_) (void)hipStreamDestroy(s_);
 }

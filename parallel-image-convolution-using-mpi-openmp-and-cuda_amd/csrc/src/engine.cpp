@@ -513,8 +513,23 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
     // no split launches.  With it, each slot's exchanges run on the slot's
     // own communication stream beside the interior launch.
     o.overlap = slot_comm && opt.overlap;
+    // PCONV_SLOT_STREAMS (experiments on the hardware-queue mapping of the
+    // slot streams, docs/PERFORMANCE.md §2): "cumask" = every slot stream on
+    // its own CU-masked queue (all CUs), "cusplit" = the CUs split evenly
+    // between the slot streams, "prio" = alternate high / normal priority.
+    const char* sm = std::getenv("PCONV_SLOT_STREAMS");
+    const std::string mode = sm ? sm : "";
     for (int i = 0; i < slots; ++i) {
-      computes_.push_back(Stream::create(0));
+      if (mode == "cumask" || mode == "cusplit") {
+        int n = 0, dev = opt.device;
+        PCONV_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+        std::vector<uint32_t> mask(static_cast<size_t>((n + 31) / 32), 0u);
+        for (int cu = 0; cu < n; ++cu)
+          if (mode == "cumask" || cu % slots == i) mask[static_cast<size_t>(cu / 32)] |= 1u << (cu % 32);
+        computes_.push_back(Stream::create_cu_masked(mask));
+      } else {
+        computes_.push_back(Stream::create(mode == "prio" && (i & 1) ? -1 : 0));
+      }
       o.compute_stream = computes_.back().get();
       if (slot_comm) {
         slot_comms_.push_back(Stream::create(-1));
