@@ -9,9 +9,10 @@
 // rows with device copies — no communication library kernel, no host
 // staging, nothing on the host path after set-up.
 //
-// Three separate dispatches per exchange, so the command processor's cache
-// release / acquire at every kernel boundary makes each side's rows visible
-// to the other on every XCD (no reliance on in-kernel cache maintenance).
+// One dispatch per exchange by default (k_ipc_exchange: the three steps in
+// one workgroup; the rows a neighbour reads always come from an earlier
+// kernel of its stream, whose end-of-kernel release wrote them back on every
+// XCD); PCONV_IPC_KERNELS=3 splits it into three dispatches.
 // Ordering across processes is device-side, through flag words in a shared
 // host-memory segment (POSIX shm, registered with hipHostRegister so every
 // rank's GPU reads and writes it with system-scope atomics).  Per (rank,
@@ -65,6 +66,11 @@ void launch_ipc_ack_wait(IpcFlags* flags, int me, int up, int down, uint64_t tim
 // source: no neighbour on that side); a no-op once this rank's wait timed out.
 void launch_ipc_pull(const IpcFlags* flags, int me, uint8_t* dst_up, const uint8_t* src_up, uint8_t* dst_down,
                      const uint8_t* src_down, int64_t bytes, hipStream_t s);
+// Signal + wait, pull and ack + wait as ONE single-workgroup dispatch (the
+// default; PCONV_IPC_KERNELS=3 issues the three kernels above instead).
+void launch_ipc_exchange(IpcFlags* flags, int me, int up, int down, uint64_t timeout_ticks, uint8_t* dst_up,
+                         const uint8_t* src_up, uint8_t* dst_down, const uint8_t* src_down, int64_t bytes,
+                         hipStream_t s);
 
 class IpcHaloTransport : public HaloTransport {
  public:
@@ -105,6 +111,7 @@ class IpcHaloTransport : public HaloTransport {
   FrameLayout lay_up_, lay_down_;
   bool connected_ = false;
   bool own_ = false;  // a neighbour is this engine itself (one-process emulation)
+  bool split_kernels_ = false;  // PCONV_IPC_KERNELS=3: signal / pull / ack as three dispatches
   uint8_t* own_base_[2] = {nullptr, nullptr};  // this engine's frames (the destructor never touches the engine)
   int64_t enqueued_ = 0;
 };

@@ -73,7 +73,64 @@ __global__ __launch_bounds__(256) void k_ipc_pull(const IpcFlags* f, int me, uin
   }
 }
 
+// The whole exchange as ONE dispatch (one workgroup): thread 0 publishes and
+// waits for the neighbours' rows, the workgroup pulls them, thread 0
+// publishes "copied" and waits for the neighbours' copies.  The rows a
+// neighbour pulls were produced by an EARLIER kernel of its stream (the
+// command processor's end-of-kernel release wrote them back on every XCD);
+// this kernel's system-scope acquire (thread 0, before the barrier)
+// invalidates this CU's caches before any thread loads them.  Three
+// dispatches (signal / pull / ack) cost ~14 us more per exchange on the
+// 8-way proxy (profiles/r04/slots_b/).
+__global__ __launch_bounds__(1024) void k_ipc_exchange(IpcFlags* f, int me, int up, int down, uint64_t timeout,
+                                                       uint4* __restrict__ dst_up, const uint4* __restrict__ src_up,
+                                                       uint4* __restrict__ dst_down,
+                                                       const uint4* __restrict__ src_down, int64_t n16) {
+  __shared__ int ok_s;
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
+    const uint32_t n = load_sys(&f[me].count) + 1;
+    store_sys(&f[me].count, n);
+    store_sys(&f[me].level, n);
+    bool ok = true;
+    if (up >= 0) ok = wait_ge(&f[up].level, n, t0, timeout);
+    if (ok && down >= 0) ok = wait_ge(&f[down].level, n, t0, timeout);
+    if (!ok) store_sys(&f[me].err, 1u);
+    ok_s = ok;
+  }
+  __syncthreads();
+  if (!ok_s) return;  // a neighbour may be gone: do not touch its frames
+  for (int64_t i = threadIdx.x; i < n16; i += blockDim.x) {
+    if (src_up) dst_up[i] = src_up[i];
+    if (src_down) dst_down[i] = src_down[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
+    const uint32_t n = load_sys(&f[me].count);
+    store_sys(&f[me].ack, n);
+    bool ok = true;
+    if (up >= 0) ok = wait_ge(&f[up].ack, n, t0, timeout);
+    if (ok && down >= 0) ok = wait_ge(&f[down].ack, n, t0, timeout);
+    if (!ok) store_sys(&f[me].err, 2u);
+  }
+}
+
 }  // namespace
+
+void launch_ipc_exchange(IpcFlags* flags, int me, int up, int down, uint64_t timeout_ticks, uint8_t* dst_up,
+                         const uint8_t* src_up, uint8_t* dst_down, const uint8_t* src_down, int64_t bytes,
+                         hipStream_t s) {
+  PCONV_CHECK(bytes % 16 == 0, "ipc exchange: rows must span whole 16-byte granules");
+  for (const void* p : {static_cast<const void*>(dst_up), static_cast<const void*>(src_up),
+                        static_cast<const void*>(dst_down), static_cast<const void*>(src_down)})
+    PCONV_CHECK(reinterpret_cast<uintptr_t>(p) % 16 == 0, "ipc exchange: unaligned row pointer");
+  k_ipc_exchange<<<dim3(1), dim3(1024), 0, s>>>(flags, me, up, down, timeout_ticks, reinterpret_cast<uint4*>(dst_up),
+                                                reinterpret_cast<const uint4*>(src_up),
+                                                reinterpret_cast<uint4*>(dst_down),
+                                                reinterpret_cast<const uint4*>(src_down), bytes / 16);
+  PCONV_HIP_CHECK(hipGetLastError());
+}
 
 void launch_ipc_pull(const IpcFlags* flags, int me, uint8_t* dst_up, const uint8_t* src_up, uint8_t* dst_down,
                      const uint8_t* src_down, int64_t bytes, hipStream_t s) {

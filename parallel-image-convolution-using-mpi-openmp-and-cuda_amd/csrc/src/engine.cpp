@@ -513,12 +513,17 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
     // no split launches.  With it, each slot's exchanges run on the slot's
     // own communication stream beside the interior launch.
     o.overlap = slot_comm && opt.overlap;
-    // PCONV_SLOT_STREAMS (experiments on the hardware-queue mapping of the
-    // slot streams, docs/PERFORMANCE.md §2): "cumask" = every slot stream on
-    // its own CU-masked queue (all CUs), "cusplit" = the CUs split evenly
-    // between the slot streams, "prio" = alternate high / normal priority.
+    // Slot streams on dedicated hardware queues: a stream created with a CU
+    // mask (all CUs) gets its own HSA queue instead of one from the
+    // runtime's round-robin pool.  From the pool, 4 slot streams landed on
+    // queues of which two ran every stencil launch ~5x longer (p50 47 vs
+    // 9.6 us; the 8-way proxy step 0.106 vs 0.055 ms at 3 slots); with
+    // CU-masked queues 4 slots run at 0.053 ms (docs/PERFORMANCE.md §2,
+    // profiles/r04/slots_b/).  PCONV_SLOT_STREAMS: "cumask" (default),
+    // "plain" (the pool), "cusplit" (CUs split evenly between the slots),
+    // "prio" (pool, alternating high / normal priority).
     const char* sm = std::getenv("PCONV_SLOT_STREAMS");
-    const std::string mode = sm ? sm : "";
+    const std::string mode = sm ? sm : "cumask";
     for (int i = 0; i < slots; ++i) {
       if (mode == "cumask" || mode == "cusplit") {
         int n = 0, dev = opt.device;

@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 
 #include "pconv/trace.hpp"
@@ -60,6 +61,8 @@ IpcHaloTransport::IpcHaloTransport(BandEngine& e, const std::string& segment, in
   int khz = 0;
   PCONV_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e.options().device));
   timeout_ticks_ = static_cast<uint64_t>(timeout_s * static_cast<double>(khz > 0 ? khz : 100000) * 1000.0);
+  const char* k = std::getenv("PCONV_IPC_KERNELS");
+  split_kernels_ = k && k[0] == '3';
   handles_.resize(2 * sizeof(hipIpcMemHandle_t));
   for (int i = 0; i < 2; ++i) {
     hipIpcMemHandle_t h;
@@ -128,15 +131,21 @@ void IpcHaloTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream
   const int par = e.cur();  // neighbours hold the same time level in the frame of the same parity
   const size_t n = static_cast<size_t>(depth * L.pitch);
   uint8_t* mine = e.frame_base(par);
-  launch_ipc_signal_wait(dflags_, me, up, down, timeout_ticks_, stream);
   // up: its last `depth` owned rows -> my ghost rows [-depth, 0); down: its
   // first `depth` owned rows -> my ghost rows [rows, rows + depth).  Whole
   // pitch-aligned rows (pads included: zero in every frame).
   const uint8_t* src_up = up >= 0 ? peer_up_[par] + lay_up_.offset(lay_up_.rows - depth) - kPadLeft : nullptr;
   const uint8_t* src_down = down >= 0 ? peer_down_[par] + lay_down_.offset(0) - kPadLeft : nullptr;
-  launch_ipc_pull(dflags_, me, mine + L.offset(-depth) - kPadLeft, src_up, mine + L.offset(b.rows) - kPadLeft,
-                  src_down, static_cast<int64_t>(n), stream);
-  launch_ipc_ack_wait(dflags_, me, up, down, timeout_ticks_, stream);
+  uint8_t* dst_up = mine + L.offset(-depth) - kPadLeft;
+  uint8_t* dst_down = mine + L.offset(b.rows) - kPadLeft;
+  if (split_kernels_) {
+    launch_ipc_signal_wait(dflags_, me, up, down, timeout_ticks_, stream);
+    launch_ipc_pull(dflags_, me, dst_up, src_up, dst_down, src_down, static_cast<int64_t>(n), stream);
+    launch_ipc_ack_wait(dflags_, me, up, down, timeout_ticks_, stream);
+  } else {
+    launch_ipc_exchange(dflags_, me, up, down, timeout_ticks_, dst_up, src_up, dst_down, src_down,
+                        static_cast<int64_t>(n), stream);
+  }
   ++enqueued_;
 }
 
