@@ -109,6 +109,9 @@ class BandEngine {
   // Base of frame `which`'s allocation (hipIpcGetMemHandle needs it).
   uint8_t* frame_base(int which) const { return frame_[which & 1].data(); }
   int cur() const { return cur_; }
+  // Start frame of the next step (a step that uploads its whole input may
+  // start in either frame).
+  void set_cur(int c) { cur_ = c & 1; }
 
   // Copy frame-local rows [r_begin, r_end) from host (pointer at row r_begin).
   // Rows in the ghost zone are accepted (pre-loaded halos).  Async on the
@@ -278,6 +281,10 @@ class BandPipeline {
   bool step_graphs_ = true;
   std::vector<std::unique_ptr<BandEngine>> slots_;
   std::vector<Event> ev_up_, ev_done_, ev_free_, ev_halo_;
+  // step-graph mode with stream_chunks > 1: images submitted while nothing is
+  // in flight (after construction / drain) are row-streamed (head streaming)
+  bool idle_ = true;
+  Event ev_head_, h2d_wait_;
   std::vector<bool> used_;
   int64_t count_ = 0;
   std::vector<Event> trace_ev_;  // 4 per traced image

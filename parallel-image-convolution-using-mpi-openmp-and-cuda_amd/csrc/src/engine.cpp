@@ -544,6 +544,13 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
       }
       slots_.push_back(std::make_unique<BandEngine>(geom, band, filter, o));
     }
+    if (step_graphs && opt.stream_chunks > 1) {
+      // head streaming: copy streams for images submitted to an idle pipeline
+      h2d_ = Stream::create(0);
+      d2h_ = Stream::create(0);
+      ev_head_ = Event::create();
+      h2d_wait_ = Event::create();
+    }
     used_.assign(slots, false);
     return;
   }
@@ -629,7 +636,30 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   }
   if (graphs_) {
     PCONV_CHECK(trace_ev_.empty(), "pipeline trace needs directly issued images (graph capture off)");
+    if (idle_ && h2d_.get()) {
+      // Head streaming: nothing is in flight, so this image's rows stream
+      // (chunked H2D ‖ launches ‖ D2H of finished rows, schedule.hpp
+      // plan_streamed) instead of waiting for its whole upload and its
+      // whole loop before the first byte comes back — the head of a burst
+      // and every single image (latency).  Images behind it run as step
+      // graphs; the slot's stream waits for the streamed image's last
+      // download before its next graph touches these frames.
+      const StreamPlan sp = e.stream_plan(reps, in_r0, in_r1);
+      if (!sp.chunks.empty()) {
+        e.set_cur(0);  // like process_graph: the whole input is uploaded, start in frame 0
+        h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
+        h2d_wait_.wait_on(h2d_.get());
+        e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, h2d_.get(), d2h_.get());
+        ev_head_.record(d2h_.get());
+        ev_head_.wait_on(e.compute_stream());
+        idle_ = false;
+        used_[k] = true;
+        ++count_;
+        return;
+      }
+    }
     e.process_graph(host_in, in_r0, in_r1, host_out, reps);
+    idle_ = false;
     used_[k] = true;
     ++count_;
     return;
@@ -709,6 +739,7 @@ void BandPipeline::drain() {
   if (h2d_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(h2d_.get()));
   for (auto& s : slots_) s->synchronize();
   if (d2h_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(d2h_.get()));
+  idle_ = true;
 }
 
 // --------------------------------------------------------------- LocalCluster

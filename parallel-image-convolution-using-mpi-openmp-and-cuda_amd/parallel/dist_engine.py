@@ -112,10 +112,14 @@ class DistributedBlur:
         # With RCCL, an exchange image is ONE captured graph (upload, ncclSend/
         # ncclRecv of the ghost zone, launches, download): one host call per
         # image instead of the transport's group calls + launches + copies.
-        # Row-streamed images are issued directly on shared H2D / compute / D2H
-        # streams (the event-ordered pipeline): captured as one graph with
-        # fork/join branches they measured 1.4-4.3x slower (profiles/r04/stream_a/).
-        streamed = int(stream_chunks) > 1 and free and not self.slot_exchange
+        # stream_chunks > 1 with step_graphs=False: EVERY image row-streamed,
+        # issued directly on shared H2D / compute / D2H streams (the
+        # event-ordered pipeline; captured as one graph with fork/join
+        # branches a streamed image measured 1.4-4.3x slower,
+        # profiles/r04/stream_a/).  Otherwise (step graphs): only an image
+        # submitted to an idle pipeline is streamed — the head of a burst,
+        # every single image — and the rest run as one graph each.
+        streamed = int(stream_chunks) > 1 and free and not self.slot_exchange and step_graphs is False
         if not streamed and (self.slot_exchange or (free if step_graphs is None else bool(step_graphs))):
             del self.pipe
             # slot_comm (exchange images): each slot also gets a communication

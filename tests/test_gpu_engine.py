@@ -266,9 +266,10 @@ def test_step_graph_cache_bounded_across_host_buffers(pconv_mod, rng):
     assert eng.cached_graphs - eng.cached_step_graphs == loop_graphs
 
 
+@pytest.mark.parametrize("direct", [True, False])
 @pytest.mark.parametrize("slots,reps,world,rank", [(1, 9, 1, 0), (2, 9, 1, 0), (3, 13, 1, 0), (2, 12, 8, 3),
                                                    (3, 7, 3, 1)])
-def test_pipeline_streamed_rings(pconv_mod, rng, slots, reps, world, rank):
+def test_pipeline_streamed_rings(pconv_mod, rng, direct, slots, reps, world, rank):
     """Row-streamed images (stream_chunks=4): three rings of images over the
     same slot inputs with no host synchronisation in between.  A slot reused
     before its previous image's last download finished would have its result
@@ -279,7 +280,8 @@ def test_pipeline_streamed_rings(pconv_mod, rng, slots, reps, world, rank):
 
     w, h = 83, 120
     blur = DistributedBlur(w, h, "rgb", "gaussian", reps, rank=rank, world=world, device=0, slots=slots,
-                           preload_halo=True, transport="none", stream_chunks=4)
+                           preload_halo=True, transport="none", stream_chunks=4,
+                           step_graphs=False if direct else None)  # every image / the head image streamed
     b = blur.band
     imgs = [rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for _ in range(slots)]
     for k, img in enumerate(imgs):

@@ -15,11 +15,15 @@ pytestmark = pytest.mark.gpu
 CH = {"grey": 1, "rgb": 3, "rgba": 4}
 
 
-def _blur(w, h, ch, filt, reps, chunks, slots=2, **kw):
+def _blur(w, h, ch, filt, reps, chunks, slots=2, mode="direct", **kw):
+    """mode "direct": every image streamed on shared event-ordered streams;
+    "head": step-graph pipeline that streams only images submitted while it
+    is idle (the first of every burst here) and runs the others as graphs."""
     from pconv.parallel.dist_engine import DistributedBlur
 
-    b = DistributedBlur(w, h, ch, filt, reps, device=0, slots=slots, stream_chunks=chunks, **kw)
-    assert not b.pipe.graphs  # streamed images are issued directly (event-ordered streams)
+    b = DistributedBlur(w, h, ch, filt, reps, device=0, slots=slots, stream_chunks=chunks,
+                        step_graphs=None if mode == "head" else False, **kw)
+    assert b.pipe.graphs == (mode == "head")
     return b
 
 
@@ -41,21 +45,23 @@ def _run_images(pconv_mod, rng, blur, w, h, ch, filt, reps, rounds=2):
             assert np.array_equal(got, ref[b.y0:b.y0 + b.rows]), (rnd, k)
 
 
+@pytest.mark.parametrize("mode", ["direct", "head"])
 @pytest.mark.parametrize("slots", [1, 3])
 @pytest.mark.parametrize("chunks", [2, 3, 5, 8])
 @pytest.mark.parametrize("w,h,ch,reps", [(67, 45, "rgb", 9), (64, 133, "grey", 40), (50, 71, "rgba", 13),
                                          (1920, 252, "rgb", 40)])
-def test_streamed_pipeline_bit_exact(pconv_mod, rng, slots, chunks, w, h, ch, reps):
-    blur = _blur(w, h, ch, "gaussian", reps, chunks, slots=slots)
+def test_streamed_pipeline_bit_exact(pconv_mod, rng, mode, slots, chunks, w, h, ch, reps):
+    blur = _blur(w, h, ch, "gaussian", reps, chunks, slots=slots, mode=mode)
     sp = blur.engine.stream_plan(reps, 0, h)
     assert len(sp.chunks) == min(chunks, h) and sp.levels == len(blur.plan(reps))
     _run_images(pconv_mod, rng, blur, w, h, ch, "gaussian", reps)
     assert blur.stats.launches >= sp.levels
 
 
+@pytest.mark.parametrize("mode", ["direct", "head"])
 @pytest.mark.parametrize("filt", ["box", "edge"])
-def test_streamed_float_filters(pconv_mod, rng, filt):
-    _run_images(pconv_mod, rng, _blur(59, 83, "rgb", filt, 11, 4), 59, 83, "rgb", filt, 11)
+def test_streamed_float_filters(pconv_mod, rng, mode, filt):
+    _run_images(pconv_mod, rng, _blur(59, 83, "rgb", filt, 11, 4, mode=mode), 59, 83, "rgb", filt, 11)
 
 
 @pytest.mark.parametrize("fuse", [8, 16])
@@ -66,20 +72,23 @@ def test_streamed_reps_exceed_chunks(pconv_mod, rng, fuse):
     _run_images(pconv_mod, rng, blur, 33, 37, "grey", "gaussian", 41)
 
 
+@pytest.mark.parametrize("mode", ["direct", "head"])
 @pytest.mark.parametrize("world,rank", [(2, 0), (3, 1), (4, 3), (8, 5)])
-def test_streamed_preloaded_bands(pconv_mod, rng, world, rank):
+def test_streamed_preloaded_bands(pconv_mod, rng, mode, world, rank):
     """A rank's band with pre-loaded ghost rows (the N>1 headline) streamed:
     the ghost rows travel with the first / last chunks."""
     w, h, reps = 61, 400, 40
-    blur = _blur(w, h, "rgb", "gaussian", reps, 3, rank=rank, world=world, preload_halo=True, transport="none")
+    blur = _blur(w, h, "rgb", "gaussian", reps, 3, rank=rank, world=world, preload_halo=True, transport="none",
+                 mode=mode)
     _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps)
 
 
-def test_streamed_step_and_reps_zero(pconv_mod, rng):
-    """blur.step (one image alone) and reps = 0 (nothing to stream: the
-    whole-image path) through a streaming pipeline."""
+@pytest.mark.parametrize("mode", ["direct", "head"])
+def test_streamed_step_and_reps_zero(pconv_mod, rng, mode):
+    """blur.step (one image alone: streamed in both modes) and reps = 0
+    (nothing to stream: the whole-image path) through a streaming pipeline."""
     w, h = 40, 30
-    blur = _blur(w, h, "rgb", "gaussian", 7, 4)
+    blur = _blur(w, h, "rgb", "gaussian", 7, 4, mode=mode)
     img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
     blur.load_image(img)
     assert np.array_equal(blur.step(7).reshape(h, w, 3), pconv_mod.numpy_convolve(img, 7))
