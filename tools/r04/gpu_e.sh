@@ -10,6 +10,8 @@ export TMPDIR=/tmp
 PYT="python -u -m pytest -x -q --timeout 200 --timeout-method thread"
 timeout -k 10 500 $PYT tests/test_gpu_ipc.py > $OUT/pytest_ipc.txt 2>&1 || { echo "ipc tests failed"; tail -40 $OUT/pytest_ipc.txt; exit 1; }
 tail -2 $OUT/pytest_ipc.txt
+timeout -k 10 500 $PYT tests/test_gpu_stream.py tests/test_gpu_engine.py -k "stream or rings" > $OUT/pytest_stream.txt 2>&1 || { echo "stream tests failed"; tail -40 $OUT/pytest_stream.txt; exit 1; }
+tail -2 $OUT/pytest_stream.txt
 one() {  # name, env..., -- bench args
   local name=$1; shift
   local envs=()
@@ -34,6 +36,14 @@ for s in 3 4; do
   one n1_s${s}_200 X=1 -- --steps 200 --warmup 30 --slots $s || exit 1
 done
 one n1_s4_plain_200 PCONV_SLOT_STREAMS=plain -- --steps 200 --warmup 30 --slots 4 || exit 1
+for s in 3 4; do
+  for c in 2 4; do
+    one n1_s${s}_head${c}_20a X=1 -- --steps 20 --warmup 5 --slots $s --stream-chunks $c || exit 1
+    one n1_s${s}_head${c}_20b X=1 -- --steps 20 --warmup 5 --slots $s --stream-chunks $c || exit 1
+  done
+done
+one n1_s4_head4_200 X=1 -- --steps 200 --warmup 30 --slots 4 --stream-chunks 4 || exit 1
+one e8_s4_head2 X=1 -- $E --slots 4 --stream-chunks 2 || exit 1
 PCONV_SLOT_STREAMS=cumask timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_s4 -o run \
   -- python3 bench.py $E --slots 4 --no-check > $OUT/trace_s4.log 2>&1 || { echo "trace failed"; tail -5 $OUT/trace_s4.log; exit 1; }
 d=$(dirname $(find $OUT/trace_s4 -name run_kernel_trace.csv | head -1))
