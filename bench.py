@@ -371,6 +371,9 @@ def run_native(a) -> int:
         cmd.append("--check")
     if a.transport == "gloo-host":
         cmd += ["--transport", "shm"]  # rehearsal: ranks may share one GPU
+    if a.emulate:
+        cmd[cmd.index("--gpus") + 1] = "1"
+        cmd += ["--emulate", a.emulate]  # one rank of a WORLD-way split, alone (per-rank proxy)
     env = dict(os.environ)
     want = a.hw_queues if a.hw_queues else max(8, a.slots + 3)  # as for the torch pipeline below
     if a.hw_queues or int(env.get("GPU_MAX_HW_QUEUES", "4")) < want:

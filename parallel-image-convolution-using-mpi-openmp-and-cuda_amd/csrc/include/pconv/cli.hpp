@@ -55,6 +55,10 @@ struct CliConfig {
   int bench_steps = 0;
   int slots = 3;
   int stream_chunks = 0;  // rows streamed within each image (EngineOptions::stream_chunks)
+  // --bench --emulate W:R: time rank R of a W-way split alone in this process
+  // (its band + pre-loaded ghost rows): the per-rank proxy of bench.py
+  // --emulate, on the native stack.  0 = off.
+  int emulate_world = 0, emulate_rank = 0;
 };
 
 // Parse argv.  Throws pconv::Error with the message to print on bad input.

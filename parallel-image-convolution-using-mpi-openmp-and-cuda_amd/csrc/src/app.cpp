@@ -603,12 +603,15 @@ constexpr double kBaselineMpix = 190.3;  // CUDA 1920x2520 RGB 40 reps end to en
 void bench_rank(const CliConfig& c, BenchShared* sh, uint8_t* image, int rank) {
   set_error_rank(rank);
   const ImageGeom g = geom_of(c);
-  const int world = c.gpus;
+  const bool emu = c.emulate_world > 0;
+  const int world = emu ? c.emulate_world : c.gpus;
+  const int ndev_ranks = emu ? 1 : world;  // processes sharing the node's GPUs
+  if (emu) rank = c.emulate_rank;
   const int ndev = device_count();
-  PCONV_CHECK(c.transport == "shm" || ndev >= world,
+  PCONV_CHECK(c.transport == "shm" || ndev >= ndev_ranks,
               "need " + std::to_string(world) + " GPUs, " + std::to_string(ndev) + " visible (--transport shm lets "
               "bench ranks share one GPU)");
-  const int device = rank % ndev;
+  const int device = emu ? 0 : rank % ndev;
   set_device(device);
   if (world > 1) (void)bind_to_device_numa(device);
   const Filter f = Filter::by_name(c.filter);
@@ -642,13 +645,14 @@ void bench_rank(const CliConfig& c, BenchShared* sh, uint8_t* image, int rank) {
   };
   for (int i = 0; i < c.warmup; ++i) submit();
   pipe.drain();
-  shm_barrier(&sh->st, world, c.timeout_s);
+  shm_barrier(&sh->st, ndev_ranks, c.timeout_s);
   const double t0 = wall_seconds();
   for (int i = 0; i < c.bench_steps; ++i) submit();
   pipe.drain();
   const double t1 = wall_seconds();
-  shm_barrier(&sh->st, world, c.timeout_s);
-  sh->sec[rank] = t1 - t0;
+  shm_barrier(&sh->st, ndev_ranks, c.timeout_s);
+  const int slot = emu ? 0 : rank;  // shared-state index of this process
+  sh->sec[slot] = t1 - t0;
   // one image alone (nothing else queued): the reference GPU_convolution() scope
   std::vector<double> lat;
   int last = 0;
@@ -659,10 +663,10 @@ void bench_rank(const CliConfig& c, BenchShared* sh, uint8_t* image, int rank) {
     lat.push_back((wall_seconds() - a) * 1e3);
   }
   std::sort(lat.begin(), lat.end());
-  sh->lat_ms[rank] = lat[lat.size() / 2];
+  sh->lat_ms[slot] = lat[lat.size() / 2];
   std::memcpy(image + b.y0 * rb, outs[last].data(), static_cast<size_t>(b.rows * rb));
-  sh->pair_ms[rank] = copy_pair_floor_ms(device, rb, in_rows, b.rows, 8);
-  if (rank == 0) {
+  sh->pair_ms[slot] = copy_pair_floor_ms(device, rb, in_rows, b.rows, 8);
+  if (slot == 0) {
     sh->launches = e0.last_stats().launches;
     sh->halo = static_cast<int>(d);
     sh->fuse = e0.options().fuse;
@@ -670,7 +674,7 @@ void bench_rank(const CliConfig& c, BenchShared* sh, uint8_t* image, int rank) {
     sh->hip_version = h.runtime_version;
     std::snprintf(sh->hip_path, sizeof(sh->hip_path), "%s", h.runtime_path.c_str());
   }
-  shm_barrier(&sh->st, world, c.timeout_s);
+  shm_barrier(&sh->st, ndev_ranks, c.timeout_s);
 }
 
 std::string bench_metric(const CliConfig& c) {
@@ -749,7 +753,18 @@ std::string run_bench_impl(const CliConfig& c) {
     pair = std::max(pair, sh->pair_ms[r]);
     per << (r ? ", " : "") << sh->sec[r] / c.bench_steps * 1e3;
   }
-  const int64_t mism = c.check ? compare_with_oracle(c, g, image) : -1;
+  int64_t mism = -1;
+  if (c.check && c.emulate_world > 0) {
+    // the emulated rank's rows only (the rest of the image was never computed)
+    const Band b = row_band(g.height, c.emulate_world, c.emulate_rank);
+    std::vector<uint8_t> in(static_cast<size_t>(g.bytes())), ref(static_cast<size_t>(g.bytes()));
+    load_rows(c, g, 0, g.height, in.data(), g.row_bytes());
+    cpu_convolve(Filter::by_name(c.filter), g, in.data(), ref.data(), c.reps, CpuBackend::OpenMP, c.threads);
+    mism = 0;
+    for (int64_t i = b.y0 * g.row_bytes(); i < (b.y0 + b.rows) * g.row_bytes(); ++i) mism += ref[i] != image[i];
+  } else if (c.check) {
+    mism = compare_with_oracle(c, g, image);
+  }
   const double px = static_cast<double>(c.width) * static_cast<double>(c.height) * c.reps;
   const double value = px * c.bench_steps / sec / 1e6;
   const bool head = c.width == 1920 && c.height == 2520 && c.channels == Channels::Rgb && c.reps == 40 &&
@@ -771,13 +786,17 @@ std::string run_bench_impl(const CliConfig& c) {
      << c.filter << " convolution, " << c.width << "x" << c.height << " " << channels_name(c.channels) << ", "
      << c.reps << " reps\", \"global_batch\": 1, \"seq_len\": " << c.height << ", \"parallelism\": \"rowband"
      << c.gpus << "\", \"step\": \"H2D + reps + D2H per image (reference GPU_convolution scope)\", \"halo_mode\": \""
-     << (c.gpus > 1 ? "preload" : "none") << "\", \"images_in_flight\": " << c.slots
+     << (c.gpus > 1 || c.emulate_world > 1 ? "preload" : "none") << "\", \"images_in_flight\": " << c.slots
      << ", \"stream_chunks\": " << c.stream_chunks << ", \"halo_depth\": " << sh->halo << ", \"fuse\": " << sh->fuse
      << ", \"launches_per_step\": " << sh->launches << "}, \"latency_ms\": " << lat
      << ", \"copy_floor\": {\"pair_ms\": " << pair << "}";
   if (mism >= 0)
     os << ", \"mismatches\": " << mism
        << ", \"check\": \"newest image of every rank vs the CPU oracle (OpenMP), after the timed region\"";
+  if (c.emulate_world > 0)
+    os << ", \"emulated\": \"rank " << c.emulate_rank << " of a " << c.emulate_world
+       << "-way split on one GPU; value = this rank's step rate x full-image pixels (proxy, not a multi-GPU "
+          "measurement)\"";
   os << ", \"runtime\": {\"stack\": \"native conv (no torch)\", \"hip_runtime_version\": " << sh->hip_version
      << ", \"hip_runtime_path\": \"" << json_escape(sh->hip_path) << "\", \"rccl_version\": null}"
      << ", \"per_rank_ms_per_step\": [" << per.str() << "]}";

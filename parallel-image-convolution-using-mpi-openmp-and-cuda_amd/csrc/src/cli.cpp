@@ -61,6 +61,7 @@ std::string help_text(const std::string& prog) {
          "                            --warmup untimed ones; prints bench.py's JSON line (native stack)\n"
          "  --slots S                 --bench: images in flight (default 3)\n"
          "  --stream-chunks C         --bench: rows of each image streamed in C chunks (0 = off)\n"
+         "  --emulate W:R             --bench: time rank R of a W-way split alone (per-rank proxy)\n"
          "\n"
          "       " + prog + " --serve SOCKET [--device D] [--idle-timeout S] [--max-engines N]\n"
          "                            resident service: initialise the GPU once, then run jobs sent by\n"
@@ -158,6 +159,12 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       c.bench_steps = static_cast<int>(parse_int(next("--bench"), "--bench", 1, 1 << 24));
     } else if (a == "--slots") {
       c.slots = static_cast<int>(parse_int(next("--slots"), "--slots", 1, 8));
+    } else if (a == "--emulate") {
+      const std::string v = next("--emulate");
+      const size_t colon = v.find(':');
+      if (colon == std::string::npos) PCONV_FAIL("invalid --emulate '" + v + "' (WORLD:RANK)");
+      c.emulate_world = static_cast<int>(parse_int(v.substr(0, colon), "--emulate world", 1, 64));
+      c.emulate_rank = static_cast<int>(parse_int(v.substr(colon + 1), "--emulate rank", 0, c.emulate_world - 1));
     } else if (a == "--stream-chunks") {
       c.stream_chunks = static_cast<int>(parse_int(next("--stream-chunks"), "--stream-chunks", 0, 4096));
     } else if (a == "--warmup") {
@@ -167,6 +174,8 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
     }
   }
   if (c.backend != Backend::Hip && c.gpus != 1) PCONV_FAIL("--gpus requires --backend hip");
+  if (c.emulate_world > 0 && (c.bench_steps == 0 || c.gpus != 1))
+    PCONV_FAIL("--emulate needs --bench and --gpus 1 (one process times one rank of the split)");
   return c;
 }
 

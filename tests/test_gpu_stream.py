@@ -121,3 +121,22 @@ def test_native_bench_line(gpus, extra):
     assert d["runtime"]["stack"].startswith("native") and "torch" not in d["runtime"]["hip_runtime_path"]
     assert d["config"]["parallelism"] == f"rowband{gpus}" and len(d["per_rank_ms_per_step"]) == gpus
     assert d["latency_ms"] > 0 and d["copy_floor"]["pair_ms"] > 0
+
+
+def test_native_bench_emulated_rank():
+    """`bench.py --native --emulate 8:3`: the per-rank proxy on the native
+    stack (its band + pre-loaded ghost rows), oracle-checked on its rows."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--native", "--emulate", "8:3", "--steps", "20",
+           "--warmup", "3"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["mismatches"] == 0 and "rank 3 of a 8-way split" in d["emulated"]
+    assert d["config"]["halo_mode"] == "preload" and d["config"]["halo_depth"] == 40
