@@ -21,6 +21,7 @@
 #include "pconv/cpu_stencil.hpp"
 #include "pconv/device.hpp"
 #include "pconv/engine.hpp"
+#include "pconv/ipc_halo.hpp"
 #include "pconv/kernels.hpp"
 #include "pconv/raw_io.hpp"
 #include "pconv/rccl_comm.hpp"
@@ -343,6 +344,10 @@ struct SharedState {
   int launches[kMaxRanks];
   int exchanges[kMaxRanks];
   char error[512];
+  // --transport ipc: every rank's frame handles (hipIpcMemHandle_t x 2) and
+  // the flag segment's name
+  uint8_t ipc_handles[kMaxRanks][2 * sizeof(hipIpcMemHandle_t)];
+  char ipc_segment[64];
 };
 
 void shm_barrier(SharedState* s, int world, double timeout_s) {
@@ -404,9 +409,10 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
   const ImageGeom g = geom_of(c);
   const int world = c.gpus;
   const int ndev = device_count();
-  const bool shm = c.transport == "shm";
-  // RCCL needs one GPU per rank; the shared-memory transport may oversubscribe.
-  PCONV_CHECK(shm || ndev >= world,
+  const bool shm = c.transport == "shm", ipc = c.transport == "ipc";
+  // RCCL needs one GPU per rank; the shared-memory and IPC transports may
+  // oversubscribe (several ranks on one GPU).
+  PCONV_CHECK(shm || ipc || ndev >= world,
               "need " + std::to_string(world) + " GPUs, " + std::to_string(ndev) + " visible (try --transport shm)");
   const int device = rank % ndev;
   set_device(device);
@@ -429,8 +435,23 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
   }
 
   std::shared_ptr<RcclComm> comm;
+  std::shared_ptr<IpcHaloTransport> ipct;
   if (shm) {
     eng.set_transport(std::make_shared<ShmTransport>(sh, halo_slots, slot_bytes, rank, world, c.timeout_s));
+  } else if (ipc) {
+    // Device-side pulls of the neighbours' rows (ipc_halo.hpp): export this
+    // rank's frames, meet, open the neighbours' frames, meet.
+    ipct = std::make_shared<IpcHaloTransport>(eng, sh->ipc_segment, 0, 1, c.timeout_s);
+    const auto h = ipct->local_handles();
+    std::memcpy(sh->ipc_handles[rank], h.data(), h.size());
+    shm_barrier(sh, world, c.timeout_s);
+    auto blob = [&](int r) {
+      return r < 0 ? std::vector<uint8_t>() : std::vector<uint8_t>(sh->ipc_handles[r], sh->ipc_handles[r] + h.size());
+    };
+    ipct->connect(blob(b.up), blob(b.down));
+    eng.set_transport(ipct);
+    shm_barrier(sh, world, c.timeout_s);
+    if (rank == 0) ipc_unlink_segment(sh->ipc_segment);  // every rank has it mapped
   } else {
     if (rank == 0) {
       const auto id = rccl_unique_id();
@@ -453,6 +474,7 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
     eng.run(c.reps);
     if (comm) comm->wait(eng.comm_stream(), c.timeout_s);
     eng.synchronize();
+    if (ipct) ipct->check();
   }
   eng.upload_rows(host.data(), rb, -above, b.rows + below);
   eng.set_halo_valid(c.preload_halo);
@@ -473,6 +495,7 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
       comm->wait(eng.comm_stream(), c.timeout_s);
     }
     eng.synchronize();
+    if (ipct) ipct->check();
     launches += eng.last_stats().launches;
     exchanges += eng.last_stats().exchanges;
     done += k;
@@ -514,6 +537,10 @@ AppReport run_multi(const CliConfig& c) {
   sh->arrived = 0;
   sh->generation = 0;
   sh->failed = 0;
+  if (c.transport == "ipc") {
+    std::snprintf(sh->ipc_segment, sizeof(sh->ipc_segment), "/pconv_conv_%d", static_cast<int>(getpid()));
+    ipc_create_segment(sh->ipc_segment, c.gpus, 1);
+  }
   // Halo staging slots for --transport shm: [rank][top|bottom][depth * pitch].
   uint8_t* slots = nullptr;
   int64_t slot_bytes = 0, slots_total = 0;
@@ -552,6 +579,7 @@ AppReport run_multi(const CliConfig& c) {
     waitpid(p, &st, 0);
     ok = ok && WIFEXITED(st) && WEXITSTATUS(st) == 0;
   }
+  if (c.transport == "ipc") ipc_unlink_segment(sh->ipc_segment);  // (no-op when rank 0 already did)
   if (slots) munmap(slots, static_cast<size_t>(slots_total));
   AppReport r;
   r.gpus = c.gpus;

@@ -48,8 +48,9 @@ std::string help_text(const std::string& prog) {
          "  --checkpoint-every K      write <out>.rep<N> every K repetitions\n"
          "  --explain                 print the halo/launch schedule\n"
          "  --timeout S               RCCL watchdog timeout in seconds (default 600)\n"
-         "  --transport {rccl,shm}    multi-GPU halo transport (shm: host-staged through shared memory;\n"
-         "                            lets several ranks share one GPU)\n"
+         "  --transport {rccl,shm,ipc}  multi-GPU halo transport (shm: host-staged through shared memory;\n"
+         "                            ipc: device-side pulls of the neighbours' rows through HIP IPC;\n"
+         "                            both let several ranks share one GPU)\n"
          "  --exchange-halo           ranks load only their own rows; ghost rows come from neighbours\n"
          "  --warmup N                untimed runs of the schedule before loading the image (default 1;\n"
          "                            loads the kernels' code objects and sets up RCCL connections)\n"
@@ -143,8 +144,8 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       c.quiet = true;
     } else if (a == "--transport") {
       c.transport = next("--transport");
-      if (c.transport != "rccl" && c.transport != "shm")
-        PCONV_FAIL("invalid --transport '" + c.transport + "' (rccl|shm)");
+      if (c.transport != "rccl" && c.transport != "shm" && c.transport != "ipc")
+        PCONV_FAIL("invalid --transport '" + c.transport + "' (rccl|shm|ipc)");
     } else if (a == "--exchange-halo") {
       c.preload_halo = false;
     } else if (a == "--copies") {

@@ -109,23 +109,31 @@ def test_cli_hip(pconv_mod, tmp_path, rng):
         assert np.array_equal(out, pconv_mod.numpy_convolve(img, 11))
 
 
-@pytest.mark.parametrize("extra", [
-    ["--gpus", "2"],
-    ["--gpus", "3", "--exchange-halo"],
-    ["--gpus", "4", "--halo", "2", "--fuse", "2"],
-    ["--gpus", "2", "--filter", "box"],
-    ["--gpus", "3", "--no-overlap", "--exchange-halo", "--filter", "edge"],
+@pytest.mark.parametrize("transport,extra", [
+    ("shm", ["--gpus", "2"]),
+    ("shm", ["--gpus", "3", "--exchange-halo"]),
+    ("shm", ["--gpus", "4", "--halo", "2", "--fuse", "2"]),
+    ("shm", ["--gpus", "2", "--filter", "box"]),
+    ("shm", ["--gpus", "3", "--no-overlap", "--exchange-halo", "--filter", "edge"]),
+    ("ipc", ["--gpus", "2", "--exchange-halo"]),
+    ("ipc", ["--gpus", "3", "--exchange-halo", "--halo", "2", "--fuse", "2"]),
+    ("ipc", ["--gpus", "4", "--exchange-halo", "--no-overlap", "--filter", "box"]),
+    ("ipc", ["--gpus", "5", "--halo", "3", "--fuse", "3", "--checkpoint-every", "5"]),
 ])
-def test_cli_multi_rank_shm(pconv_mod, tmp_path, rng, extra):
-    """Native fork launcher, several ranks on one GPU, host-staged shm halos."""
+def test_cli_multi_rank_shm(pconv_mod, tmp_path, rng, transport, extra):
+    """Native fork launcher, several ranks on one GPU: host-staged shm halos,
+    or device-side IPC pulls of the neighbours' rows (ipc_halo.hpp) —
+    exchanges at every phase with --exchange-halo / shallow halos."""
     img = rng.integers(0, 256, size=(77, 61, 3), dtype=np.uint8)
     pconv_mod.write_raw(str(tmp_path / "img.raw"), img)
-    r = subprocess.run([CONV_BIN, "img.raw", "61", "77", "13", "rgb", "--transport", "shm", "--check", "--json"]
+    r = subprocess.run([CONV_BIN, "img.raw", "61", "77", "13", "rgb", "--transport", transport, "--check", "--json"]
                        + extra, cwd=tmp_path, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     meta = json.loads(r.stdout.strip().splitlines()[-1])
     assert meta["mismatches"] == 0
     assert meta["gpus"] == int(extra[1])
+    if "--exchange-halo" in extra or "--halo" in extra:
+        assert meta["exchanges"] >= 1
     filt = extra[extra.index("--filter") + 1] if "--filter" in extra else "gaussian"
     out = pconv_mod.read_raw(str(tmp_path / "blur_img.raw"), 61, 77, "rgb")
     assert np.array_equal(out, pconv_mod.numpy_convolve(img, 13, filt))

@@ -44,6 +44,11 @@ for s in 3 4; do
 done
 one n1_s4_head4_200 X=1 -- --steps 200 --warmup 30 --slots 4 --stream-chunks 4 || exit 1
 one e8_s4_head2 X=1 -- $E --slots 4 --stream-chunks 2 || exit 1
+# the same steps on the native stack (conv --bench: ROCm's HIP runtime, no torch)
+for s in 3 4; do
+  one nat_n1_s${s}_200 X=1 -- --native --steps 200 --warmup 30 --slots $s || exit 1
+  one nat_e8_s${s} X=1 -- --native $E --slots $s || exit 1
+done
 PCONV_SLOT_STREAMS=cumask timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_s4 -o run \
   -- python3 bench.py $E --slots 4 --no-check > $OUT/trace_s4.log 2>&1 || { echo "trace failed"; tail -5 $OUT/trace_s4.log; exit 1; }
 d=$(dirname $(find $OUT/trace_s4 -name run_kernel_trace.csv | head -1))
