@@ -119,3 +119,11 @@ def test_ipc_stalled_neighbour_times_out(pconv_mod):
     res = _run(pconv_mod, 2, cfg, timeout=200)
     r0 = res[0]
     assert isinstance(r0[2], str) and "timed out" in r0[2], r0
+
+
+def test_ipc_segments_unlinked():
+    """Every IPC job unlinks its flag segment once all ranks have mapped it:
+    nothing of this suite is left in /dev/shm."""
+    import glob
+
+    assert not glob.glob("/dev/shm/pconv_ipc_*") and not glob.glob("/dev/shm/pconv_conv_*")

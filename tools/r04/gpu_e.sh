@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 PYT="python -u -m pytest -x -q --timeout 200 --timeout-method thread"
 timeout -k 10 500 $PYT tests/test_gpu_ipc.py > $OUT/pytest_ipc.txt 2>&1 || { echo "ipc tests failed"; tail -40 $OUT/pytest_ipc.txt; exit 1; }
 tail -2 $OUT/pytest_ipc.txt
-timeout -k 10 500 $PYT tests/test_gpu_stream.py tests/test_gpu_engine.py -k "stream or rings" > $OUT/pytest_stream.txt 2>&1 || { echo "stream tests failed"; tail -40 $OUT/pytest_stream.txt; exit 1; }
+timeout -k 10 500 $PYT tests/test_gpu_stream.py tests/test_gpu_engine.py -k "stream or rings or multi_rank" > $OUT/pytest_stream.txt 2>&1 || { echo "stream tests failed"; tail -40 $OUT/pytest_stream.txt; exit 1; }
 tail -2 $OUT/pytest_stream.txt
 one() {  # name, env..., -- bench args
   local name=$1; shift
