@@ -35,6 +35,12 @@ struct AppReport {
   // creation included; these phases say where that time goes.
   std::vector<std::pair<std::string, double>> phases;
   double since_exec_s = 0;  // process start (exec) -> report, 10 ms resolution (/proc)
+  // --backend auto: repetitions run on the CPU before the handoff / on the
+  // GPU after it, the CPU's measured time per repetition, and why the GPU
+  // was (not) used.
+  int cpu_reps = -1, gpu_reps = -1;
+  double cpu_rep_s = 0;
+  std::string auto_choice;
 };
 
 // Runs the CLI (argv as given).  Returns the process exit code.

@@ -17,7 +17,9 @@
 
 namespace pconv {
 
-enum class Backend { Hip, Cpu, Omp };
+// Auto (one-shot, 1 GPU): the CPU starts at once while the GPU comes up, the
+// GPU takes over the remaining repetitions (app.cpp run_auto).
+enum class Backend { Hip, Cpu, Omp, Auto };
 enum class TimeFormat { Auto, Cuda, Mpi, Both };
 
 struct CliConfig {

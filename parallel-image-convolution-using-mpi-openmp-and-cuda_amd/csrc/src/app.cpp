@@ -333,6 +333,158 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   return r;
 }
 
+// ------------------------------------------------------- CPU head start + GPU
+// `--backend auto`, the one-shot form of the reference's cuda/main.c:20-49
+// run.  A cold process spends 50-190 ms bringing the GPU up (runtime,
+// context, first queue; BASELINE.md phase tables) before its first kernel,
+// while one repetition of a 1920x2520 RGB frame takes ~0.5 ms on the
+// node's CPUs.  So the CPU starts the repetitions at once (OpenMP, the
+// bit-exact oracle path), and:
+//   * after the first, timed repetition the rest of the job is priced on the
+//     CPU; below kAutoGpuMinS the GPU is never touched (no HIP call at all:
+//     no driver open, no teardown wait for the next process);
+//   * otherwise a helper thread brings the GPU up (context, code objects,
+//     queue, frames, pinned staging, one warm-up schedule) while the CPU
+//     keeps going; at the first repetition boundary after the device is
+//     ready the newest CPU frame is uploaded and the GPU runs the rest.
+// CPU and GPU repetitions are bit-identical step by step, so the handoff
+// point never shows in the output.  A failed GPU bring-up leaves the job on
+// the CPU (reported in auto_choice).
+// CPU time left after the first repetition below which the GPU is not
+// started (PCONV_AUTO_GPU_MIN_S overrides; 0 = always start it).
+constexpr double kAutoGpuMinS = 0.1;
+
+double auto_gpu_min_s() {
+  const char* v = std::getenv("PCONV_AUTO_GPU_MIN_S");
+  return v && *v ? std::strtod(v, nullptr) : kAutoGpuMinS;
+}
+
+AppReport run_auto(const CliConfig& c) {
+  AppReport r;
+  const double t0 = wall_seconds();
+  PhaseClock pc(&r.phases);
+  const ImageGeom g = geom_of(c);
+  if (!c.synthetic) validate_input_file(c.image, g);
+  const Filter f = Filter::by_name(c.filter);
+  const int64_t rb = g.row_bytes();
+  const FrameLayout lay = FrameLayout::make(rb, g.height, 1);
+  std::vector<uint8_t> fa(static_cast<size_t>(lay.bytes()), 0), fb(static_cast<size_t>(lay.bytes()), 0);
+  load_rows(c, g, 0, g.height, fa.data() + lay.offset(0), lay.pitch);
+  pc.mark(c.synthetic ? "synthesize" : "read");
+  if (c.threads > 0)
+    omp_set_num_threads(c.threads);
+  else
+    (void)configure_cpu_threads();  // leaves a CPU for the bring-up thread
+  uint8_t* src = fa.data();
+  uint8_t* dst = fb.data();
+  r.output = out_path(c);
+  r.kernel = "cpu-omp";
+  const double l0 = wall_seconds();
+  int done = 0;
+  auto cpu_rep = [&] {
+    cpu_step(f, g.channels, lay, src, dst, 0, g.height, CpuBackend::OpenMP);
+    std::swap(src, dst);  // newest result is always `src`
+    ++done;
+  };
+  if (c.reps > 0) cpu_rep();
+  r.cpu_rep_s = wall_seconds() - l0;
+  const double cpu_rest_s = r.cpu_rep_s * (c.reps - done);
+  const bool use_gpu = done < c.reps && cpu_rest_s >= auto_gpu_min_s();
+  r.auto_choice = use_gpu ? "gpu started after the first cpu repetition" : "cpu only (job shorter than gpu start-up)";
+
+  // GPU bring-up on a helper thread; `ready` publishes the finished engine.
+  struct Gpu {
+    std::atomic<int> state{0};  // 0 pending, 1 ready, 2 failed
+    std::string error;
+    PinnedBuffer host;
+    Stream stream;
+    std::unique_ptr<BandEngine> eng;
+    double ready_s = 0;
+  } gpu;
+  const int device = 0;
+  std::thread bring_up;
+  if (use_gpu) {
+    bring_up = std::thread([&] {
+      try {
+        set_device(device);
+        PCONV_HIP_CHECK(hipFree(nullptr));
+        preload_kernel_module();
+        const bool prev = std::getenv("PCONV_AUTOTUNE") ? true : set_shape_tuning(false);
+        gpu.host = PinnedBuffer(static_cast<size_t>(g.bytes()));
+        EngineOptions o = engine_options(c, g, 1, device);
+        o.kernel_copies = c.copies != 0;  // one-shot process: CU copies unless --copies sdma
+        gpu.stream = Stream::create(0);
+        o.compute_stream = gpu.stream.get();
+        gpu.eng = std::make_unique<BandEngine>(g, row_band(g.height, 1, 0), f, o);
+        // one launch of the production kernel on the zeroed frames (first-use costs)
+        for (int i = 0; i < std::max(1, c.warmup); ++i) gpu.eng->run(std::min(c.reps, gpu.eng->options().fuse));
+        gpu.eng->synchronize();
+        if (!std::getenv("PCONV_AUTOTUNE")) (void)set_shape_tuning(prev);
+        gpu.ready_s = wall_seconds() - t0;
+        gpu.state.store(1, std::memory_order_release);
+      } catch (const std::exception& e) {
+        gpu.error = e.what();
+        gpu.state.store(2, std::memory_order_release);
+      }
+    });
+  }
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } join_bring_up{bring_up};
+  // CPU repetitions until the device is ready (or the job is done).
+  while (done < c.reps && !(use_gpu && gpu.state.load(std::memory_order_acquire) == 1)) cpu_rep();
+  r.cpu_reps = done;
+  r.gpu_reps = 0;
+  if (done < c.reps) {
+    // Handoff: the newest CPU frame -> pinned staging -> device, the rest on the GPU.
+    pc.mark("cpu_loop");
+    set_device(device);
+    BandEngine& eng = *gpu.eng;
+    uint8_t* host = gpu.host.data();
+#pragma omp parallel for schedule(static)
+    for (int64_t y = 0; y < g.height; ++y) std::memcpy(host + y * rb, src + lay.offset(y), static_cast<size_t>(rb));
+    eng.upload_rows(host, rb, 0, g.height);
+    eng.run(c.reps - done);
+    eng.download_rows(host, rb, 0, g.height);
+    eng.synchronize();
+    r.launches = eng.last_stats().launches;
+    r.gpu_reps = c.reps - done;
+    r.loop_s = wall_seconds() - l0;
+    pc.mark("gpu_loop");
+    r.halo = eng.options().halo_depth;
+    r.fuse = eng.options().fuse;
+    r.kernel = std::string("cpu-omp+") + kernel_variant_name(eng.options().variant);
+    r.copies = eng.options().kernel_copies ? "kernel" : "sdma";
+    r.auto_choice += "; gpu ready at " + std::to_string(gpu.ready_s) + " s";
+    write_image(r.output, g, host);
+    pc.mark("write");
+    r.e2e_s = wall_seconds() - t0;
+    if (c.check) r.mismatches = compare_with_oracle(c, g, host);
+  } else {
+    r.loop_s = wall_seconds() - l0;
+    pc.mark("cpu_loop");
+    std::vector<uint8_t> img(static_cast<size_t>(g.bytes()));
+    for (int64_t y = 0; y < g.height; ++y) std::memcpy(img.data() + y * rb, src + lay.offset(y), static_cast<size_t>(rb));
+    write_image(r.output, g, img.data());
+    pc.mark("write");
+    if (use_gpu) {
+      // The CPU finished first: the bring-up still has to end before the
+      // process may (its time is in e2e_s).
+      bring_up.join();
+      pc.mark("gpu_join");
+      r.auto_choice += gpu.state.load() == 2 ? "; gpu bring-up failed: " + gpu.error : "; cpu finished first";
+    }
+    r.e2e_s = wall_seconds() - t0;
+    if (c.check) r.mismatches = compare_with_oracle(c, g, img.data());
+  }
+  r.gpus = r.gpu_reps > 0 ? 1 : 0;
+  r.since_exec_s = seconds_since_exec();
+  return r;
+}
+
 // ------------------------------------------------------------------ N GPUs
 struct SharedState {
   std::atomic<int> id_ready;
@@ -839,14 +991,20 @@ std::string run_bench(const CliConfig& c) { return run_bench_impl(c); }
 
 AppReport run_app(const CliConfig& c, JobCache* cache) {
   AppReport r;
-  if (c.backend != Backend::Hip)
+  if (c.backend == Backend::Auto && cache == nullptr && c.checkpoint_every == 0) {
+    r = run_auto(c);  // sets r.gpus (0 when the GPU was not used)
+  } else if (c.backend == Backend::Cpu || c.backend == Backend::Omp) {
     r = run_cpu(c);
-  else if (c.gpus > 1) {
+    r.gpus = 0;
+  } else if (c.gpus > 1) {
+    // (--backend auto in a resident server or with checkpoints: the GPU path)
     PCONV_CHECK(cache == nullptr, "the resident service runs one GPU per server (--gpus 1)");
     r = run_multi(c);
-  } else
+    r.gpus = c.gpus;
+  } else {
     r = run_gpu1(c, cache);
-  r.gpus = c.backend == Backend::Hip ? c.gpus : 0;
+    r.gpus = c.gpus;
+  }
   const double px = static_cast<double>(c.width) * static_cast<double>(c.height) * c.reps;
   r.mpix_per_s = r.loop_s > 0 ? px / r.loop_s / 1e6 : 0.0;
   return r;
@@ -857,7 +1015,8 @@ std::string report_json(const CliConfig& c, const AppReport& r) {
   const double px = static_cast<double>(c.width) * static_cast<double>(c.height) * c.reps;
   os << "{\"width\": " << c.width << ", \"height\": " << c.height << ", \"channels\": \""
      << channels_name(c.channels) << "\", \"reps\": " << c.reps << ", \"filter\": \"" << c.filter
-     << "\", \"backend\": \"" << (c.backend == Backend::Hip ? "hip" : c.backend == Backend::Omp ? "omp" : "cpu")
+     << "\", \"backend\": \""
+     << (c.backend == Backend::Hip ? "hip" : c.backend == Backend::Omp ? "omp" : c.backend == Backend::Auto ? "auto" : "cpu")
      << "\", \"gpus\": " << r.gpus << ", \"kernel\": \"" << r.kernel << "\", \"halo\": " << r.halo
      << ", \"fuse\": " << r.fuse << ", \"launches\": " << r.launches << ", \"exchanges\": " << r.exchanges
      << ", \"loop_s\": " << r.loop_s << ", \"e2e_s\": " << r.e2e_s << ", \"loop_mpix_per_s\": " << r.mpix_per_s
@@ -866,7 +1025,10 @@ std::string report_json(const CliConfig& c, const AppReport& r) {
      << ", \"rccl_loaded\": " << (rccl_loaded() ? "true" : "false");
   if (rccl_loaded()) os << ", \"rccl_version\": \"" << rccl_version() << "\", \"rccl_path\": \""
                         << json_escape(rccl_library_path()) << "\"";
-  if (c.backend == Backend::Hip && c.gpus <= 1) {  // (the --gpus N launcher process never touches HIP)
+  if (r.cpu_reps >= 0)
+    os << ", \"cpu_reps\": " << r.cpu_reps << ", \"gpu_reps\": " << r.gpu_reps << ", \"cpu_rep_s\": " << r.cpu_rep_s
+       << ", \"auto_choice\": \"" << json_escape(r.auto_choice) << "\"";
+  if ((c.backend == Backend::Hip && c.gpus <= 1) || r.gpu_reps > 0) {  // (the --gpus N launcher never touches HIP)
     const HipRuntimeInfo h = hip_runtime_info();
     os << ", \"hip_runtime_version\": " << h.runtime_version << ", \"hip_runtime_path\": \""
        << json_escape(h.runtime_path) << "\"";
@@ -1008,7 +1170,8 @@ int conv_main(int argc, char** argv) {
     const AppReport r = run_app(c);
     if (!c.quiet) {
       TimeFormat fmt = c.format;
-      if (fmt == TimeFormat::Auto) fmt = (c.backend == Backend::Hip && c.gpus == 1) ? TimeFormat::Cuda : TimeFormat::Mpi;
+      if (fmt == TimeFormat::Auto)
+        fmt = ((c.backend == Backend::Hip || c.backend == Backend::Auto) && c.gpus == 1) ? TimeFormat::Cuda : TimeFormat::Mpi;
       if (fmt == TimeFormat::Mpi || fmt == TimeFormat::Both) std::printf("%f\n", r.loop_s);
       if (fmt == TimeFormat::Cuda || fmt == TimeFormat::Both) std::printf("Execution time: %.3f sec\n", r.e2e_s);
     }

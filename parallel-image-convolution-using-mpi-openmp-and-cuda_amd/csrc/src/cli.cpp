@@ -31,7 +31,9 @@ std::string usage_text(const std::string& prog) {
 std::string help_text(const std::string& prog) {
   return "usage: " + prog +
          " image.raw width height repetitions {grey,rgb,rgba} [options]\n"
-         "  --backend {hip,cpu,omp}   compute backend (default hip)\n"
+         "  --backend {hip,cpu,omp,auto}  compute backend (default hip; auto: the CPU starts the repetitions\n"
+         "                            at once while the GPU initialises, the GPU takes over the rest; jobs\n"
+         "                            shorter on the CPU than the GPU's start-up never touch the GPU)\n"
          "  --gpus N                  row-band decomposition over N GPUs, one process each (RCCL halos)\n"
          "  --filter {gaussian,box,edge}  3x3 filter (default gaussian)\n"
          "  --halo D                  ghost rows exchanged at once (default: auto)\n"
@@ -92,7 +94,8 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       if (v == "hip") c.backend = Backend::Hip;
       else if (v == "cpu") c.backend = Backend::Cpu;
       else if (v == "omp") c.backend = Backend::Omp;
-      else PCONV_FAIL("invalid --backend '" + v + "' (hip|cpu|omp)");
+      else if (v == "auto") c.backend = Backend::Auto;
+      else PCONV_FAIL("invalid --backend '" + v + "' (hip|cpu|omp|auto)");
     } else if (a == "--gpus") {
       c.gpus = static_cast<int>(parse_int(next("--gpus"), "--gpus", 1, 64));
     } else if (a == "--filter") {
@@ -175,6 +178,7 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
     }
   }
   if (c.backend != Backend::Hip && c.gpus != 1) PCONV_FAIL("--gpus requires --backend hip");
+  if (c.backend == Backend::Auto && c.bench_steps > 0) PCONV_FAIL("--bench runs on the GPU (--backend hip)");
   if (c.emulate_world > 0 && (c.bench_steps == 0 || c.gpus != 1))
     PCONV_FAIL("--emulate needs --bench and --gpus 1 (one process times one rank of the split)");
   return c;

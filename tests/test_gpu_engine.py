@@ -312,3 +312,29 @@ def test_copy_pair_floor(native):
     assert ms >= rb * rows / 64e9 * 1e3
     with pytest.raises(Exception):
         native.copy_pair_floor_ms(0, rb, 0, rows, 4)
+
+
+@pytest.mark.parametrize("typ,filt,reps", [("rgb", "gaussian", 1500), ("grey", "gaussian", 3000), ("rgb", "box", 600)])
+def test_cli_auto_backend_hands_off_to_gpu(pconv_mod, tmp_path, typ, filt, reps):
+    """`--backend auto` with the GPU started at once (PCONV_AUTO_GPU_MIN_S=0):
+    the CPU (one thread here, so it is still busy when the device is up) runs
+    repetitions while the GPU comes up, then the newest CPU frame moves to the
+    GPU, which runs the rest; the result equals the CPU oracle of all `reps`
+    bit for bit whatever the handoff point."""
+    from pconv.models.filters import get_filter
+
+    w, h = 640, 480
+    env = dict(os.environ, PCONV_AUTO_GPU_MIN_S="0")
+    r = subprocess.run([CONV_BIN, "s.raw", str(w), str(h), str(reps), typ, "--synthetic", "11", "--backend", "auto",
+                        "--threads", "1", "--filter", filt, "--json", "--quiet"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    meta = json.loads(r.stdout.strip().splitlines()[-1])
+    assert meta["cpu_reps"] >= 1 and meta["gpu_reps"] >= 1 and meta["cpu_reps"] + meta["gpu_reps"] == reps, meta
+    assert meta["gpus"] == 1 and meta["kernel"].startswith("cpu-omp+")
+    out = pconv_mod.read_raw(str(tmp_path / "blur_s.raw"), w, h, typ)
+    img = pconv_mod.synthetic_image(w, h, typ, seed=11)
+    ref = np.empty_like(img)
+    pconv_mod.native.cpu_convolve(img.reshape(-1), ref.reshape(-1), w, h, typ, reps, get_filter(filt).to_native(),
+                                  True, 0)
+    assert np.array_equal(out, ref)

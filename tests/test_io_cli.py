@@ -125,3 +125,37 @@ def test_cli_bench_flags(tmp_path):
     assert r.returncode == 1 and "invalid --stream-chunks" in r.stderr
     r = _run(["--help"], tmp_path)
     assert "--bench K" in r.stdout and "--stream-chunks" in r.stdout
+
+
+@pytest.mark.parametrize("typ", ["grey", "rgb"])
+def test_cli_auto_backend_small_job_stays_on_cpu(pconv_mod, tmp_path, rng, typ):
+    """`--backend auto`: a job whose CPU time (priced from its first, timed
+    repetition) is below the GPU's start-up never touches the GPU; the output
+    is the oracle's and the JSON says where every repetition ran."""
+    c = 1 if typ == "grey" else 3
+    img = rng.integers(0, 256, size=(37, 29, c) if c > 1 else (37, 29), dtype=np.uint8)
+    pconv_mod.write_raw(str(tmp_path / "img.raw"), img)
+    r = _run(["img.raw", "29", "37", "7", typ, "--backend", "auto", "--json", "--check"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert lines[0].startswith("Execution time:")  # the one-shot (CUDA-style) line
+    meta = json.loads(lines[-1])
+    assert meta["backend"] == "auto" and meta["gpus"] == 0
+    assert meta["cpu_reps"] == 7 and meta["gpu_reps"] == 0 and meta["mismatches"] == 0
+    assert meta["auto_choice"].startswith("cpu only")
+    out = pconv_mod.read_raw(str(tmp_path / "blur_img.raw"), 29, 37, typ)
+    assert np.array_equal(out, pconv_mod.numpy_convolve(img, 7))
+
+
+def test_cli_auto_backend_without_gpu_falls_back(pconv_mod, tmp_path):
+    """Forced GPU start (PCONV_AUTO_GPU_MIN_S=0) on a machine whose GPU cannot
+    come up: the job finishes on the CPU, bit-exact, and says why."""
+    env = dict(os.environ, PCONV_AUTO_GPU_MIN_S="0", HIP_VISIBLE_DEVICES="-1")
+    r = subprocess.run([CONV_BIN, "s.raw", "48", "40", "9", "rgb", "--synthetic", "5", "--backend", "auto", "--json",
+                        "--check", "--quiet"], cwd=tmp_path, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    meta = json.loads(r.stdout.strip().splitlines()[-1])
+    assert meta["cpu_reps"] == 9 and meta["gpu_reps"] == 0 and meta["mismatches"] == 0
+    assert "gpu started" in meta["auto_choice"] and "failed" in meta["auto_choice"]
+    out = pconv_mod.read_raw(str(tmp_path / "blur_s.raw"), 48, 40, "rgb")
+    assert np.array_equal(out, pconv_mod.numpy_convolve(pconv_mod.synthetic_image(48, 40, "rgb", seed=5), 9))
