@@ -94,8 +94,9 @@ int auto_fuse(const Filter& f, KernelVariant v, int64_t frame_bytes, int channel
 // program is involved — a one-shot process saves their first-use set-up
 // (~8 ms per SDMA direction and the blit code object, profiles/r02/), at
 // 44-53 GB/s instead of SDMA's 54 (tools/ubench/copy_bw.hip).
+// max_blocks > 0 caps the grid (a copy beside stencil launches leaves them CUs).
 void launch_copy_rows(const uint8_t* src, int64_t sp, uint8_t* dst, int64_t dp, int64_t row_bytes, int64_t rows,
-                      hipStream_t stream);
+                      hipStream_t stream, int max_blocks = 0);
 // Zero `bytes` (a multiple of 16, 16-byte aligned) with a kernel of this module.
 void launch_fill_zero(uint8_t* p, int64_t bytes, hipStream_t stream);
 // Load the code object of the temporal / copy kernels now (a one-shot process

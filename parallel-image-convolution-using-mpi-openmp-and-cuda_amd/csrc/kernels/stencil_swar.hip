@@ -899,11 +899,13 @@ unsigned copy_blocks(int64_t work) {
 }  // namespace
 
 void launch_copy_rows(const uint8_t* src, int64_t sp, uint8_t* dst, int64_t dp, int64_t row_bytes, int64_t rows,
-                      hipStream_t stream) {
+                      hipStream_t stream, int max_blocks) {
   PCONV_CHECK(row_bytes >= 0 && rows >= 0 && sp >= row_bytes && dp >= row_bytes, "copy_rows: bad geometry");
   if (row_bytes == 0 || rows == 0) return;
   const int64_t cpr = ceil_div<int64_t>(row_bytes, 16), total = cpr * rows;
-  k_copy_rows<<<dim3(copy_blocks(total)), dim3(256), 0, stream>>>(src, sp, dst, dp, row_bytes, cpr, total);
+  unsigned blocks = copy_blocks(total);
+  if (max_blocks > 0) blocks = std::min<unsigned>(blocks, static_cast<unsigned>(max_blocks));
+  k_copy_rows<<<dim3(blocks), dim3(256), 0, stream>>>(src, sp, dst, dp, row_bytes, cpr, total);
   PCONV_HIP_CHECK(hipGetLastError());
 }
 

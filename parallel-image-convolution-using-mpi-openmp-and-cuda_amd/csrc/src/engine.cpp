@@ -374,10 +374,25 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
   // previous chunk's launches), then each chunk's launches behind its
   // upload's event, then each download behind its chunk's event.  One event
   // per chunk and direction (no re-recorded event is waited on).
+  // PCONV_STREAM_COPIES=kernel (A/B): chunk copies as CU kernels (a capped
+  // grid beside the launches) instead of SDMA.
+  static const int kcopy_blocks = [] {
+    const char* v = std::getenv("PCONV_STREAM_COPIES");
+    return v && std::string(v).rfind("kernel", 0) == 0 ? std::max(8, std::atoi(v + 6) > 0 ? std::atoi(v + 6) : 128)
+                                                        : 0;
+  }();
+  auto copy = [&](uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, int64_t rows, hipMemcpyKind kind,
+                  hipStream_t s) {
+    if (rows <= 0) return;
+    if (kcopy_blocks > 0)
+      launch_copy_rows(src, spitch, dst, dpitch, rb, rows, s, kcopy_blocks);
+    else
+      PCONV_HIP_CHECK(hipMemcpy2DAsync(dst, dpitch, src, spitch, rb, rows, kind, s));
+  };
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
-    PCONV_HIP_CHECK(hipMemcpy2DAsync(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, rb,
-                                     ch.up_hi - ch.up_lo, hipMemcpyHostToDevice, up));
+    copy(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, ch.up_hi - ch.up_lo,
+         hipMemcpyHostToDevice, up);
     if (up != cs_) up_evs_[c].record(up);
   }
   bool pending = false;  // launches not yet covered by a download-side event
@@ -402,8 +417,8 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
     const StreamChunk& ch = sp.chunks[c];
     if (!(ch.down_hi > ch.down_lo && host_out)) continue;
     if (down != cs_) dn_evs_[c].wait_on(down);
-    PCONV_HIP_CHECK(hipMemcpy2DAsync(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, rb,
-                                     ch.down_hi - ch.down_lo, hipMemcpyDeviceToHost, down));
+    copy(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, ch.down_hi - ch.down_lo, hipMemcpyDeviceToHost,
+         down);
   }
   if (pending && down != cs_) dn_evs_[nc].wait_on(down);
   cur_ = (c0 + sp.levels) & 1;

@@ -22,3 +22,11 @@ for c in 2 4; do
     python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['ms_per_step'], d['latency_ms'], d['copy_floor']['pair_ms'], d.get('mismatches'))" $OUT/bench_h${c}_$i.json
   done
 done
+# single-image latency of a row-streamed image: SDMA chunk copies vs CU copy kernels (capped grids)
+for cc in sdma kernel64 kernel128 kernel256; do
+  for c in 4 8; do
+    n=lat_${cc}_c$c
+    PCONV_STREAM_COPIES=$cc timeout -k 10 150 python -u bench.py --gpus 1 --steps 20 --warmup 5 --stream-chunks $c --loop-steps 3 > $OUT/$n.json 2> $OUT/$n.err || { echo "bench $n failed"; tail -5 $OUT/$n.err; exit 1; }
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['ms_per_step'], d['latency_ms'], d['copy_floor']['pair_ms'], d.get('mismatches'))" $OUT/$n.json
+  done
+done
