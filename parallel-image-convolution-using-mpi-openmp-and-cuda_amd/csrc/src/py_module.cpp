@@ -184,6 +184,29 @@ PYBIND11_MODULE(_pconv_native, m) {
   m.def("stream_cuts", &stream_cuts, py::arg("in_lo"), py::arg("in_hi"), py::arg("chunks"));
   m.def("plan_streamed", &plan_streamed, py::arg("plan"), py::arg("in_lo"), py::arg("in_hi"), py::arg("owned_rows"),
         py::arg("cuts"));
+  py::class_<WaveTask>(m, "WaveTask")
+      .def_readonly("kind", &WaveTask::kind)
+      .def_readonly("level", &WaveTask::level)
+      .def_readonly("a", &WaveTask::a)
+      .def_readonly("b", &WaveTask::b)
+      .def_readonly("part", &WaveTask::part)
+      .def_readonly("tile", &WaveTask::tile)
+      .def_readonly("dep_lo", &WaveTask::dep_lo)
+      .def_readonly("dep_hi", &WaveTask::dep_hi)
+      .def_property_readonly("dep_level", &WaveTask::dep_level);
+  py::class_<WavePlan>(m, "WavePlan")
+      .def_readonly("levels", &WavePlan::levels)
+      .def_readonly("tile_rows", &WavePlan::tile_rows)
+      .def_readonly("steps", &WavePlan::steps)
+      .def_readonly("lo", &WavePlan::lo)
+      .def_readonly("hi", &WavePlan::hi)
+      .def_readonly("tiles", &WavePlan::tiles)
+      .def_readonly("arrivals", &WavePlan::arrivals)
+      .def_readonly("counter_base", &WavePlan::counter_base)
+      .def_readonly("counters", &WavePlan::counters)
+      .def_readonly("tasks", &WavePlan::tasks);
+  m.def("plan_wave", &plan_wave, py::arg("plan"), py::arg("in_lo"), py::arg("in_hi"), py::arg("owned_rows"),
+        py::arg("tile_rows"), py::arg("col_groups"), py::arg("load_parts") = 1, py::arg("store_parts") = 1);
 
   // ---------------------------------------------------------------- CPU oracle
   m.def(

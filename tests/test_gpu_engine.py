@@ -314,16 +314,17 @@ def test_copy_pair_floor(native):
         native.copy_pair_floor_ms(0, rb, 0, rows, 4)
 
 
-@pytest.mark.parametrize("typ,filt,reps", [("rgb", "gaussian", 1500), ("grey", "gaussian", 3000), ("rgb", "box", 600)])
-def test_cli_auto_backend_hands_off_to_gpu(pconv_mod, tmp_path, typ, filt, reps):
+@pytest.mark.parametrize("typ,filt,w,h,reps", [("rgb", "gaussian", 1536, 1024, 2000), ("grey", "gaussian", 2048, 2048, 4000),
+                                               ("rgb", "box", 1024, 768, 600)])
+def test_cli_auto_backend_hands_off_to_gpu(pconv_mod, tmp_path, typ, filt, w, h, reps):
     """`--backend auto` with the GPU started at once (PCONV_AUTO_GPU_MIN_S=0):
     the CPU (one thread here, so it is still busy when the device is up) runs
     repetitions while the GPU comes up, then the newest CPU frame moves to the
     GPU, which runs the rest; the result equals the CPU oracle of all `reps`
-    bit for bit whatever the handoff point."""
+    bit for bit whatever the handoff point.  (Jobs of ~1-2 s on one CPU
+    thread: the GPU comes up within a few hundred ms.)"""
     from pconv.models.filters import get_filter
 
-    w, h = 640, 480
     env = dict(os.environ, PCONV_AUTO_GPU_MIN_S="0")
     r = subprocess.run([CONV_BIN, "s.raw", str(w), str(h), str(reps), typ, "--synthetic", "11", "--backend", "auto",
                         "--threads", "1", "--filter", filt, "--json", "--quiet"], cwd=tmp_path, capture_output=True,
