@@ -72,7 +72,9 @@ struct EngineOptions {
   // image overlap on three streams.  0 / 1: whole-image chain.  Issued
   // directly (BandPipeline's event-ordered mode): captured as one graph with
   // fork/join branches it measured 1.4-4.3x slower per image
-  // (profiles/r04/stream_a/).
+  // (profiles/r04/stream_a/).  -1: the image is ONE persistent launch
+  // instead (enqueue_wave, kernels/stencil_wave.hip): copies by the CUs and
+  // every level in one grid, device-side hand-offs, no cross-stream hop.
   int stream_chunks = 0;
 };
 
@@ -166,6 +168,18 @@ class BandEngine {
   // chunk).  The caller orders `up` after any earlier use of these frames.
   void enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
                         const StreamPlan& sp, hipStream_t up, hipStream_t down);
+  // Wave image: the same serving step as ONE persistent launch on `stream`
+  // (default: the compute stream) — loads from pinned host memory, every
+  // level and stores to pinned host memory by one resident grid taking
+  // plan_wave's tasks in ticket order.  wave_able() says whether this
+  // image can (exchange-free gaussian plan, whole dwords per row, a task
+  // list of bounded size); enqueue_wave throws otherwise.  A dependency
+  // wait that times out inside the kernel raises at synchronize().
+  bool wave_able(int reps, int64_t in_r0, int64_t in_r1) const;
+  void enqueue_wave(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps,
+                    hipStream_t stream = nullptr);
+  // Tasks of the cached wave plan for these rows (tests / diagnostics; 0 if none).
+  int wave_tasks(int reps, int64_t in_r0, int64_t in_r1) const;
   // Phase-by-phase execution for multi-band emulation on one device.
   std::vector<Phase> plan(int reps) const;
   void exec_exchange(const Phase& p);
@@ -219,6 +233,16 @@ class BandEngine {
   // entries the stream is drained and the cache is emptied.
   void trim_graph_caches();
   std::map<std::tuple<int, int, const uint8_t*, int64_t, int64_t, uint8_t*>, StepGraph> step_graphs_;
+  // wave images: task list + per-level table on the device per (reps, in_r0, in_r1)
+  struct WaveDev {
+    int ntasks = 0, levels = 0;
+    DeviceBuffer tasks, table;
+  };
+  std::map<std::tuple<int, int64_t, int64_t>, WaveDev> waves_;
+  DeviceBuffer wave_ctl_;  // ticket, abort, tile counters (zeroed by every launch)
+  PinnedBuffer wave_err_;  // set by the kernel when a dependency wait timed out
+  uint64_t wave_timeout_ticks_ = 0;
+  const WaveDev& wave_dev(int reps, int64_t in_r0, int64_t in_r1);
 };
 
 // Serving pipeline: S band engines ("slots") so that the H2D copy of image
@@ -284,6 +308,7 @@ class BandPipeline {
   // step-graph mode with stream_chunks > 1: images submitted while nothing is
   // in flight (after construction / drain) are row-streamed (head streaming)
   bool idle_ = true;
+  bool wave_all_ = false;  // stream_chunks -1: every image a wave launch (A/B), not only the head
   Event ev_head_, h2d_wait_;
   std::vector<bool> used_;
   int64_t count_ = 0;

@@ -99,6 +99,33 @@ void launch_copy_rows(const uint8_t* src, int64_t sp, uint8_t* dst, int64_t dp, 
                       hipStream_t stream, int max_blocks = 0);
 // Zero `bytes` (a multiple of 16, 16-byte aligned) with a kernel of this module.
 void launch_fill_zero(uint8_t* p, int64_t bytes, hipStream_t stream);
+// ONE persistent launch for a whole serving step (kernels/stencil_wave.hip;
+// task list from schedule.hpp plan_wave, gaussian only).
+struct WaveTask;
+struct WaveLaunch {
+  const WaveTask* tasks = nullptr;  // device copy of WavePlan::tasks (ticket order)
+  int ntasks = 0;
+  int levels = 0;                   // L
+  int channels = 1;
+  const int* levels_dev = nullptr;  // device int4 per level 0..L: {steps, arrivals, counter_base, 0}
+  uint32_t* ctl = nullptr;          // zeroed by every launch: [0] ticket, [1] abort, [4..] tile counters
+  int64_t ctl_bytes = 0;            // a multiple of 16
+  uint32_t* err = nullptr;          // pinned host word, set to 1 when a wait timed out
+  const uint8_t* host_in = nullptr; // pinned, input rows [in_r0, in_r1) contiguous
+  int64_t in_r0 = 0;
+  uint8_t* host_out = nullptr;      // pinned, owned rows contiguous
+  uint8_t* frame0 = nullptr;        // device frames at (row 0, column 0)
+  uint8_t* frame1 = nullptr;
+  int64_t pitch = 0, row_bytes = 0, g_row0 = 0, height = 0;
+  uint64_t timeout_ticks = 0;       // wall-clock ticks a dependency wait may take
+  int max_workgroups = 0;           // 0: the resident grid
+};
+void launch_wave_image(const WaveLaunch& w, hipStream_t stream);
+// Rows one wave-kernel tile computes at `max_steps` steps (the plan's tile_rows).
+int wave_tile_rows(int max_steps);
+// Column groups (strip pairs) of one wave-kernel level tile; 0 = steps too deep.
+int wave_col_groups(int channels, int steps, int64_t row_bytes);
+
 // Load the code object of the temporal / copy kernels now (a one-shot process
 // calls it from a helper thread while it creates its first hardware queue).
 void preload_kernel_module();

@@ -1,0 +1,325 @@
+// One image as ONE persistent launch: H2D by the CUs, every level of the
+// temporal-blocked gaussian, D2H by the CUs (schedule.hpp: plan_wave).
+//
+// What it replaces: the reference's GPU_convolution() is a serial chain of
+// cudaMemcpy -> `reps` launches -> cudaMemcpy (cuda/cuda_convolution.cu:
+// 60-97); the row-streamed image (engine.cpp enqueue_streamed) overlaps the
+// three across streams but pays 15-22 us per cross-stream hand-off.  Here the
+// workgroups of one resident grid take tasks in ticket order:
+//   * load: host rows -> frame 0 (16-byte loads straight from pinned host
+//     memory over PCIe, 8 in flight per lane);
+//   * level tile: one SWAR temporal tile (the k_swar_pf tile of
+//     stencil_swar.hip: 4-byte lanes, buffer-op loads with the range check
+//     doing the zero padding, `steps` repetitions in registers with LDS
+//     boundary rows) of level j, frame (j-1) % 2 -> frame j % 2;
+//   * store: final rows -> host.
+// A task first waits for the row tiles it depends on (plan_wave: the tiles it
+// reads and the tiles that still read what it overwrites), each complete when
+// its counter holds the level's task count.  Hand-offs follow the agent-scope
+// recipe of the CDNA4 guide (per-XCD L2s are not coherent): producer — every
+// wave drains its stores (s_waitcnt vmcnt(0)), workgroup barrier, one lane
+// releases (buffer_wbl2 sc1), waits again, then adds to the counter;
+// consumer — one lane polls the counters with relaxed agent loads (s_sleep
+// between polls), ONE acquire (buffer_inv sc1) + wait, workgroup barrier,
+// then plain loads.  Every poll is bounded by a wall-clock timeout: a
+// timed-out wait sets the abort word, every workgroup leaves at its next
+// ticket, and the host raises (BandEngine::synchronize).
+// Tickets come from one device-scope counter; the plan's ticket order is
+// topological, so a workgroup only ever waits on tasks already claimed by
+// running workgroups and the grid drains at any residency.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+
+#include "pconv/device.hpp"
+#include "pconv/kernels.hpp"
+#include "pconv/schedule.hpp"
+#include "swar_device.hpp"
+
+namespace pconv {
+namespace {
+
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+// Shared words are accessed as GLOBAL (not flat) agent-scope atomics.
+__device__ __forceinline__ gu32* gptr(const uint32_t* p) { return (gu32*)(const_cast<uint32_t*>(p)); }
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Rows [a, b) of `row_bytes` bytes from src (pitch sp) to dst (pitch dp), by
+// the whole workgroup: one row per wave at a time, 16-byte granules (4-byte
+// when the rows are not 16-byte aligned), up to 8 loads in flight per lane.
+__device__ __forceinline__ void copy_rows(const uint8_t* src, int64_t sp, uint8_t* dst, int64_t dp, int a, int b,
+                                          int row_bytes, int nwaves) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int U = 8;
+  const bool wide = (row_bytes % 16 == 0) && (sp % 16 == 0) && (dp % 16 == 0) &&
+                    (reinterpret_cast<uintptr_t>(src) % 16 == 0) && (reinterpret_cast<uintptr_t>(dst) % 16 == 0);
+  if (wide) {
+    const int g = row_bytes / 16;
+    for (int r = a + w; r < b; r += nwaves) {
+      const uint4* s = reinterpret_cast<const uint4*>(src + static_cast<int64_t>(r) * sp);
+      uint4* d = reinterpret_cast<uint4*>(dst + static_cast<int64_t>(r) * dp);
+      for (int c0 = lane; c0 < g; c0 += 64 * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (c0 + 64 * u < g) v[u] = s[c0 + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (c0 + 64 * u < g) d[c0 + 64 * u] = v[u];
+      }
+    }
+  } else {
+    const int g = row_bytes / 4;  // the wave path requires row_bytes % 4 == 0
+    for (int r = a + w; r < b; r += nwaves) {
+      const uint32_t* s = reinterpret_cast<const uint32_t*>(src + static_cast<int64_t>(r) * sp);
+      uint32_t* d = reinterpret_cast<uint32_t*>(dst + static_cast<int64_t>(r) * dp);
+      for (int c0 = lane; c0 < g; c0 += 64 * U) {
+        uint32_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (c0 + 64 * u < g) v[u] = s[c0 + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (c0 + 64 * u < g) d[c0 + 64 * u] = v[u];
+      }
+    }
+  }
+}
+
+// One tile of k_swar_pf (stencil_swar.hip) as a device function: output rows
+// [r0, r1) (r1 - r0 <= NW*M - 2*steps), column strip pair `col`.
+template <int CH, int M, int NW, bool ALT>
+__device__ __forceinline__ void wave_tile(const uint8_t* src, uint8_t* dst, int pitch, int row_bytes, int r0, int r1,
+                                          int steps, int g_row0, int height, int col,
+                                          uint4 (&lds)[2][NW][2][1][64]) {
+  constexpr int LW = 4, NP = 4;
+  constexpr u32 kOut = 0x80000000u;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hl = (steps * CH + LW - 1) / LW;
+  const int vbytes = (64 - 2 * hl) * LW;
+  const int nstrips = (row_bytes + vbytes - 1) / vbytes;
+  const int pair_stride = (nstrips + 1) / 2;
+  const int lo_ok = max(r0 - steps, -g_row0), hi_ok = min(r1 + steps, height - g_row0);
+  const int st_end = min(r1, height - g_row0);
+  const auto srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src) + static_cast<int64_t>(lo_ok) * pitch,
+                                                       0, max(hi_ok - lo_ok, 0) * pitch, 0x00020000);
+  const auto drsrc = __builtin_amdgcn_make_buffer_rsrc(dst + static_cast<int64_t>(r0) * pitch, 0,
+                                                       max(st_end - r0, 0) * pitch, 0x00020000);
+  const int sB = col + pair_stride;
+  const int baseA = col * vbytes - hl * LW, baseB = sB * vbytes - hl * LW;
+  const int pa = baseA + lane * LW, pb = baseB + lane * LW;
+  const int xA = (pa >= 0 && pa < row_bytes) ? pa : -1;
+  const int xB = (sB < nstrips && pb >= 0 && pb < row_bytes) ? pb : -1;
+  const bool needs_mask = baseA < 0 || baseA + 64 * LW > row_bytes || sB >= nstrips || baseB + 64 * LW > row_bytes;
+  const int row_base = r0 - steps + w * M;
+  u32 D[M][NP];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const int fr = row_base + i;
+    const bool rok = fr >= lo_ok && fr < hi_ok;
+    const u32 ro = static_cast<u32>(fr - lo_ok) * static_cast<u32>(pitch);
+    const u32 a = __builtin_amdgcn_raw_buffer_load_b32(srsrc, (rok && xA >= 0) ? ro + xA : kOut, 0, 0);
+    const u32 b = __builtin_amdgcn_raw_buffer_load_b32(srsrc, (rok && xB >= 0) ? ro + xB : kOut, 0, 0);
+    unpack<NP>(a, b, D[i]);
+  }
+  u32 cm[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k)
+    cm[k] = (xA >= 0 && xA + k < row_bytes ? 0xffffu : 0u) | (xB >= 0 && xB + k < row_bytes ? 0xffff0000u : 0u);
+  const int out_top = min(max(-g_row0 - row_base, 0), M);
+  const int out_bot = min(max(height - g_row0 - row_base, 0), M);
+  if constexpr (ALT) {
+    int s = 0;
+    for (; s + 2 <= steps; s += 2) {
+      swar_step<CH, NP, M, NW, 1>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+      swar_step<CH, NP, M, NW, 2>(D, lds, 1, w, lane, needs_mask, cm, out_top, out_bot);
+    }
+    if (s < steps) swar_step<CH, NP, M, NW, 0>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+  } else {
+    for (int s = 0; s < steps; ++s) swar_step<CH, NP, M, NW, 0>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
+  }
+  const bool lane_in = lane >= hl && lane < 64 - hl;
+  const int st_hi = min(r0 + NW * M - 2 * steps, st_end);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const int fr = row_base + i;
+    const bool rst = fr >= r0 && fr < st_hi;
+    const u32 ro = static_cast<u32>(fr - r0) * static_cast<u32>(pitch);
+    u32 a, bb;
+    pack<NP>(D[i], a, bb);
+    __builtin_amdgcn_raw_buffer_store_b32(a, drsrc, (rst && lane_in && xA >= 0) ? ro + xA : kOut, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(bb, drsrc, (rst && lane_in && xB >= 0) ? ro + xB : kOut, 0, 0);
+  }
+}
+
+struct WaveLevelDev {
+  int steps;
+  int arrivals;
+  int counter_base;
+  int pad;
+};
+
+struct WaveArgs {
+  const WaveTask* tasks;
+  int ntasks;
+  int levels;
+  uint32_t* ctl;  // [0] ticket, [1] abort; counters from ctl + 4
+  const WaveLevelDev* lv;
+  const uint8_t* host_in;  // row r of the input at host_in + (r - in_r0) * row_bytes
+  int in_r0;
+  uint8_t* host_out;       // owned row r at host_out + r * row_bytes
+  uint8_t* frame0;         // frames at (row 0, column 0)
+  uint8_t* frame1;
+  int pitch, row_bytes, g_row0, height;
+  uint64_t timeout;        // wall-clock ticks
+  uint32_t* err;           // pinned host word: 1 = a wait timed out
+};
+
+template <int CH, int M, int NW, bool ALT>
+__global__ __launch_bounds__(64 * NW) void k_wave(WaveArgs A) {
+  __shared__ uint4 lds[2][NW][2][1][64];
+  __shared__ int sh[2];
+  const int tid = threadIdx.x;
+  uint32_t* counters = A.ctl + 4;
+  while (true) {
+    if (tid == 0) {
+      int t = static_cast<int>(__hip_atomic_fetch_add(gptr(A.ctl), 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+      if (ld_agent(A.ctl + 1) != 0) t = A.ntasks;  // another workgroup gave up: drain
+      sh[0] = t;
+    }
+    __syncthreads();
+    const int ti = sh[0];
+    if (ti >= A.ntasks) break;  // uniform
+    const WaveTask k = A.tasks[ti];
+    if (tid == 0) {
+      int ok = 1;
+      if (k.kind != 0) {
+        const WaveLevelDev d = A.lv[k.level - 1];
+        const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
+        for (int x = k.dep_lo; x <= k.dep_hi && ok; ++x) {
+          const uint32_t* c = counters + d.counter_base + x;
+          while (static_cast<int>(ld_agent(c)) < d.arrivals) {
+            if (static_cast<uint64_t>(wall_clock64()) - t0 > A.timeout || ld_agent(A.ctl + 1) != 0) {
+              ok = 0;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        if (!ok) {
+          __hip_atomic_store(gptr(A.ctl + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      sh[1] = ok;
+    }
+    __syncthreads();
+    if (!sh[1]) break;  // uniform: a dependency never completed
+    if (k.kind == 0) {
+      copy_rows(A.host_in - static_cast<int64_t>(A.in_r0) * A.row_bytes, A.row_bytes, A.frame0, A.pitch, k.a, k.b,
+                A.row_bytes, NW);
+    } else if (k.kind == 1) {
+      const int s = A.lv[k.level].steps;
+      const uint8_t* src = (k.level - 1) & 1 ? A.frame1 : A.frame0;
+      uint8_t* dst = k.level & 1 ? A.frame1 : A.frame0;
+      wave_tile<CH, M, NW, ALT>(src, dst, A.pitch, A.row_bytes, k.a, k.b, s, A.g_row0, A.height, k.part, lds);
+    } else {
+      copy_rows(A.levels & 1 ? A.frame1 : A.frame0, A.pitch, A.host_out, A.row_bytes, k.a, k.b, A.row_bytes, NW);
+    }
+    if (k.kind != 2) {
+      // publish: every wave's stores drained, then one release and the arrival
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(gptr(counters + A.lv[k.level].counter_base + k.tile), 1u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();  // LDS and sh[] are reused by the next task
+  }
+}
+
+constexpr int kWaveM = 8, kWaveNW = 8;
+
+template <int CH>
+const void* wave_fn() {
+  return reinterpret_cast<const void*>(&k_wave<CH, kWaveM, kWaveNW, true>);
+}
+
+int wave_resident(const void* fn) {
+  static std::mutex mu;
+  static std::map<const void*, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(fn);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0, dev = 0, cus = 0;
+  PCONV_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * kWaveNW, 0));
+  PCONV_HIP_CHECK(hipGetDevice(&dev));
+  PCONV_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int n = std::max(1, per_cu) * std::max(1, cus);
+  cache.emplace(fn, n);
+  return n;
+}
+
+}  // namespace
+
+int wave_tile_rows(int max_steps) { return kWaveM * kWaveNW - 2 * max_steps; }
+
+int wave_col_groups(int channels, int steps, int64_t row_bytes) {
+  const int hl = (steps * channels + 3) / 4;
+  const int vbytes = (64 - 2 * hl) * 4;
+  if (vbytes <= 0) return 0;
+  const int64_t nstrips = (row_bytes + vbytes - 1) / vbytes;
+  return static_cast<int>((nstrips + 1) / 2);
+}
+
+void launch_wave_image(const WaveLaunch& w, hipStream_t s) {
+  PCONV_CHECK(w.tasks && w.levels_dev && w.ctl && w.err && w.frame0 && w.frame1 && w.host_in && w.host_out,
+              "wave launch: missing buffers");
+  PCONV_CHECK(w.row_bytes % 4 == 0 && w.pitch % 16 == 0, "wave launch: rows must be whole dwords");
+  PCONV_CHECK(w.ntasks > 0 && w.levels >= 1, "wave launch: empty plan");
+  PCONV_HIP_CHECK(hipMemsetAsync(w.ctl, 0, static_cast<size_t>(w.ctl_bytes), s));
+  WaveArgs A;
+  A.tasks = w.tasks;
+  A.ntasks = w.ntasks;
+  A.levels = w.levels;
+  A.ctl = w.ctl;
+  A.lv = reinterpret_cast<const WaveLevelDev*>(w.levels_dev);
+  A.host_in = w.host_in;
+  A.in_r0 = static_cast<int>(w.in_r0);
+  A.host_out = w.host_out;
+  A.frame0 = w.frame0;
+  A.frame1 = w.frame1;
+  A.pitch = static_cast<int>(w.pitch);
+  A.row_bytes = static_cast<int>(w.row_bytes);
+  A.g_row0 = static_cast<int>(w.g_row0);
+  A.height = static_cast<int>(std::min<int64_t>(w.height, int64_t(1) << 30));
+  A.timeout = w.timeout_ticks;
+  A.err = w.err;
+  const void* fn = w.channels == 1 ? wave_fn<1>() : w.channels == 3 ? wave_fn<3>() : wave_fn<4>();
+  int grid = std::min(w.ntasks, wave_resident(fn));
+  if (w.max_workgroups > 0) grid = std::min(grid, w.max_workgroups);
+  const dim3 g(static_cast<unsigned>(std::max(1, grid))), b(64 * kWaveNW);
+  switch (w.channels) {
+    case 1: k_wave<1, kWaveM, kWaveNW, true><<<g, b, 0, s>>>(A); break;
+    case 3: k_wave<3, kWaveM, kWaveNW, true><<<g, b, 0, s>>>(A); break;
+    case 4: k_wave<4, kWaveM, kWaveNW, true><<<g, b, 0, s>>>(A); break;
+    default: PCONV_FAIL("wave launch: channels must be 1, 3 or 4");
+  }
+  PCONV_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace pconv

@@ -63,7 +63,8 @@ std::string help_text(const std::string& prog) {
          "  --bench K                 serving bench: K timed images (H2D + reps + D2H each) per rank after\n"
          "                            --warmup untimed ones; prints bench.py's JSON line (native stack)\n"
          "  --slots S                 --bench: images in flight (default 3)\n"
-         "  --stream-chunks C         --bench: rows of each image streamed in C chunks (0 = off)\n"
+         "  --stream-chunks C         --bench: rows of each image streamed in C chunks (0 = off; -1 = one\n"
+         "                            persistent wave launch per image, stencil_wave.hip)\n"
          "  --emulate W:R             --bench: time rank R of a W-way split alone (per-rank proxy)\n"
          "\n"
          "       " + prog + " --serve SOCKET [--device D] [--idle-timeout S] [--max-engines N]\n"
@@ -170,7 +171,7 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       c.emulate_world = static_cast<int>(parse_int(v.substr(0, colon), "--emulate world", 1, 64));
       c.emulate_rank = static_cast<int>(parse_int(v.substr(colon + 1), "--emulate rank", 0, c.emulate_world - 1));
     } else if (a == "--stream-chunks") {
-      c.stream_chunks = static_cast<int>(parse_int(next("--stream-chunks"), "--stream-chunks", 0, 4096));
+      c.stream_chunks = static_cast<int>(parse_int(next("--stream-chunks"), "--stream-chunks", -1, 4096));
     } else if (a == "--warmup") {
       c.warmup = static_cast<int>(parse_int(next("--warmup"), "--warmup", 0, 100));
     } else {

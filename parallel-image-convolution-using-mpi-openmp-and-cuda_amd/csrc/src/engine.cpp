@@ -425,6 +425,118 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
   halo_valid_ = false;
 }
 
+namespace {
+
+constexpr int kWaveMaxTasks = 1 << 17;  // beyond this the ticket counter's serial rate dominates
+constexpr int kWaveLoadParts = 2, kWaveStoreParts = 2;
+
+}  // namespace
+
+bool BandEngine::wave_able(int reps, int64_t in_r0, int64_t in_r1) const {
+  if (reps < 1 || !filter_.binomial121 || lay_.row_bytes % 4 != 0) return false;
+  if (opt_.variant != KernelVariant::Auto && opt_.variant != KernelVariant::Temporal) return false;
+  if (lay_.total_rows() * lay_.pitch >= (int64_t(1) << 31) || geom_.height >= (int64_t(1) << 30)) return false;
+  PlanConfig c = engine_plan_config(geom_, band_, filter_, opt_);
+  c.halo_preloaded = input_preloaded(in_r0, in_r1);
+  const std::vector<Phase> ph = plan_band(band_, reps, c);
+  if (!streamable(ph)) return false;
+  int smax = 0;
+  int64_t tasks = 0;
+  for (const auto& p : ph) smax = std::max(smax, p.steps);
+  const int tr = wave_tile_rows(smax);
+  if (tr < 1) return false;
+  for (const auto& p : ph) {
+    const int g = wave_col_groups(geom_.ch(), p.steps, lay_.row_bytes);
+    if (g < 1) return false;
+    tasks += (p.launches[0].hi - p.launches[0].lo + tr - 1) / tr * g;
+  }
+  return tasks <= kWaveMaxTasks;
+}
+
+const BandEngine::WaveDev& BandEngine::wave_dev(int reps, int64_t in_r0, int64_t in_r1) {
+  const auto key = std::make_tuple(reps, in_r0, in_r1);
+  auto it = waves_.find(key);
+  if (it != waves_.end()) return it->second;
+  PCONV_CHECK(wave_able(reps, in_r0, in_r1), "enqueue_wave: this image cannot run as one wave launch");
+  PlanConfig c = engine_plan_config(geom_, band_, filter_, opt_);
+  c.halo_preloaded = input_preloaded(in_r0, in_r1);
+  const std::vector<Phase> ph = plan_band(band_, reps, c);
+  int smax = 0;
+  for (const auto& p : ph) smax = std::max(smax, p.steps);
+  std::vector<int> groups(ph.size() + 1, 0);
+  for (size_t j = 0; j < ph.size(); ++j) groups[j + 1] = wave_col_groups(geom_.ch(), ph[j].steps, lay_.row_bytes);
+  const WavePlan wp = plan_wave(ph, in_r0, in_r1, band_.rows, wave_tile_rows(smax), groups, kWaveLoadParts,
+                                kWaveStoreParts);
+  WaveDev d;
+  d.ntasks = static_cast<int>(wp.tasks.size());
+  d.levels = wp.levels;
+  d.tasks = DeviceBuffer(wp.tasks.size() * sizeof(WaveTask));
+  PCONV_HIP_CHECK(hipMemcpy(d.tasks.data(), wp.tasks.data(), wp.tasks.size() * sizeof(WaveTask), hipMemcpyHostToDevice));
+  std::vector<int> table(4 * (wp.levels + 1), 0);
+  for (int j = 0; j <= wp.levels; ++j) {
+    table[4 * j] = wp.steps[j];
+    table[4 * j + 1] = wp.arrivals[j];
+    table[4 * j + 2] = wp.counter_base[j];
+  }
+  d.table = DeviceBuffer(table.size() * sizeof(int));
+  PCONV_HIP_CHECK(hipMemcpy(d.table.data(), table.data(), table.size() * sizeof(int), hipMemcpyHostToDevice));
+  const size_t ctl = static_cast<size_t>(16 + 4 * wp.counters + 15) / 16 * 16;
+  if (wave_ctl_.size() < ctl) {
+    PCONV_HIP_CHECK(hipStreamSynchronize(cs_));  // an earlier wave may still use the old block
+    wave_ctl_ = DeviceBuffer(ctl);
+  }
+  if (!wave_err_.data()) {
+    wave_err_ = PinnedBuffer(64);
+    std::memset(wave_err_.data(), 0, 64);
+    int khz = 0;
+    PCONV_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, opt_.device));
+    double s = 2.0;  // a whole image is milliseconds; a stuck wait gives up after this
+    if (const char* t = std::getenv("PCONV_WAVE_TIMEOUT_S")) s = std::max(1e-7, std::atof(t));
+    wave_timeout_ticks_ = static_cast<uint64_t>(s * static_cast<double>(khz > 0 ? khz : 100000) * 1000.0);
+  }
+  return waves_.emplace(key, std::move(d)).first->second;
+}
+
+int BandEngine::wave_tasks(int reps, int64_t in_r0, int64_t in_r1) const {
+  auto it = waves_.find(std::make_tuple(reps, in_r0, in_r1));
+  return it == waves_.end() ? 0 : it->second.ntasks;
+}
+
+void BandEngine::enqueue_wave(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps,
+                              hipStream_t stream) {
+  TraceRange tr("pconv.wave_image");
+  PCONV_CHECK(host_in && host_out, "enqueue_wave: pinned host buffers required");
+  PCONV_CHECK(band_.y0 + in_r0 >= 0 && band_.y0 + in_r1 <= geom_.height && in_r0 >= -lay_.halo &&
+                  in_r1 <= lay_.rows + lay_.halo,
+              "enqueue_wave: input rows outside frame / image");
+  const WaveDev& d = wave_dev(reps, in_r0, in_r1);
+  WaveLaunch w;
+  w.tasks = static_cast<const WaveTask*>(static_cast<const void*>(d.tasks.data()));
+  w.ntasks = d.ntasks;
+  w.levels = d.levels;
+  w.channels = geom_.ch();
+  w.levels_dev = static_cast<const int*>(static_cast<const void*>(d.table.data()));
+  w.ctl = static_cast<uint32_t*>(static_cast<void*>(wave_ctl_.data()));
+  w.ctl_bytes = static_cast<int64_t>(wave_ctl_.size());
+  w.err = static_cast<uint32_t*>(static_cast<void*>(wave_err_.data()));
+  w.host_in = host_in;
+  w.in_r0 = in_r0;
+  w.host_out = host_out;
+  w.frame0 = frame_at(0);
+  w.frame1 = frame_at(1);
+  w.pitch = lay_.pitch;
+  w.row_bytes = lay_.row_bytes;
+  w.g_row0 = band_.y0;
+  w.height = geom_.height;
+  w.timeout_ticks = wave_timeout_ticks_;
+  if (const char* g = std::getenv("PCONV_WAVE_GRID")) w.max_workgroups = std::atoi(g);
+  launch_wave_image(w, stream ? stream : cs_);
+  stats_ = RunStats{};
+  stats_.launches = 1;
+  cur_ = d.levels & 1;
+  halo_valid_ = false;
+}
+
 void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
   TraceRange tr("pconv.step_graph");
   PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
@@ -500,6 +612,13 @@ void BandEngine::exec_compute(const Phase& p) {
 void BandEngine::synchronize() {
   PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
   if (ms_ != cs_) PCONV_HIP_CHECK(hipStreamSynchronize(ms_));
+  if (wave_err_.data()) {
+    auto* e = reinterpret_cast<volatile uint32_t*>(wave_err_.data());
+    if (*e != 0) {
+      *e = 0;
+      PCONV_FAIL("wave image: a dependency wait timed out inside the kernel (results of that image are invalid)");
+    }
+  }
   if (timing_pending_) {
     stats_.loop_ms = Event::elapsed_ms(ev_t0_, ev_t1_);
     stats_.wall_ms = (wall_seconds() - wall_t0_) * 1e3;
@@ -567,6 +686,10 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
       h2d_wait_ = Event::create();
     }
     used_.assign(slots, false);
+    // PCONV_WAVE_ALL=1 (A/B, with stream_chunks -1): every image a wave
+    // launch, not only the one submitted to an idle pipeline
+    const char* wa = std::getenv("PCONV_WAVE_ALL");
+    wave_all_ = wa && wa[0] == '1';
     return;
   }
   // Streams: H2D, D2H, communication (only with neighbours) and compute.
@@ -651,6 +774,16 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   }
   if (graphs_) {
     PCONV_CHECK(trace_ev_.empty(), "pipeline trace needs directly issued images (graph capture off)");
+    const bool wave = e.options().stream_chunks < 0;
+    if (wave && (idle_ || wave_all_) && e.wave_able(reps, in_r0, in_r1)) {
+      // Wave image: the whole step is ONE persistent launch on the slot's own
+      // stream (stream order covers the frames' earlier and later graphs).
+      e.enqueue_wave(host_in, in_r0, in_r1, host_out, reps, e.compute_stream());
+      idle_ = false;
+      used_[k] = true;
+      ++count_;
+      return;
+    }
     if (idle_ && h2d_.get()) {
       // Head streaming: nothing is in flight, so this image's rows stream
       // (chunked H2D ‖ launches ‖ D2H of finished rows, schedule.hpp

@@ -473,6 +473,8 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("kernel_copies") = false, py::arg("stream_chunks") = 0)
       .def_property_readonly("band", &BandEngine::band)
       .def("stream_plan", &BandEngine::stream_plan, py::arg("reps"), py::arg("in_r0"), py::arg("in_r1"))
+      .def("wave_able", &BandEngine::wave_able, py::arg("reps"), py::arg("in_r0"), py::arg("in_r1"))
+      .def("wave_tasks", &BandEngine::wave_tasks, py::arg("reps"), py::arg("in_r0"), py::arg("in_r1"))
       .def_property_readonly("halo", [](const BandEngine& e) { return e.layout().halo; })
       .def_property_readonly("fuse", [](const BandEngine& e) { return e.options().fuse; })
       .def_property_readonly("cached_graphs", &BandEngine::cached_graphs)
