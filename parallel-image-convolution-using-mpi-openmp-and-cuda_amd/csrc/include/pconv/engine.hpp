@@ -76,6 +76,9 @@ struct EngineOptions {
   // instead (enqueue_wave, kernels/stencil_wave.hip): copies by the CUs and
   // every level in one grid, device-side hand-offs, no cross-stream hop.
   int stream_chunks = 0;
+  // Step graphs record an event right after their upload (upload_event()):
+  // a pipeline staggers the first images of a burst on it (BandPipeline).
+  bool upload_event = false;
 };
 
 struct RunStats {
@@ -180,6 +183,9 @@ class BandEngine {
                     hipStream_t stream = nullptr);
   // Tasks of the cached wave plan for these rows (tests / diagnostics; 0 if none).
   int wave_tasks(int reps, int64_t in_r0, int64_t in_r1) const;
+  // With options().upload_event: recorded by every step graph once its
+  // upload is done.
+  const Event& upload_event() const { return ev_uploaded_; }
   // Phase-by-phase execution for multi-band emulation on one device.
   std::vector<Phase> plan(int reps) const;
   void exec_exchange(const Phase& p);
@@ -214,7 +220,7 @@ class BandEngine {
   int pre_exchanges_ = 0;  // exchange_now() calls since the last run()
   Stream own_cs_, own_ms_;
   hipStream_t cs_ = nullptr, ms_ = nullptr;
-  Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_;
+  Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_, ev_uploaded_;
   std::vector<Event> up_evs_, dn_evs_;  // streamed images: per chunk, uploaded / rows final
   std::shared_ptr<HaloTransport> transport_;
   RunStats stats_;
@@ -309,6 +315,13 @@ class BandPipeline {
   // in flight (after construction / drain) are row-streamed (head streaming)
   bool idle_ = true;
   bool wave_all_ = false;  // stream_chunks -1: every image a wave launch (A/B), not only the head
+  // Burst stagger (step-graph mode): image i < slots of a burst (counted from
+  // the last drain) starts its upload only when image i-1's upload is done,
+  // instead of all slots uploading at once and moving in lockstep.
+  bool stagger_ = true;
+  int burst_ = 0;
+  const Event* last_upload_ = nullptr;  // upload-done event of the burst's previous image
+  Event head_up_;                       // a streamed head image's uploads done
   Event ev_head_, h2d_wait_;
   std::vector<bool> used_;
   int64_t count_ = 0;

@@ -119,6 +119,8 @@ struct WaveLaunch {
   int64_t pitch = 0, row_bytes = 0, g_row0 = 0, height = 0;
   uint64_t timeout_ticks = 0;       // wall-clock ticks a dependency wait may take
   int max_workgroups = 0;           // 0: the resident grid
+  int poll_sleep = 2;               // s_sleep(8) (~0.2 us) between two polls of an incomplete counter
+  uint64_t* trace = nullptr;        // device, 4 x u64 per task (claimed, ready, done, wg | xcc << 32); nullable
 };
 void launch_wave_image(const WaveLaunch& w, hipStream_t stream);
 // Rows one wave-kernel tile computes at `max_steps` steps (the plan's tile_rows).

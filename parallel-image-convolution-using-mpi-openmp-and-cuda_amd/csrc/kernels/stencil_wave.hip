@@ -181,6 +181,8 @@ struct WaveArgs {
   int pitch, row_bytes, g_row0, height;
   uint64_t timeout;        // wall-clock ticks
   uint32_t* err;           // pinned host word: 1 = a wait timed out
+  int poll_sleep;          // s_sleep(8) (~0.2 us) per unsuccessful poll
+  uint64_t* trace;         // nullable: per task {claimed, deps met, done, workgroup | xcc << 32} (wall clock)
 };
 
 template <int CH, int M, int NW, bool ALT>
@@ -200,6 +202,8 @@ __global__ __launch_bounds__(64 * NW) void k_wave(WaveArgs A) {
     const int ti = sh[0];
     if (ti >= A.ntasks) break;  // uniform
     const WaveTask k = A.tasks[ti];
+    uint64_t tr_claim = 0;
+    if (A.trace && tid == 0) tr_claim = static_cast<uint64_t>(wall_clock64());
     if (tid == 0) {
       int ok = 1;
       if (k.kind != 0) {
@@ -212,7 +216,7 @@ __global__ __launch_bounds__(64 * NW) void k_wave(WaveArgs A) {
               ok = 0;
               break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            for (int z = 0; z < A.poll_sleep; ++z) __builtin_amdgcn_s_sleep(8);
           }
         }
         if (!ok) {
@@ -224,6 +228,8 @@ __global__ __launch_bounds__(64 * NW) void k_wave(WaveArgs A) {
       }
       sh[1] = ok;
     }
+    uint64_t tr_ready = 0;
+    if (A.trace && tid == 0) tr_ready = static_cast<uint64_t>(wall_clock64());
     __syncthreads();
     if (!sh[1]) break;  // uniform: a dependency never completed
     if (k.kind == 0) {
@@ -247,6 +253,15 @@ __global__ __launch_bounds__(64 * NW) void k_wave(WaveArgs A) {
         __hip_atomic_fetch_add(gptr(counters + A.lv[k.level].counter_base + k.tile), 1u,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+    }
+    if (A.trace && tid == 0) {
+      uint32_t xcc = 0;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+      uint64_t* t = A.trace + 4 * static_cast<int64_t>(ti);
+      t[0] = tr_claim;
+      t[1] = tr_ready;
+      t[2] = static_cast<uint64_t>(wall_clock64());
+      t[3] = static_cast<uint64_t>(blockIdx.x) | (static_cast<uint64_t>(xcc) << 32);
     }
     __syncthreads();  // LDS and sh[] are reused by the next task
   }
@@ -309,6 +324,8 @@ void launch_wave_image(const WaveLaunch& w, hipStream_t s) {
   A.height = static_cast<int>(std::min<int64_t>(w.height, int64_t(1) << 30));
   A.timeout = w.timeout_ticks;
   A.err = w.err;
+  A.poll_sleep = std::max(1, w.poll_sleep);
+  A.trace = w.trace;
   const void* fn = w.channels == 1 ? wave_fn<1>() : w.channels == 3 ? wave_fn<3>() : wave_fn<4>();
   int grid = std::min(w.ntasks, wave_resident(fn));
   if (w.max_workgroups > 0) grid = std::min(grid, w.max_workgroups);

@@ -64,6 +64,7 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
   ev_sync_ = Event::create();
   ev_t0_ = Event::create(true);
   ev_t1_ = Event::create(true);
+  if (opt_.upload_event) ev_uploaded_ = Event::create();
   PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
 }
 
@@ -530,7 +531,39 @@ void BandEngine::enqueue_wave(const uint8_t* host_in, int64_t in_r0, int64_t in_
   w.height = geom_.height;
   w.timeout_ticks = wave_timeout_ticks_;
   if (const char* g = std::getenv("PCONV_WAVE_GRID")) w.max_workgroups = std::atoi(g);
+  if (const char* z = std::getenv("PCONV_WAVE_SLEEP")) w.poll_sleep = std::max(1, std::atoi(z));
+  // PCONV_WAVE_TRACE=file: per-task wall-clock timeline of the next few wave
+  // images appended to `file` as JSON lines (diagnostics: the host waits for
+  // each traced image)
+  const char* trace_path = std::getenv("PCONV_WAVE_TRACE");
+  static int traced = 0;
+  DeviceBuffer trace;
+  if (trace_path && traced < 4) {
+    trace = DeviceBuffer(static_cast<size_t>(d.ntasks) * 32);
+    PCONV_HIP_CHECK(hipMemsetAsync(trace.data(), 0, trace.size(), stream ? stream : cs_));
+    w.trace = static_cast<uint64_t*>(static_cast<void*>(trace.data()));
+  }
   launch_wave_image(w, stream ? stream : cs_);
+  if (w.trace) {
+    ++traced;
+    PCONV_HIP_CHECK(hipStreamSynchronize(stream ? stream : cs_));
+    std::vector<uint64_t> t(static_cast<size_t>(d.ntasks) * 4);
+    std::vector<WaveTask> tasks(static_cast<size_t>(d.ntasks));
+    PCONV_HIP_CHECK(hipMemcpy(t.data(), trace.data(), trace.size(), hipMemcpyDeviceToHost));
+    PCONV_HIP_CHECK(hipMemcpy(tasks.data(), d.tasks.data(), d.tasks.size(), hipMemcpyDeviceToHost));
+    if (FILE* f = std::fopen(trace_path, "a")) {
+      std::fprintf(f, "{\"row_bytes\": %lld, \"rows\": %lld, \"levels\": %d, \"tasks\": [",
+                   static_cast<long long>(lay_.row_bytes), static_cast<long long>(band_.rows), d.levels);
+      for (size_t i = 0; i < tasks.size(); ++i) {
+        const WaveTask& k = tasks[i];
+        std::fprintf(f, "%s[%d,%d,%d,%d,%d,%d,%llu,%llu,%llu,%llu]", i ? "," : "", k.kind, k.level, k.a, k.b, k.part,
+                     k.tile, static_cast<unsigned long long>(t[4 * i]), static_cast<unsigned long long>(t[4 * i + 1]),
+                     static_cast<unsigned long long>(t[4 * i + 2]), static_cast<unsigned long long>(t[4 * i + 3]));
+      }
+      std::fprintf(f, "]}\n");
+      std::fclose(f);
+    }
+  }
   stats_ = RunStats{};
   stats_.launches = 1;
   cur_ = d.levels & 1;
@@ -574,6 +607,7 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     prepare(ph);  // tile-shape tuning cannot run inside the capture
     PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
     upload_rows(host_in, rb, in_r0, in_r1, cs_);
+    if (opt_.upload_event) ev_uploaded_.record(cs_);  // an event record node: the upload is done
     if (zone_first) {
       transport_->exchange(*this, lay_.halo, cs_);  // stream order: after the upload, before the launches
       ++stats_.exchanges;
@@ -647,6 +681,10 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
     // no split launches.  With it, each slot's exchanges run on the slot's
     // own communication stream beside the interior launch.
     o.overlap = slot_comm && opt.overlap;
+    // PCONV_STAGGER=0 (A/B): every slot of a burst uploads at once
+    const char* st = std::getenv("PCONV_STAGGER");
+    stagger_ = step_graphs && !(st && st[0] == '0');
+    o.upload_event = stagger_;
     // Slot streams on dedicated hardware queues: a stream created with a CU
     // mask (all CUs) gets its own HSA queue instead of one from the
     // runtime's round-robin pool.  From the pool, 4 slot streams landed on
@@ -684,6 +722,7 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
       d2h_ = Stream::create(0);
       ev_head_ = Event::create();
       h2d_wait_ = Event::create();
+      head_up_ = Event::create();
     }
     used_.assign(slots, false);
     // PCONV_WAVE_ALL=1 (A/B, with stream_chunks -1): every image a wave
@@ -774,11 +813,17 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   }
   if (graphs_) {
     PCONV_CHECK(trace_ev_.empty(), "pipeline trace needs directly issued images (graph capture off)");
+    if (idle_) {
+      burst_ = 0;
+      last_upload_ = nullptr;
+    }
+    const int pos = burst_++;
     const bool wave = e.options().stream_chunks < 0;
     if (wave && (idle_ || wave_all_) && e.wave_able(reps, in_r0, in_r1)) {
       // Wave image: the whole step is ONE persistent launch on the slot's own
       // stream (stream order covers the frames' earlier and later graphs).
       e.enqueue_wave(host_in, in_r0, in_r1, host_out, reps, e.compute_stream());
+      last_upload_ = nullptr;  // its loads are inside the launch: nothing to stagger on
       idle_ = false;
       used_[k] = true;
       ++count_;
@@ -798,6 +843,8 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
         h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
         h2d_wait_.wait_on(h2d_.get());
         e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, h2d_.get(), d2h_.get());
+        head_up_.record(h2d_.get());  // every chunk upload issued first: all of them done
+        last_upload_ = &head_up_;
         ev_head_.record(d2h_.get());
         ev_head_.wait_on(e.compute_stream());
         idle_ = false;
@@ -806,7 +853,16 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
         return;
       }
     }
+    if (stagger_ && pos > 0 && pos < slots() && last_upload_) {
+      // Head of a burst: start this upload when the previous image's is done
+      // (one cross-stream wait per image, first `slots` images only).  All
+      // slots uploading at once would split the link three ways and move the
+      // slots in lockstep — no download beside an upload until the whole
+      // first group is in (the driver's 20-image window pays that).
+      last_upload_->wait_on(e.compute_stream());
+    }
     e.process_graph(host_in, in_r0, in_r1, host_out, reps);
+    last_upload_ = stagger_ ? &e.upload_event() : nullptr;
     idle_ = false;
     used_[k] = true;
     ++count_;
