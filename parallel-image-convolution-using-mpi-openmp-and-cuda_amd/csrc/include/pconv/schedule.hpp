@@ -160,8 +160,11 @@ struct WavePlan {
 // col_groups[j] (j = 1..L; [0] ignored): column groups of level j's tiles.
 // tile_rows: rows of one tile, at most what one workgroup tile computes at
 // the level with the most steps.
+// load_lead: loads take their tickets this many ranks before the level
+// tiles that first need them (more uploads in flight early).
 WavePlan plan_wave(const std::vector<Phase>& plan, int64_t in_lo, int64_t in_hi, int64_t owned_rows,
-                   int tile_rows, const std::vector<int>& col_groups, int load_parts, int store_parts);
+                   int tile_rows, const std::vector<int>& col_groups, int load_parts, int store_parts,
+                   int load_lead = 2);
 // Throws unless every dependency of every task has all its arrivals earlier
 // in ticket order (tests and the launcher's debug check).
 void check_wave_order(const WavePlan& wp);

@@ -7,7 +7,7 @@
 // three across streams but pays 15-22 us per cross-stream hand-off.  Here the
 // workgroups of one resident grid take tasks in ticket order:
 //   * load: host rows -> frame 0 (16-byte loads straight from pinned host
-//     memory over PCIe, 8 in flight per lane);
+//     memory over PCIe, 16 in flight per lane);
 //   * level tile: one SWAR temporal tile (the k_swar_pf tile of
 //     stencil_swar.hip: 4-byte lanes, buffer-op loads with the range check
 //     doing the zero padding, `steps` repetitions in registers with LDS
@@ -42,6 +42,9 @@ namespace pconv {
 namespace {
 
 typedef __attribute__((address_space(1))) uint32_t gu32;
+// A native 16-byte vector (HIP's uint4 is a struct: an array of them is not
+// promoted to registers and went through scratch).
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
 // Shared words are accessed as GLOBAL (not flat) agent-scope atomics.
 __device__ __forceinline__ gu32* gptr(const uint32_t* p) { return (gu32*)(const_cast<uint32_t*>(p)); }
@@ -51,46 +54,42 @@ __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
 }
 
 // Rows [a, b) of `row_bytes` bytes from src (pitch sp) to dst (pitch dp), by
-// the whole workgroup: one row per wave at a time, 16-byte granules (4-byte
-// when the rows are not 16-byte aligned), up to 8 loads in flight per lane.
+// the whole workgroup over the flattened (row, granule) space: 16-byte
+// granules (4-byte when the rows are not 16-byte aligned), U loads in flight
+// per lane before the first store — a PCIe read from pinned host memory
+// takes microseconds, so the bytes in flight set the rate (the first form,
+// one row per wave, ran at 2-3 GB/s per workgroup: profiles/r04/wave2/).
+template <int U, typename T>
+__device__ __forceinline__ void copy_flat(const uint8_t* src, int64_t sp, uint8_t* dst, int64_t dp, int a, int b,
+                                          int g) {
+  const int n = (b - a) * g;
+  const int nt = static_cast<int>(blockDim.x);
+  for (int i0 = static_cast<int>(threadIdx.x); i0 < n; i0 += nt * U) {
+    // Indices past the end are clamped to the last granule: those lanes load
+    // and store it again (the same bytes to the same place), so neither loop
+    // branches and the U values stay in registers.
+    T v[U];
+    int r[U], c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u * nt, n - 1);
+      r[u] = i / g;
+      c[u] = i - r[u] * g;
+      v[u] = reinterpret_cast<const T*>(src + static_cast<int64_t>(a + r[u]) * sp)[c[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) reinterpret_cast<T*>(dst + static_cast<int64_t>(a + r[u]) * dp)[c[u]] = v[u];
+  }
+}
+
 __device__ __forceinline__ void copy_rows(const uint8_t* src, int64_t sp, uint8_t* dst, int64_t dp, int a, int b,
-                                          int row_bytes, int nwaves) {
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  constexpr int U = 8;
+                                          int row_bytes) {
   const bool wide = (row_bytes % 16 == 0) && (sp % 16 == 0) && (dp % 16 == 0) &&
                     (reinterpret_cast<uintptr_t>(src) % 16 == 0) && (reinterpret_cast<uintptr_t>(dst) % 16 == 0);
-  if (wide) {
-    const int g = row_bytes / 16;
-    for (int r = a + w; r < b; r += nwaves) {
-      const uint4* s = reinterpret_cast<const uint4*>(src + static_cast<int64_t>(r) * sp);
-      uint4* d = reinterpret_cast<uint4*>(dst + static_cast<int64_t>(r) * dp);
-      for (int c0 = lane; c0 < g; c0 += 64 * U) {
-        uint4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (c0 + 64 * u < g) v[u] = s[c0 + 64 * u];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (c0 + 64 * u < g) d[c0 + 64 * u] = v[u];
-      }
-    }
-  } else {
-    const int g = row_bytes / 4;  // the wave path requires row_bytes % 4 == 0
-    for (int r = a + w; r < b; r += nwaves) {
-      const uint32_t* s = reinterpret_cast<const uint32_t*>(src + static_cast<int64_t>(r) * sp);
-      uint32_t* d = reinterpret_cast<uint32_t*>(dst + static_cast<int64_t>(r) * dp);
-      for (int c0 = lane; c0 < g; c0 += 64 * U) {
-        uint32_t v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (c0 + 64 * u < g) v[u] = s[c0 + 64 * u];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (c0 + 64 * u < g) d[c0 + 64 * u] = v[u];
-      }
-    }
-  }
+  if (wide)
+    copy_flat<8, v4u32>(src, sp, dst, dp, a, b, row_bytes / 16);
+  else
+    copy_flat<16, uint32_t>(src, sp, dst, dp, a, b, row_bytes / 4);  // the wave path requires row_bytes % 4 == 0
 }
 
 // One tile of k_swar_pf (stencil_swar.hip) as a device function: output rows
@@ -234,14 +233,14 @@ __global__ __launch_bounds__(64 * NW) void k_wave(WaveArgs A) {
     if (!sh[1]) break;  // uniform: a dependency never completed
     if (k.kind == 0) {
       copy_rows(A.host_in - static_cast<int64_t>(A.in_r0) * A.row_bytes, A.row_bytes, A.frame0, A.pitch, k.a, k.b,
-                A.row_bytes, NW);
+                A.row_bytes);
     } else if (k.kind == 1) {
       const int s = A.lv[k.level].steps;
       const uint8_t* src = (k.level - 1) & 1 ? A.frame1 : A.frame0;
       uint8_t* dst = k.level & 1 ? A.frame1 : A.frame0;
       wave_tile<CH, M, NW, ALT>(src, dst, A.pitch, A.row_bytes, k.a, k.b, s, A.g_row0, A.height, k.part, lds);
     } else {
-      copy_rows(A.levels & 1 ? A.frame1 : A.frame0, A.pitch, A.host_out, A.row_bytes, k.a, k.b, A.row_bytes, NW);
+      copy_rows(A.levels & 1 ? A.frame1 : A.frame0, A.pitch, A.host_out, A.row_bytes, k.a, k.b, A.row_bytes);
     }
     if (k.kind != 2) {
       // publish: every wave's stores drained, then one release and the arrival

@@ -466,8 +466,12 @@ const BandEngine::WaveDev& BandEngine::wave_dev(int reps, int64_t in_r0, int64_t
   for (const auto& p : ph) smax = std::max(smax, p.steps);
   std::vector<int> groups(ph.size() + 1, 0);
   for (size_t j = 0; j < ph.size(); ++j) groups[j + 1] = wave_col_groups(geom_.ch(), ph[j].steps, lay_.row_bytes);
-  const WavePlan wp = plan_wave(ph, in_r0, in_r1, band_.rows, wave_tile_rows(smax), groups, kWaveLoadParts,
-                                kWaveStoreParts);
+  // A/B knobs: PCONV_WAVE_PARTS (row parts per load / store tile), PCONV_WAVE_LEAD
+  const char* pe = std::getenv("PCONV_WAVE_PARTS");
+  const char* le = std::getenv("PCONV_WAVE_LEAD");
+  const int parts = pe ? std::max(1, std::atoi(pe)) : kWaveLoadParts;
+  const WavePlan wp = plan_wave(ph, in_r0, in_r1, band_.rows, wave_tile_rows(smax), groups, parts,
+                                pe ? parts : kWaveStoreParts, le ? std::atoi(le) : 2);
   WaveDev d;
   d.ntasks = static_cast<int>(wp.tasks.size());
   d.levels = wp.levels;

@@ -145,7 +145,7 @@ int64_t floor_div(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1)
 }  // namespace
 
 WavePlan plan_wave(const std::vector<Phase>& plan, int64_t in_lo, int64_t in_hi, int64_t owned_rows, int tile_rows,
-                   const std::vector<int>& col_groups, int load_parts, int store_parts) {
+                   const std::vector<int>& col_groups, int load_parts, int store_parts, int load_lead) {
   PCONV_CHECK(streamable(plan), "plan_wave: the plan must be exchange-free with one launch per phase");
   PCONV_CHECK(in_lo <= 0 && in_hi >= owned_rows && in_lo < in_hi, "plan_wave: input rows must cover the band");
   PCONV_CHECK(tile_rows >= 1 && load_parts >= 1 && store_parts >= 1, "plan_wave: bad tiling");
@@ -195,7 +195,7 @@ WavePlan plan_wave(const std::vector<Phase>& plan, int64_t in_lo, int64_t in_hi,
   };
   std::vector<Keyed> all;
   std::vector<std::vector<int64_t>> rank(L + 1);
-  constexpr int64_t kLoadLead = 2;  // loads take their tickets this many ranks early
+  const int64_t kLoadLead = std::max(0, load_lead);  // loads take their tickets this many ranks early
   // rows of a tile split into `parts` row parts (empty parts dropped)
   auto parts_of = [](int64_t a, int64_t b, int parts, int p, int64_t& pa, int64_t& pb) {
     pa = a + (b - a) * p / parts;
