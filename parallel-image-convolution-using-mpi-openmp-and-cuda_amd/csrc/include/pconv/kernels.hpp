@@ -103,13 +103,16 @@ void launch_fill_zero(uint8_t* p, int64_t bytes, hipStream_t stream);
 // task list from schedule.hpp plan_wave, gaussian only).
 struct WaveTask;
 struct WaveLaunch {
-  const WaveTask* tasks = nullptr;  // device copy of WavePlan::tasks (ticket order)
-  int ntasks = 0;
+  // device copy of WavePlan::tasks partitioned by kind — loads, level tiles,
+  // stores — each part in ticket order
+  const WaveTask* tasks = nullptr;
+  int nload = 0, ncomp = 0, nstore = 0;
+  int loaders = 0, storers = 0;     // workgroups dedicated to loads / stores (0: grid / 8 each)
   int levels = 0;                   // L
   int channels = 1;
   const int* levels_dev = nullptr;  // device int4 per level 0..L: {steps, arrivals, counter_base, 0}
-  uint32_t* ctl = nullptr;          // zeroed by every launch: [0] ticket, [1] abort, [4..] tile counters
-  int64_t ctl_bytes = 0;            // a multiple of 16
+  uint32_t* ctl = nullptr;          // zeroed by every launch: 8 control words (tickets, abort), then tile counters
+  int64_t ctl_bytes = 0;            // a multiple of 16, >= 32 + 4 x counters
   uint32_t* err = nullptr;          // pinned host word, set to 1 when a wait timed out
   const uint8_t* host_in = nullptr; // pinned, input rows [in_r0, in_r1) contiguous
   int64_t in_r0 = 0;

@@ -167,10 +167,11 @@ struct WaveLevelDev {
 };
 
 struct WaveArgs {
-  const WaveTask* tasks;
-  int ntasks;
+  const WaveTask* tasks;   // [loads | level tiles | stores], each part in ticket order
+  int nload, ncomp, nstore;
+  int loaders, storers;    // workgroups dedicated to loads / stores (the first claimers of a role ticket)
   int levels;
-  uint32_t* ctl;  // [0] ticket, [1] abort; counters from ctl + 4
+  uint32_t* ctl;  // [0] level-tile ticket, [1] abort, [2] role ticket, [3] load ticket, [4] store ticket; counters from ctl + 8
   const WaveLevelDev* lv;
   const uint8_t* host_in;  // row r of the input at host_in + (r - in_r0) * row_bytes
   int in_r0;
@@ -184,22 +185,39 @@ struct WaveArgs {
   uint64_t* trace;         // nullable: per task {claimed, deps met, done, workgroup | xcc << 32} (wall clock)
 };
 
+// Roles: the first `loaders` workgroups to start stream the input (no
+// dependencies: uploads run at the link's rate whatever the levels are
+// doing — one CU keeps only a few KB of PCIe reads in flight, ~2 GB/s, so the
+// uploads need many CUs at once: profiles/r04/wave3/), the next `storers`
+// stream finished rows out, every other workgroup takes level tiles.  Roles
+// come from a ticket taken when the workgroup starts, so every loader is
+// running: level tiles wait only on loads and earlier level tiles, stores
+// only on level tiles — no cycle, whatever the residency.
 template <int CH, int M, int NW, bool ALT>
 __global__ __launch_bounds__(64 * NW) void k_wave(WaveArgs A) {
   __shared__ uint4 lds[2][NW][2][1][64];
-  __shared__ int sh[2];
+  __shared__ int sh[3];
   const int tid = threadIdx.x;
-  uint32_t* counters = A.ctl + 4;
+  uint32_t* counters = A.ctl + 8;
+  if (tid == 0) {
+    const int r = static_cast<int>(__hip_atomic_fetch_add(gptr(A.ctl + 2), 1u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT));
+    sh[2] = r < A.loaders ? 0 : r < A.loaders + A.storers ? 2 : 1;
+  }
+  __syncthreads();
+  const int role = sh[2];
+  const int base = role == 0 ? 0 : role == 1 ? A.nload : A.nload + A.ncomp;
+  const int count = role == 0 ? A.nload : role == 1 ? A.ncomp : A.nstore;
+  uint32_t* ticket = A.ctl + (role == 0 ? 3 : role == 1 ? 0 : 4);
   while (true) {
     if (tid == 0) {
-      int t = static_cast<int>(__hip_atomic_fetch_add(gptr(A.ctl), 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT));
-      if (ld_agent(A.ctl + 1) != 0) t = A.ntasks;  // another workgroup gave up: drain
+      int t = static_cast<int>(__hip_atomic_fetch_add(gptr(ticket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (ld_agent(A.ctl + 1) != 0) t = count;  // another workgroup gave up: drain
       sh[0] = t;
     }
     __syncthreads();
-    const int ti = sh[0];
-    if (ti >= A.ntasks) break;  // uniform
+    if (sh[0] >= count) break;  // uniform
+    const int ti = base + sh[0];
     const WaveTask k = A.tasks[ti];
     uint64_t tr_claim = 0;
     if (A.trace && tid == 0) tr_claim = static_cast<uint64_t>(wall_clock64());
@@ -301,14 +319,22 @@ int wave_col_groups(int channels, int steps, int64_t row_bytes) {
 }
 
 void launch_wave_image(const WaveLaunch& w, hipStream_t s) {
-  PCONV_CHECK(w.tasks && w.levels_dev && w.ctl && w.err && w.frame0 && w.frame1 && w.host_in && w.host_out,
+  PCONV_CHECK(w.ctl_bytes >= 32 && w.tasks && w.levels_dev && w.ctl && w.err && w.frame0 && w.frame1 && w.host_in && w.host_out,
               "wave launch: missing buffers");
   PCONV_CHECK(w.row_bytes % 4 == 0 && w.pitch % 16 == 0, "wave launch: rows must be whole dwords");
-  PCONV_CHECK(w.ntasks > 0 && w.levels >= 1, "wave launch: empty plan");
+  PCONV_CHECK(w.nload > 0 && w.ncomp > 0 && w.nstore > 0 && w.levels >= 1, "wave launch: empty plan");
   PCONV_HIP_CHECK(hipMemsetAsync(w.ctl, 0, static_cast<size_t>(w.ctl_bytes), s));
+  const void* fn = w.channels == 1 ? wave_fn<1>() : w.channels == 3 ? wave_fn<3>() : wave_fn<4>();
+  int grid = std::min(w.nload + w.ncomp + w.nstore, wave_resident(fn));
+  if (w.max_workgroups > 0) grid = std::min(grid, w.max_workgroups);
+  grid = std::max(grid, 3);  // a loader, a storer and a level-tile workgroup at least
   WaveArgs A;
   A.tasks = w.tasks;
-  A.ntasks = w.ntasks;
+  A.nload = w.nload;
+  A.ncomp = w.ncomp;
+  A.nstore = w.nstore;
+  A.loaders = std::max(1, std::min(w.loaders > 0 ? w.loaders : grid / 8, (grid - 1) / 2));
+  A.storers = std::max(1, std::min(w.storers > 0 ? w.storers : grid / 8, grid - 1 - A.loaders));
   A.levels = w.levels;
   A.ctl = w.ctl;
   A.lv = reinterpret_cast<const WaveLevelDev*>(w.levels_dev);
@@ -325,9 +351,6 @@ void launch_wave_image(const WaveLaunch& w, hipStream_t s) {
   A.err = w.err;
   A.poll_sleep = std::max(1, w.poll_sleep);
   A.trace = w.trace;
-  const void* fn = w.channels == 1 ? wave_fn<1>() : w.channels == 3 ? wave_fn<3>() : wave_fn<4>();
-  int grid = std::min(w.ntasks, wave_resident(fn));
-  if (w.max_workgroups > 0) grid = std::min(grid, w.max_workgroups);
   const dim3 g(static_cast<unsigned>(std::max(1, grid))), b(64 * kWaveNW);
   switch (w.channels) {
     case 1: k_wave<1, kWaveM, kWaveNW, true><<<g, b, 0, s>>>(A); break;

@@ -475,8 +475,15 @@ const BandEngine::WaveDev& BandEngine::wave_dev(int reps, int64_t in_r0, int64_t
   WaveDev d;
   d.ntasks = static_cast<int>(wp.tasks.size());
   d.levels = wp.levels;
-  d.tasks = DeviceBuffer(wp.tasks.size() * sizeof(WaveTask));
-  PCONV_HIP_CHECK(hipMemcpy(d.tasks.data(), wp.tasks.data(), wp.tasks.size() * sizeof(WaveTask), hipMemcpyHostToDevice));
+  // loads | level tiles | stores, each in ticket order (the kernel's roles)
+  std::vector<WaveTask> part;
+  part.reserve(wp.tasks.size());
+  for (int kind = 0; kind < 3; ++kind)
+    for (const auto& k : wp.tasks)
+      if (k.kind == kind) part.push_back(k);
+  for (const auto& k : wp.tasks) (k.kind == 0 ? d.nload : k.kind == 1 ? d.ncomp : d.nstore) += 1;
+  d.tasks = DeviceBuffer(part.size() * sizeof(WaveTask));
+  PCONV_HIP_CHECK(hipMemcpy(d.tasks.data(), part.data(), part.size() * sizeof(WaveTask), hipMemcpyHostToDevice));
   std::vector<int> table(4 * (wp.levels + 1), 0);
   for (int j = 0; j <= wp.levels; ++j) {
     table[4 * j] = wp.steps[j];
@@ -485,7 +492,7 @@ const BandEngine::WaveDev& BandEngine::wave_dev(int reps, int64_t in_r0, int64_t
   }
   d.table = DeviceBuffer(table.size() * sizeof(int));
   PCONV_HIP_CHECK(hipMemcpy(d.table.data(), table.data(), table.size() * sizeof(int), hipMemcpyHostToDevice));
-  const size_t ctl = static_cast<size_t>(16 + 4 * wp.counters + 15) / 16 * 16;
+  const size_t ctl = static_cast<size_t>(32 + 4 * wp.counters + 15) / 16 * 16;
   if (wave_ctl_.size() < ctl) {
     PCONV_HIP_CHECK(hipStreamSynchronize(cs_));  // an earlier wave may still use the old block
     wave_ctl_ = DeviceBuffer(ctl);
@@ -517,7 +524,11 @@ void BandEngine::enqueue_wave(const uint8_t* host_in, int64_t in_r0, int64_t in_
   const WaveDev& d = wave_dev(reps, in_r0, in_r1);
   WaveLaunch w;
   w.tasks = static_cast<const WaveTask*>(static_cast<const void*>(d.tasks.data()));
-  w.ntasks = d.ntasks;
+  w.nload = d.nload;
+  w.ncomp = d.ncomp;
+  w.nstore = d.nstore;
+  if (const char* v = std::getenv("PCONV_WAVE_LOADERS")) w.loaders = std::atoi(v);
+  if (const char* v = std::getenv("PCONV_WAVE_STORERS")) w.storers = std::atoi(v);
   w.levels = d.levels;
   w.channels = geom_.ch();
   w.levels_dev = static_cast<const int*>(static_cast<const void*>(d.table.data()));
