@@ -161,10 +161,13 @@ struct WavePlan {
 // tile_rows: rows of one tile, at most what one workgroup tile computes at
 // the level with the most steps.
 // load_lead: loads take their tickets this many ranks before the level
-// tiles that first need them (more uploads in flight early).
+// tiles that first need them (more uploads in flight early).  level_gap: a
+// level tile's rank is its latest dependency's plus this (1: tiles of all
+// levels interleave along the upload front; larger: the lower levels run
+// further ahead of the higher ones, closer to level after level).
 WavePlan plan_wave(const std::vector<Phase>& plan, int64_t in_lo, int64_t in_hi, int64_t owned_rows,
                    int tile_rows, const std::vector<int>& col_groups, int load_parts, int store_parts,
-                   int load_lead = 2);
+                   int load_lead = 2, int level_gap = 1);
 // Throws unless every dependency of every task has all its arrivals earlier
 // in ticket order (tests and the launcher's debug check).
 void check_wave_order(const WavePlan& wp);

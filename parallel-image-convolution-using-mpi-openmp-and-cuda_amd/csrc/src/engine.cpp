@@ -471,7 +471,8 @@ const BandEngine::WaveDev& BandEngine::wave_dev(int reps, int64_t in_r0, int64_t
   const char* le = std::getenv("PCONV_WAVE_LEAD");
   const int parts = pe ? std::max(1, std::atoi(pe)) : kWaveLoadParts;
   const WavePlan wp = plan_wave(ph, in_r0, in_r1, band_.rows, wave_tile_rows(smax), groups, parts,
-                                pe ? parts : kWaveStoreParts, le ? std::atoi(le) : 2);
+                                pe ? parts : kWaveStoreParts, le ? std::atoi(le) : 2,
+                                std::getenv("PCONV_WAVE_GAP") ? std::atoi(std::getenv("PCONV_WAVE_GAP")) : 1);
   WaveDev d;
   d.ntasks = static_cast<int>(wp.tasks.size());
   d.levels = wp.levels;

@@ -207,7 +207,7 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_readonly("tasks", &WavePlan::tasks);
   m.def("plan_wave", &plan_wave, py::arg("plan"), py::arg("in_lo"), py::arg("in_hi"), py::arg("owned_rows"),
         py::arg("tile_rows"), py::arg("col_groups"), py::arg("load_parts") = 1, py::arg("store_parts") = 1,
-        py::arg("load_lead") = 2);
+        py::arg("load_lead") = 2, py::arg("level_gap") = 1);
 
   // ---------------------------------------------------------------- CPU oracle
   m.def(

@@ -145,7 +145,8 @@ int64_t floor_div(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1)
 }  // namespace
 
 WavePlan plan_wave(const std::vector<Phase>& plan, int64_t in_lo, int64_t in_hi, int64_t owned_rows, int tile_rows,
-                   const std::vector<int>& col_groups, int load_parts, int store_parts, int load_lead) {
+                   const std::vector<int>& col_groups, int load_parts, int store_parts, int load_lead,
+                   int level_gap) {
   PCONV_CHECK(streamable(plan), "plan_wave: the plan must be exchange-free with one launch per phase");
   PCONV_CHECK(in_lo <= 0 && in_hi >= owned_rows && in_lo < in_hi, "plan_wave: input rows must cover the band");
   PCONV_CHECK(tile_rows >= 1 && load_parts >= 1 && store_parts >= 1, "plan_wave: bad tiling");
@@ -240,7 +241,7 @@ WavePlan plan_wave(const std::vector<Phase>& plan, int64_t in_lo, int64_t in_hi,
       r1 = std::min<int64_t>(r1, wp.tiles[j - 1] - 1);
       int64_t rk = 0;
       for (int64_t d = r0; d <= r1; ++d) rk = std::max(rk, rank[j - 1][d]);
-      rank[j][t] = rk + 1;
+      rank[j][t] = rk + std::max(1, level_gap);
       for (int g = 0; g < col_groups[j]; ++g) {
         WaveTask k;
         k.kind = 1;

@@ -25,12 +25,15 @@ from pconv.ops.reference import numpy_convolve
 from test_stream_plan import _plan, _step_rows
 
 
-def _wave(native, plan, in_lo, in_hi, rows, tile_rows, groups, lp, sp):
+def _wave(native, plan, in_lo, in_hi, rows, tile_rows, groups, lp, sp, gap=1):
     L = len(plan)
-    return native.plan_wave(plan, in_lo, in_hi, rows, tile_rows, [0] + [groups] * L, lp, sp)
+    return native.plan_wave(plan, in_lo, in_hi, rows, tile_rows, [0] + [groups] * L, lp, sp, 2, gap)
 
 
-def _replay(native, wp, band, height, row_bytes, ch, img_rows, in_lo, in_hi, workers, rng):
+def _replay(native, wp, band, height, row_bytes, ch, img_rows, in_lo, in_hi, workers, rng, roles=False):
+    """roles=False: one queue in ticket order; roles=True: the GPU kernel's
+    form — loads, level tiles and stores each in its own queue (in ticket
+    order), with at least one worker per queue."""
     L = wp.levels
     off = 64 - in_lo
     n = in_hi - in_lo + 128
@@ -85,14 +88,22 @@ def _replay(native, wp, band, height, row_bytes, ch, img_rows, in_lo, in_hi, wor
         if t.kind != 2:
             counters[t.level][t.tile] += 1
 
-    nxt, claimed = 0, []
-    while nxt < len(tasks) or claimed:
-        while len(claimed) < workers and nxt < len(tasks):
-            claimed.append(tasks[nxt])
-            nxt += 1
-        ok = [i for i, t in enumerate(claimed) if ready(t)]
+    if roles:
+        queues = [[t for t in tasks if t.kind == k] for k in (0, 1, 2)]
+        caps = [1 + workers // 8, max(1, workers), 1 + workers // 8]
+    else:
+        queues, caps = [list(tasks)], [workers]
+    nxt = [0] * len(queues)
+    claimed = [[] for _ in queues]
+    while any(nxt[q] < len(queues[q]) or claimed[q] for q in range(len(queues))):
+        for q in range(len(queues)):
+            while len(claimed[q]) < caps[q] and nxt[q] < len(queues[q]):
+                claimed[q].append(queues[q][nxt[q]])
+                nxt[q] += 1
+        ok = [(q, i) for q in range(len(queues)) for i, t in enumerate(claimed[q]) if ready(t)]
         assert ok, "deadlock: every claimed task waits"
-        run(claimed.pop(ok[int(rng.integers(0, len(ok)))]))
+        q, i = ok[int(rng.integers(0, len(ok)))]
+        run(claimed[q].pop(i))
     return out
 
 
@@ -128,10 +139,11 @@ def test_wave_plan_values(native, rng, ch, height, world, reps, fuse, tile_rows,
     rows = img.reshape(height, -1).astype(np.int32)
     for rank in range(world):
         band, plan, in_lo, in_hi, _ = _plan(native, height, world, rank, reps, fuse, world > 1)
-        wp = _wave(native, plan, in_lo, in_hi, band.rows, tile_rows, 2, 2, 2)
-        for _ in range(3):
-            got = _replay(native, wp, band, height, width * ch, ch, rows, in_lo, in_hi, workers, rng)
-            assert np.array_equal(got, ref[band.y0:band.y0 + band.rows]), rank
+        for gap, roles in ((1, False), (1, True), (4, True)):
+            wp = _wave(native, plan, in_lo, in_hi, band.rows, tile_rows, 2, 2, 2, gap)
+            for _ in range(2):
+                got = _replay(native, wp, band, height, width * ch, ch, rows, in_lo, in_hi, workers, rng, roles)
+                assert np.array_equal(got, ref[band.y0:band.y0 + band.rows]), (rank, gap, roles)
 
 
 def test_wave_plan_rejects_exchanges(native):
