@@ -124,6 +124,7 @@ struct WaveLaunch {
   int max_workgroups = 0;           // 0: the resident grid
   int poll_sleep = 2;               // s_sleep(8) (~0.2 us) between two polls of an incomplete counter
   uint64_t* trace = nullptr;        // device, 4 x u64 per task (claimed, ready, done, wg | xcc << 32); nullable
+  bool write_through = true;        // hand-offs by sc1 stores (no release fence per task) vs plain + release
 };
 void launch_wave_image(const WaveLaunch& w, hipStream_t stream);
 // Rows one wave-kernel tile computes at `max_steps` steps (the plan's tile_rows).

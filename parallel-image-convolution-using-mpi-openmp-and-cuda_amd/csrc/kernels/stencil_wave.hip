@@ -82,6 +82,35 @@ __device__ __forceinline__ void copy_flat(const uint8_t* src, int64_t sp, uint8_
   }
 }
 
+// Host rows -> frame rows [a, b) with buffer stores (sc1 = write-through
+// when `wt`: the published rows then need no release fence).
+template <int U>
+__device__ __forceinline__ void load_rows_to_frame(const uint8_t* src, int64_t sp, uint8_t* frame, int dp, int a,
+                                                   int b, int g, bool wt) {
+  const int n = (b - a) * g;
+  const int nt = static_cast<int>(blockDim.x);
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(frame + static_cast<int64_t>(a) * dp, 0, (b - a) * dp,
+                                                      0x00020000);
+  for (int i0 = static_cast<int>(threadIdx.x); i0 < n; i0 += nt * U) {
+    v4u32 v[U];
+    int r[U], c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u * nt, n - 1);
+      r[u] = i / g;
+      c[u] = i - r[u] * g;
+      v[u] = reinterpret_cast<const v4u32*>(src + static_cast<int64_t>(a + r[u]) * sp)[c[u]];
+    }
+    if (wt) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) __builtin_amdgcn_raw_buffer_store_b128(v[u], rsrc, r[u] * dp + c[u] * 16, 0, 16);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) __builtin_amdgcn_raw_buffer_store_b128(v[u], rsrc, r[u] * dp + c[u] * 16, 0, 0);
+    }
+  }
+}
+
 __device__ __forceinline__ void copy_rows(const uint8_t* src, int64_t sp, uint8_t* dst, int64_t dp, int a, int b,
                                           int row_bytes) {
   const bool wide = (row_bytes % 16 == 0) && (sp % 16 == 0) && (dp % 16 == 0) &&
@@ -97,7 +126,7 @@ __device__ __forceinline__ void copy_rows(const uint8_t* src, int64_t sp, uint8_
 template <int CH, int M, int NW, bool ALT>
 __device__ __forceinline__ void wave_tile(const uint8_t* src, uint8_t* dst, int pitch, int row_bytes, int r0, int r1,
                                           int steps, int g_row0, int height, int col,
-                                          uint4 (&lds)[2][NW][2][1][64]) {
+                                          uint4 (&lds)[2][NW][2][1][64], bool wt) {
   constexpr int LW = 4, NP = 4;
   constexpr u32 kOut = 0x80000000u;
   const int lane = threadIdx.x & 63;
@@ -154,8 +183,13 @@ __device__ __forceinline__ void wave_tile(const uint8_t* src, uint8_t* dst, int 
     const u32 ro = static_cast<u32>(fr - r0) * static_cast<u32>(pitch);
     u32 a, bb;
     pack<NP>(D[i], a, bb);
-    __builtin_amdgcn_raw_buffer_store_b32(a, drsrc, (rst && lane_in && xA >= 0) ? ro + xA : kOut, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b32(bb, drsrc, (rst && lane_in && xB >= 0) ? ro + xB : kOut, 0, 0);
+    if (wt) {  // sc1: write-through, no release fence needed before the arrival
+      __builtin_amdgcn_raw_buffer_store_b32(a, drsrc, (rst && lane_in && xA >= 0) ? ro + xA : kOut, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(bb, drsrc, (rst && lane_in && xB >= 0) ? ro + xB : kOut, 0, 16);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b32(a, drsrc, (rst && lane_in && xA >= 0) ? ro + xA : kOut, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(bb, drsrc, (rst && lane_in && xB >= 0) ? ro + xB : kOut, 0, 0);
+    }
   }
 }
 
@@ -183,6 +217,7 @@ struct WaveArgs {
   uint32_t* err;           // pinned host word: 1 = a wait timed out
   int poll_sleep;          // s_sleep(8) (~0.2 us) per unsuccessful poll
   uint64_t* trace;         // nullable: per task {claimed, deps met, done, workgroup | xcc << 32} (wall clock)
+  int write_through;       // published rows stored sc1 (no release fence) instead of plain + release
 };
 
 // Roles: the first `loaders` workgroups to start stream the input (no
@@ -250,22 +285,30 @@ __global__ __launch_bounds__(64 * NW) void k_wave(WaveArgs A) {
     __syncthreads();
     if (!sh[1]) break;  // uniform: a dependency never completed
     if (k.kind == 0) {
-      copy_rows(A.host_in - static_cast<int64_t>(A.in_r0) * A.row_bytes, A.row_bytes, A.frame0, A.pitch, k.a, k.b,
-                A.row_bytes);
+      const uint8_t* hin = A.host_in - static_cast<int64_t>(A.in_r0) * A.row_bytes;
+      if (A.row_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(hin) % 16 == 0)
+        load_rows_to_frame<8>(hin, A.row_bytes, A.frame0, A.pitch, k.a, k.b, A.row_bytes / 16, A.write_through != 0);
+      else
+        copy_rows(hin, A.row_bytes, A.frame0, A.pitch, k.a, k.b, A.row_bytes);
     } else if (k.kind == 1) {
       const int s = A.lv[k.level].steps;
       const uint8_t* src = (k.level - 1) & 1 ? A.frame1 : A.frame0;
       uint8_t* dst = k.level & 1 ? A.frame1 : A.frame0;
-      wave_tile<CH, M, NW, ALT>(src, dst, A.pitch, A.row_bytes, k.a, k.b, s, A.g_row0, A.height, k.part, lds);
+      wave_tile<CH, M, NW, ALT>(src, dst, A.pitch, A.row_bytes, k.a, k.b, s, A.g_row0, A.height, k.part, lds,
+                                A.write_through != 0);
     } else {
       copy_rows(A.levels & 1 ? A.frame1 : A.frame0, A.pitch, A.host_out, A.row_bytes, k.a, k.b, A.row_bytes);
     }
     if (k.kind != 2) {
-      // publish: every wave's stores drained, then one release and the arrival
+      // publish: every wave's stores drained, then (plain stores) one release,
+      // and the arrival.  Write-through (sc1) payload needs no release; the
+      // row copy of an unaligned input keeps plain stores and the release.
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const bool plain = !A.write_through ||
+                           (k.kind == 0 && !(A.row_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(A.host_in) % 16 == 0));
+        if (plain) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(gptr(counters + A.lv[k.level].counter_base + k.tile), 1u,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -351,6 +394,7 @@ void launch_wave_image(const WaveLaunch& w, hipStream_t s) {
   A.err = w.err;
   A.poll_sleep = std::max(1, w.poll_sleep);
   A.trace = w.trace;
+  A.write_through = w.write_through ? 1 : 0;
   const dim3 g(static_cast<unsigned>(std::max(1, grid))), b(64 * kWaveNW);
   switch (w.channels) {
     case 1: k_wave<1, kWaveM, kWaveNW, true><<<g, b, 0, s>>>(A); break;

@@ -548,6 +548,7 @@ void BandEngine::enqueue_wave(const uint8_t* host_in, int64_t in_r0, int64_t in_
   w.timeout_ticks = wave_timeout_ticks_;
   if (const char* g = std::getenv("PCONV_WAVE_GRID")) w.max_workgroups = std::atoi(g);
   if (const char* z = std::getenv("PCONV_WAVE_SLEEP")) w.poll_sleep = std::max(1, std::atoi(z));
+  if (const char* x = std::getenv("PCONV_WAVE_WT")) w.write_through = x[0] != '0';
   // PCONV_WAVE_TRACE=file: per-task wall-clock timeline of the next few wave
   // images appended to `file` as JSON lines (diagnostics: the host waits for
   // each traced image)

@@ -22,7 +22,7 @@ R="--width 8192 --height 8192 --channels rgb --reps 100"
 one g_s3 $G --steps 10 --warmup 4 --slots 3 --loop-steps 3 || exit 1
 one g_s4 $G --steps 10 --warmup 4 --slots 4 --loop-steps 3 || exit 1
 one g_s4_head4 $G --steps 10 --warmup 4 --slots 4 --stream-chunks 4 --loop-steps 3 || exit 1
-one g_s4_head8 $G --steps 10 --warmup 4 --slots 4 --stream-chunks 8 --loop-steps 3 || exit 1
+
 one r_s3 $R --steps 20 --warmup 4 --slots 3 --loop-steps 5 || exit 1
 one r_s4 $R --steps 20 --warmup 4 --slots 4 --loop-steps 5 || exit 1
 one r_s4_head4 $R --steps 20 --warmup 4 --slots 4 --stream-chunks 4 --loop-steps 5 || exit 1
