@@ -23,6 +23,11 @@ def main(path):
     for k in ("h2d", "reps", "d2h", "latency", "period"):
         vals = [r[k] for r in body if r[k] == r[k]]
         print(f"  median {k:8s} {us(statistics.median(vals))} us")
+    slots = sorted({r["slot"] for r in body})
+    if len(slots) > 1:
+        print("  per slot median reps / latency (us): " + ", ".join(
+            f"slot {k}: {us(statistics.median(r['reps'] for r in body if r['slot'] == k)).strip()} / "
+            f"{us(statistics.median(r['latency'] for r in body if r['slot'] == k)).strip()}" for k in slots))
     total = ms[-1][4] - ms[0][1]
     print(f"  wall {us(total)} us for {len(ms)} images = {us(total / len(ms))} us/image")
     print("  img slot   start     h2d    reps     d2h  (us)")
