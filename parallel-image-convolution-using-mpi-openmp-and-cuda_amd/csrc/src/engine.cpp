@@ -6,6 +6,7 @@
 #include "pconv/trace.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <thread>
 
@@ -553,9 +554,9 @@ void BandEngine::enqueue_wave(const uint8_t* host_in, int64_t in_r0, int64_t in_
   // images appended to `file` as JSON lines (diagnostics: the host waits for
   // each traced image)
   const char* trace_path = std::getenv("PCONV_WAVE_TRACE");
-  static int traced = 0;
+  static std::atomic<int> traced{0};
   DeviceBuffer trace;
-  if (trace_path && traced < 4) {
+  if (trace_path && traced.load() < 4) {
     trace = DeviceBuffer(static_cast<size_t>(d.ntasks) * 32);
     PCONV_HIP_CHECK(hipMemsetAsync(trace.data(), 0, trace.size(), stream ? stream : cs_));
     w.trace = static_cast<uint64_t*>(static_cast<void*>(trace.data()));
