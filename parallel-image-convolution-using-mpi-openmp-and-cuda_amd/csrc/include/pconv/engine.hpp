@@ -242,7 +242,8 @@ class BandEngine {
   // wave images: task list + per-level table on the device per (reps, in_r0, in_r1)
   struct WaveDev {
     int ntasks = 0, levels = 0;
-    int nload = 0, ncomp = 0, nstore = 0;
+    int nload = 0, ncomp = 0, nstore = 0, counters = 0;
+    bool dynamic = true;
     DeviceBuffer tasks, table;
   };
   std::map<std::tuple<int, int64_t, int64_t>, WaveDev> waves_;

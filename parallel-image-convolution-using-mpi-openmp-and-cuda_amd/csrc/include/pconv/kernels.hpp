@@ -110,7 +110,7 @@ struct WaveLaunch {
   int loaders = 0, storers = 0;     // workgroups dedicated to loads / stores (0: grid / 8 each)
   int levels = 0;                   // L
   int channels = 1;
-  const int* levels_dev = nullptr;  // device int4 per level 0..L: {steps, arrivals, counter_base, 0}
+  const int* levels_dev = nullptr;  // device, 8 ints per level 0..L: {steps, arrivals, counter_base, qbase, qcount}
   uint32_t* ctl = nullptr;          // zeroed by every launch: 8 control words (tickets, abort), then tile counters
   int64_t ctl_bytes = 0;            // a multiple of 16, >= 32 + 4 x counters
   uint32_t* err = nullptr;          // pinned host word, set to 1 when a wait timed out
@@ -125,6 +125,11 @@ struct WaveLaunch {
   int poll_sleep = 2;               // s_sleep(8) (~0.2 us) between two polls of an incomplete counter
   uint64_t* trace = nullptr;        // device, 4 x u64 per task (claimed, ready, done, wg | xcc << 32); nullable
   bool write_through = true;        // hand-offs by sc1 stores (no release fence per task) vs plain + release
+  // Level tiles claimed only when ready, deepest level first (the level-tile
+  // section grouped by level, levels_dev carrying each level's range); else
+  // one ticket queue in topological order.
+  bool dynamic = true;
+  int ncounters = 0;                // tile counters in ctl (the per-level heads follow them)
 };
 void launch_wave_image(const WaveLaunch& w, hipStream_t stream);
 // Rows one wave-kernel tile computes at `max_steps` steps (the plan's tile_rows).

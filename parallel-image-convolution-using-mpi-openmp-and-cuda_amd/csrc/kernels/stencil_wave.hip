@@ -195,10 +195,12 @@ __device__ __forceinline__ void wave_tile(const uint8_t* src, uint8_t* dst, int 
 
 struct WaveLevelDev {
   int steps;
-  int arrivals;
-  int counter_base;
-  int pad;
+  int arrivals;      // tasks per row tile of this level
+  int counter_base;  // first tile counter of this level
+  int qbase, qcount; // dynamic mode: this level's tasks in the level-tile section
+  int pad[3];
 };
+static_assert(sizeof(WaveLevelDev) == 32, "8 ints per level");
 
 struct WaveArgs {
   const WaveTask* tasks;   // [loads | level tiles | stores], each part in ticket order
@@ -218,7 +220,16 @@ struct WaveArgs {
   int poll_sleep;          // s_sleep(8) (~0.2 us) per unsuccessful poll
   uint64_t* trace;         // nullable: per task {claimed, deps met, done, workgroup | xcc << 32} (wall clock)
   int write_through;       // published rows stored sc1 (no release fence) instead of plain + release
+  int dyn;                 // level tiles claimed only when ready (per-level heads) instead of one ticket queue
+  int ncounters;           // tile counters; the per-level heads follow them
 };
+
+// Dependencies of `k` complete (relaxed agent loads; the caller acquires).
+__device__ __forceinline__ bool deps_ready(const WaveTask& k, const WaveLevelDev& d, const uint32_t* counters) {
+  for (int x = k.dep_lo; x <= k.dep_hi; ++x)
+    if (static_cast<int>(ld_agent(counters + d.counter_base + x)) < d.arrivals) return false;
+  return true;
+}
 
 // Roles: the first `loaders` workgroups to start stream the input (no
 // dependencies: uploads run at the link's rate whatever the levels are
@@ -244,9 +255,48 @@ __global__ __launch_bounds__(64 * NW) void k_wave(WaveArgs A) {
   const int base = role == 0 ? 0 : role == 1 ? A.nload : A.nload + A.ncomp;
   const int count = role == 0 ? A.nload : role == 1 ? A.ncomp : A.nstore;
   uint32_t* ticket = A.ctl + (role == 0 ? 3 : role == 1 ? 0 : 4);
+  uint32_t* heads = counters + A.ncounters;
+  const bool dyn = role == 1 && A.dyn;
   while (true) {
     if (tid == 0) {
-      int t = static_cast<int>(__hip_atomic_fetch_add(gptr(ticket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      int t = count;
+      if (dyn) {
+        // Dynamic: claim a level tile only once its dependencies are complete
+        // (deepest level first), so no workgroup holds a task while it
+        // waits; give up after the timeout without progress.
+        const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
+        while (true) {
+          bool left = false;
+          int got = -1;
+          for (int j = A.levels; j >= 1 && got < 0; --j) {
+            const WaveLevelDev d = A.lv[j];
+            uint32_t h = ld_agent(heads + j);
+            while (static_cast<int>(h) < d.qcount) {
+              left = true;
+              const WaveTask c = A.tasks[base + d.qbase + static_cast<int>(h)];
+              if (!deps_ready(c, A.lv[j - 1], counters)) break;
+              if (__hip_atomic_compare_exchange_strong(gptr(heads + j), &h, h + 1, __ATOMIC_RELAXED,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                got = d.qbase + static_cast<int>(h);
+                break;
+              }  // lost the race: h holds the new head, look at that task
+            }
+          }
+          if (got >= 0) {
+            t = got;
+            break;
+          }
+          if (!left) break;  // every level tile claimed: done
+          if (static_cast<uint64_t>(wall_clock64()) - t0 > A.timeout || ld_agent(A.ctl + 1) != 0) {
+            __hip_atomic_store(gptr(A.ctl + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          for (int z = 0; z < A.poll_sleep; ++z) __builtin_amdgcn_s_sleep(8);
+        }
+      } else {
+        t = static_cast<int>(__hip_atomic_fetch_add(gptr(ticket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
       if (ld_agent(A.ctl + 1) != 0) t = count;  // another workgroup gave up: drain
       sh[0] = t;
     }
@@ -395,6 +445,8 @@ void launch_wave_image(const WaveLaunch& w, hipStream_t s) {
   A.poll_sleep = std::max(1, w.poll_sleep);
   A.trace = w.trace;
   A.write_through = w.write_through ? 1 : 0;
+  A.dyn = w.dynamic ? 1 : 0;
+  A.ncounters = w.ncounters;
   const dim3 g(static_cast<unsigned>(std::max(1, grid))), b(64 * kWaveNW);
   switch (w.channels) {
     case 1: k_wave<1, kWaveM, kWaveNW, true><<<g, b, 0, s>>>(A); break;

@@ -477,24 +477,45 @@ const BandEngine::WaveDev& BandEngine::wave_dev(int reps, int64_t in_r0, int64_t
   WaveDev d;
   d.ntasks = static_cast<int>(wp.tasks.size());
   d.levels = wp.levels;
-  // loads | level tiles | stores, each in ticket order (the kernel's roles)
+  // loads | level tiles | stores, each in ticket order (the kernel's roles);
+  // dynamic mode (default; PCONV_WAVE_DYN=0: one ticket queue): the level
+  // tiles grouped by level, each level in tile order
+  const char* dy = std::getenv("PCONV_WAVE_DYN");
+  d.dynamic = !(dy && dy[0] == '0');
   std::vector<WaveTask> part;
   part.reserve(wp.tasks.size());
-  for (int kind = 0; kind < 3; ++kind)
+  for (const auto& k : wp.tasks)
+    if (k.kind == 0) part.push_back(k);
+  std::vector<int> qbase(wp.levels + 1, 0), qcount(wp.levels + 1, 0);
+  if (d.dynamic) {
+    const size_t c0 = part.size();
+    for (int j = 1; j <= wp.levels; ++j) {
+      qbase[j] = static_cast<int>(part.size() - c0);
+      for (const auto& k : wp.tasks)
+        if (k.kind == 1 && k.level == j) part.push_back(k);
+      qcount[j] = static_cast<int>(part.size() - c0) - qbase[j];
+    }
+  } else {
     for (const auto& k : wp.tasks)
-      if (k.kind == kind) part.push_back(k);
+      if (k.kind == 1) part.push_back(k);
+  }
+  for (const auto& k : wp.tasks)
+    if (k.kind == 2) part.push_back(k);
   for (const auto& k : wp.tasks) (k.kind == 0 ? d.nload : k.kind == 1 ? d.ncomp : d.nstore) += 1;
+  d.counters = wp.counters;
   d.tasks = DeviceBuffer(part.size() * sizeof(WaveTask));
   PCONV_HIP_CHECK(hipMemcpy(d.tasks.data(), part.data(), part.size() * sizeof(WaveTask), hipMemcpyHostToDevice));
-  std::vector<int> table(4 * (wp.levels + 1), 0);
+  std::vector<int> table(8 * (wp.levels + 1), 0);
   for (int j = 0; j <= wp.levels; ++j) {
-    table[4 * j] = wp.steps[j];
-    table[4 * j + 1] = wp.arrivals[j];
-    table[4 * j + 2] = wp.counter_base[j];
+    table[8 * j] = wp.steps[j];
+    table[8 * j + 1] = wp.arrivals[j];
+    table[8 * j + 2] = wp.counter_base[j];
+    table[8 * j + 3] = qbase[j];
+    table[8 * j + 4] = qcount[j];
   }
   d.table = DeviceBuffer(table.size() * sizeof(int));
   PCONV_HIP_CHECK(hipMemcpy(d.table.data(), table.data(), table.size() * sizeof(int), hipMemcpyHostToDevice));
-  const size_t ctl = static_cast<size_t>(32 + 4 * wp.counters + 15) / 16 * 16;
+  const size_t ctl = static_cast<size_t>(32 + 4 * (wp.counters + wp.levels + 1) + 15) / 16 * 16;
   if (wave_ctl_.size() < ctl) {
     PCONV_HIP_CHECK(hipStreamSynchronize(cs_));  // an earlier wave may still use the old block
     wave_ctl_ = DeviceBuffer(ctl);
@@ -529,6 +550,8 @@ void BandEngine::enqueue_wave(const uint8_t* host_in, int64_t in_r0, int64_t in_
   w.nload = d.nload;
   w.ncomp = d.ncomp;
   w.nstore = d.nstore;
+  w.dynamic = d.dynamic;
+  w.ncounters = d.counters;
   if (const char* v = std::getenv("PCONV_WAVE_LOADERS")) w.loaders = std::atoi(v);
   if (const char* v = std::getenv("PCONV_WAVE_STORERS")) w.storers = std::atoi(v);
   w.levels = d.levels;

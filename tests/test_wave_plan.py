@@ -30,10 +30,14 @@ def _wave(native, plan, in_lo, in_hi, rows, tile_rows, groups, lp, sp, gap=1):
     return native.plan_wave(plan, in_lo, in_hi, rows, tile_rows, [0] + [groups] * L, lp, sp, 2, gap)
 
 
-def _replay(native, wp, band, height, row_bytes, ch, img_rows, in_lo, in_hi, workers, rng, roles=False):
+def _replay(native, wp, band, height, row_bytes, ch, img_rows, in_lo, in_hi, workers, rng, roles=False,
+            dynamic=False):
     """roles=False: one queue in ticket order; roles=True: the GPU kernel's
     form — loads, level tiles and stores each in its own queue (in ticket
-    order), with at least one worker per queue."""
+    order), with at least one worker per queue; dynamic=True (with roles): a
+    level tile is claimed only once its dependencies are complete, from
+    per-level queues in tile order, deepest level first (the kernel's
+    default)."""
     L = wp.levels
     off = 64 - in_lo
     n = in_hi - in_lo + 128
@@ -88,6 +92,35 @@ def _replay(native, wp, band, height, row_bytes, ch, img_rows, in_lo, in_hi, wor
         if t.kind != 2:
             counters[t.level][t.tile] += 1
 
+    if dynamic:
+        loads = [t for t in tasks if t.kind == 0]
+        stores = [t for t in tasks if t.kind == 2]
+        levels = [[t for t in tasks if t.kind == 1 and t.level == j] for j in range(L + 1)]
+        head = [0] * (L + 1)
+        li = si = 0
+        pending_l, pending_s = [], []
+        while li < len(loads) or si < len(stores) or pending_l or pending_s or any(
+                head[j] < len(levels[j]) for j in range(1, L + 1)):
+            while len(pending_l) < 1 + workers // 8 and li < len(loads):
+                pending_l.append(loads[li])
+                li += 1
+            while len(pending_s) < 1 + workers // 8 and si < len(stores):
+                pending_s.append(stores[si])
+                si += 1
+            ready_levels = [j for j in range(L, 0, -1) if head[j] < len(levels[j]) and ready(levels[j][head[j]])]
+            choices = [("l", i) for i, t in enumerate(pending_l)] + \
+                      [("s", i) for i, t in enumerate(pending_s) if ready(t)] + \
+                      [("c", j) for j in ready_levels]
+            assert choices, "stalled: no load, ready store or ready level tile"
+            kind, i = choices[int(rng.integers(0, len(choices)))]
+            if kind == "l":
+                run(pending_l.pop(i))
+            elif kind == "s":
+                run(pending_s.pop(i))
+            else:
+                run(levels[i][head[i]])
+                head[i] += 1
+        return out
     if roles:
         queues = [[t for t in tasks if t.kind == k] for k in (0, 1, 2)]
         caps = [1 + workers // 8, max(1, workers), 1 + workers // 8]
@@ -139,11 +172,11 @@ def test_wave_plan_values(native, rng, ch, height, world, reps, fuse, tile_rows,
     rows = img.reshape(height, -1).astype(np.int32)
     for rank in range(world):
         band, plan, in_lo, in_hi, _ = _plan(native, height, world, rank, reps, fuse, world > 1)
-        for gap, roles in ((1, False), (1, True), (4, True)):
+        for gap, roles, dyn in ((1, False, False), (1, True, False), (4, True, False), (1, True, True)):
             wp = _wave(native, plan, in_lo, in_hi, band.rows, tile_rows, 2, 2, 2, gap)
             for _ in range(2):
-                got = _replay(native, wp, band, height, width * ch, ch, rows, in_lo, in_hi, workers, rng, roles)
-                assert np.array_equal(got, ref[band.y0:band.y0 + band.rows]), (rank, gap, roles)
+                got = _replay(native, wp, band, height, width * ch, ch, rows, in_lo, in_hi, workers, rng, roles, dyn)
+                assert np.array_equal(got, ref[band.y0:band.y0 + band.rows]), (rank, gap, roles, dyn)
 
 
 def test_wave_plan_rejects_exchanges(native):
