@@ -92,7 +92,9 @@ def parse():
     p.add_argument("--loop-steps", type=int, default=None, help="timed device-resident loops (default = --steps)")
     p.add_argument("--variant", default="auto")
     p.add_argument("--seed", type=int, default=1234)
-    p.add_argument("--slots", type=int, default=None, help="images in flight (default 3)")
+    p.add_argument("--slots", type=int, default=None,
+                   help="images in flight (default 4: slot streams on CU-masked queues; 4 beat 3 on the 8-way "
+                        "per-rank proxy in every halo mode and tie at N=1, profiles/r04/e2/, final_b/)")
     p.add_argument("--concurrent", choices=["auto", "on", "off"], default="off",
                    help="one compute stream per image in flight (default: one shared compute stream)")
     p.add_argument("--transport", choices=["rccl", "gloo-host"], default="rccl",
@@ -391,7 +393,7 @@ def run_native(a) -> int:
 def main():
     a = parse()
     if a.slots is None:
-        a.slots = 3
+        a.slots = 4
     if a.native:
         sys.exit(run_native(a))
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not a.emulate:

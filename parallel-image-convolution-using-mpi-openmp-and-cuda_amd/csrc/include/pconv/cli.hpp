@@ -55,7 +55,7 @@ struct CliConfig {
   // Serving bench (bench.py's step on the native stack): K timed images, each
   // H2D + reps + D2H, `slots` in flight; 0 = off (a normal run).
   int bench_steps = 0;
-  int slots = 3;
+  int slots = 4;
   int stream_chunks = 0;  // rows streamed within each image (EngineOptions::stream_chunks)
   // --bench --emulate W:R: time rank R of a W-way split alone in this process
   // (its band + pre-loaded ghost rows): the per-rank proxy of bench.py

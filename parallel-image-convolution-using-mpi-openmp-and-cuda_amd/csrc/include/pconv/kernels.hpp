@@ -127,8 +127,8 @@ struct WaveLaunch {
   bool write_through = true;        // hand-offs by sc1 stores (no release fence per task) vs plain + release
   // Level tiles claimed only when ready, deepest level first (the level-tile
   // section grouped by level, levels_dev carrying each level's range); else
-  // one ticket queue in topological order.
-  bool dynamic = true;
+  // (default) one ticket queue in topological order.
+  bool dynamic = false;
   int ncounters = 0;                // tile counters in ctl (the per-level heads follow them)
 };
 void launch_wave_image(const WaveLaunch& w, hipStream_t stream);

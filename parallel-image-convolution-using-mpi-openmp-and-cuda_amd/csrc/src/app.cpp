@@ -375,6 +375,8 @@ AppReport run_auto(const CliConfig& c) {
     omp_set_num_threads(c.threads);
   else
     (void)configure_cpu_threads();  // leaves a CPU for the bring-up thread
+#pragma omp parallel
+  { (void)omp_get_thread_num(); }  // the team starts here, not inside the timed first repetition
   uint8_t* src = fa.data();
   uint8_t* dst = fb.data();
   r.output = out_path(c);

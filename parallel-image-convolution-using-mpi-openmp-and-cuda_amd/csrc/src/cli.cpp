@@ -62,7 +62,7 @@ std::string help_text(const std::string& prog) {
          "                            kernels in a one-shot process, SDMA in a resident server)\n"
          "  --bench K                 serving bench: K timed images (H2D + reps + D2H each) per rank after\n"
          "                            --warmup untimed ones; prints bench.py's JSON line (native stack)\n"
-         "  --slots S                 --bench: images in flight (default 3)\n"
+         "  --slots S                 --bench: images in flight (default 4)\n"
          "  --stream-chunks C         --bench: rows of each image streamed in C chunks (0 = off; -1 = one\n"
          "                            persistent wave launch per image, stencil_wave.hip)\n"
          "  --emulate W:R             --bench: time rank R of a W-way split alone (per-rank proxy)\n"

@@ -473,15 +473,18 @@ const BandEngine::WaveDev& BandEngine::wave_dev(int reps, int64_t in_r0, int64_t
   const int parts = pe ? std::max(1, std::atoi(pe)) : kWaveLoadParts;
   const WavePlan wp = plan_wave(ph, in_r0, in_r1, band_.rows, wave_tile_rows(smax), groups, parts,
                                 pe ? parts : kWaveStoreParts, le ? std::atoi(le) : 2,
-                                std::getenv("PCONV_WAVE_GAP") ? std::atoi(std::getenv("PCONV_WAVE_GAP")) : 1);
+                                std::getenv("PCONV_WAVE_GAP") ? std::atoi(std::getenv("PCONV_WAVE_GAP")) : 8);
   WaveDev d;
   d.ntasks = static_cast<int>(wp.tasks.size());
   d.levels = wp.levels;
   // loads | level tiles | stores, each in ticket order (the kernel's roles);
-  // dynamic mode (default; PCONV_WAVE_DYN=0: one ticket queue): the level
-  // tiles grouped by level, each level in tile order
+  // PCONV_WAVE_DYN=1 (A/B): the level tiles grouped by level, each level in
+  // tile order, claimed only when ready — measured 6x slower than one ticket
+  // queue: every idle workgroup re-scans the per-level heads and their
+  // dependency counters and they contend on one compare-and-swap word per
+  // level (profiles/r04/wave7/)
   const char* dy = std::getenv("PCONV_WAVE_DYN");
-  d.dynamic = !(dy && dy[0] == '0');
+  d.dynamic = dy && dy[0] == '1';
   std::vector<WaveTask> part;
   part.reserve(wp.tasks.size());
   for (const auto& k : wp.tasks)
