@@ -381,18 +381,59 @@ AppReport run_auto(const CliConfig& c) {
   uint8_t* dst = fb.data();
   r.output = out_path(c);
   r.kernel = "cpu-omp";
-  const double l0 = wall_seconds();
   int done = 0;
   auto cpu_rep = [&] {
     cpu_step(f, g.channels, lay, src, dst, 0, g.height, CpuBackend::OpenMP);
     std::swap(src, dst);  // newest result is always `src`
     ++done;
   };
+  // Price the job: one repetition of a row sample (its output is scratch:
+  // the first real repetition rewrites every row of `dst`).
+  const int64_t sample = std::min<int64_t>(g.height, 256);
+  if (c.reps > 0) {
+    const double s0 = wall_seconds();
+    cpu_step(f, g.channels, lay, src, dst, 0, sample, CpuBackend::OpenMP);
+    r.cpu_rep_s = (wall_seconds() - s0) * static_cast<double>(g.height) / static_cast<double>(sample);
+  }
+  const double cpu_s = r.cpu_rep_s * c.reps;
+  const bool use_gpu = c.reps > 0 && cpu_s >= auto_gpu_min_s();
+  const char* ho = std::getenv("PCONV_AUTO_HANDOFF");
+  const bool handoff = use_gpu && ho && ho[0] == '1';
+  char est[96];
+  std::snprintf(est, sizeof(est), "cpu estimate %.4f s", cpu_s);
+  if (use_gpu && !handoff) {
+    // The GPU path on its own: measured faster than a CPU head start with a
+    // handoff once the job is worth a GPU (8192^2 RGB x100 0.23 vs 0.31 s,
+    // 32768^2 grey x200 0.74 vs 1.43 s: the CPU's work slows the bring-up,
+    // and the handoff adds a host copy into pinned memory; profiles/r04/).
+    try {
+      std::vector<uint8_t>().swap(fa);  // the GPU path stages the image itself
+      std::vector<uint8_t>().swap(fb);
+      const double pre = wall_seconds() - t0;
+      AppReport gr = run_gpu1(c, nullptr);
+      gr.e2e_s += pre;  // reading the image and pricing the job count too
+      gr.cpu_reps = 0;
+      gr.gpu_reps = c.reps;
+      gr.cpu_rep_s = r.cpu_rep_s;
+      gr.gpus = 1;
+      gr.auto_choice = std::string("gpu (") + est + ")";
+      gr.phases.insert(gr.phases.begin(), {"auto_read_and_price", pre});
+      return gr;
+    } catch (const std::exception& e) {
+      r.auto_choice = std::string("gpu failed (") + e.what() + "); cpu, " + est;
+      // back to the CPU: the frames again, from the image
+      fa.assign(static_cast<size_t>(lay.bytes()), 0);
+      fb.assign(static_cast<size_t>(lay.bytes()), 0);
+      load_rows(c, g, 0, g.height, fa.data() + lay.offset(0), lay.pitch);
+      src = fa.data();
+      dst = fb.data();
+    }
+  } else {
+    r.auto_choice = handoff ? std::string("gpu started beside the cpu, handoff (") + est + ")"
+                            : std::string("cpu only (job shorter than gpu start-up: ") + est + ")";
+  }
+  const double l0 = wall_seconds();
   if (c.reps > 0) cpu_rep();
-  r.cpu_rep_s = wall_seconds() - l0;
-  const double cpu_rest_s = r.cpu_rep_s * (c.reps - done);
-  const bool use_gpu = done < c.reps && cpu_rest_s >= auto_gpu_min_s();
-  r.auto_choice = use_gpu ? "gpu started after the first cpu repetition" : "cpu only (job shorter than gpu start-up)";
 
   // GPU bring-up on a helper thread; `ready` publishes the finished engine.
   struct Gpu {
@@ -405,7 +446,7 @@ AppReport run_auto(const CliConfig& c) {
   } gpu;
   const int device = 0;
   std::thread bring_up;
-  if (use_gpu) {
+  if (handoff) {
     bring_up = std::thread([&] {
       try {
         set_device(device);
@@ -437,7 +478,7 @@ AppReport run_auto(const CliConfig& c) {
     }
   } join_bring_up{bring_up};
   // CPU repetitions until the device is ready (or the job is done).
-  while (done < c.reps && !(use_gpu && gpu.state.load(std::memory_order_acquire) == 1)) cpu_rep();
+  while (done < c.reps && !(handoff && gpu.state.load(std::memory_order_acquire) == 1)) cpu_rep();
   r.cpu_reps = done;
   r.gpu_reps = 0;
   if (done < c.reps) {
@@ -472,7 +513,7 @@ AppReport run_auto(const CliConfig& c) {
     for (int64_t y = 0; y < g.height; ++y) std::memcpy(img.data() + y * rb, src + lay.offset(y), static_cast<size_t>(rb));
     write_image(r.output, g, img.data());
     pc.mark("write");
-    if (use_gpu) {
+    if (handoff) {
       // The CPU finished first: the bring-up still has to end before the
       // process may (its time is in e2e_s).
       bring_up.join();

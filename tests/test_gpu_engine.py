@@ -317,15 +317,16 @@ def test_copy_pair_floor(native):
 @pytest.mark.parametrize("typ,filt,w,h,reps", [("rgb", "gaussian", 1536, 1024, 2000), ("grey", "gaussian", 2048, 2048, 4000),
                                                ("rgb", "box", 1024, 768, 600)])
 def test_cli_auto_backend_hands_off_to_gpu(pconv_mod, tmp_path, typ, filt, w, h, reps):
-    """`--backend auto` with the GPU started at once (PCONV_AUTO_GPU_MIN_S=0):
-    the CPU (one thread here, so it is still busy when the device is up) runs
+    """`--backend auto` with the GPU brought up beside the CPU
+    (PCONV_AUTO_GPU_MIN_S=0, PCONV_AUTO_HANDOFF=1): the CPU (one thread here,
+    so it is still busy when the device is up) runs
     repetitions while the GPU comes up, then the newest CPU frame moves to the
     GPU, which runs the rest; the result equals the CPU oracle of all `reps`
     bit for bit whatever the handoff point.  (Jobs of ~1-2 s on one CPU
     thread: the GPU comes up within a few hundred ms.)"""
     from pconv.models.filters import get_filter
 
-    env = dict(os.environ, PCONV_AUTO_GPU_MIN_S="0")
+    env = dict(os.environ, PCONV_AUTO_GPU_MIN_S="0", PCONV_AUTO_HANDOFF="1")
     r = subprocess.run([CONV_BIN, "s.raw", str(w), str(h), str(reps), typ, "--synthetic", "11", "--backend", "auto",
                         "--threads", "1", "--filter", filt, "--json", "--quiet"], cwd=tmp_path, capture_output=True,
                        text=True, timeout=300, env=env)
@@ -339,3 +340,21 @@ def test_cli_auto_backend_hands_off_to_gpu(pconv_mod, tmp_path, typ, filt, w, h,
     pconv_mod.native.cpu_convolve(img.reshape(-1), ref.reshape(-1), w, h, typ, reps, get_filter(filt).to_native(),
                                   True, 0)
     assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("typ,filt,reps", [("rgb", "gaussian", 40), ("grey", "edge", 9)])
+def test_cli_auto_backend_gpu_path(pconv_mod, tmp_path, typ, filt, reps):
+    """`--backend auto` on a job priced above the GPU's start-up (forced with
+    PCONV_AUTO_GPU_MIN_S=0): the GPU path runs on its own, all repetitions on
+    the GPU, bit-exact with the oracle."""
+    w, h = 320, 200
+    env = dict(os.environ, PCONV_AUTO_GPU_MIN_S="0")
+    r = subprocess.run([CONV_BIN, "s.raw", str(w), str(h), str(reps), typ, "--synthetic", "3", "--backend", "auto",
+                        "--filter", filt, "--json", "--check", "--quiet"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    meta = json.loads(r.stdout.strip().splitlines()[-1])
+    assert meta["gpus"] == 1 and meta["cpu_reps"] == 0 and meta["gpu_reps"] == reps and meta["mismatches"] == 0
+    assert meta["auto_choice"].startswith("gpu (") and not meta["kernel"].startswith("cpu")
+    out = pconv_mod.read_raw(str(tmp_path / "blur_s.raw"), w, h, typ)
+    assert np.array_equal(out, pconv_mod.numpy_convolve(pconv_mod.synthetic_image(w, h, typ, seed=3), reps, filt))
