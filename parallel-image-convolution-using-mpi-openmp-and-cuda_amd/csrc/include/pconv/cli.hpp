@@ -17,8 +17,10 @@
 
 namespace pconv {
 
-// Auto (one-shot, 1 GPU): the CPU starts at once while the GPU comes up, the
-// GPU takes over the remaining repetitions (app.cpp run_auto).
+// Auto (one-shot, 1 GPU): the job is priced on the CPU from a row sample;
+// short jobs run on the CPU and never touch the GPU, the rest on the GPU
+// path alone (app.cpp run_auto; the CPU-head-start handoff is opt-in,
+// PCONV_AUTO_HANDOFF=1).
 enum class Backend { Hip, Cpu, Omp, Auto };
 enum class TimeFormat { Auto, Cuda, Mpi, Both };
 

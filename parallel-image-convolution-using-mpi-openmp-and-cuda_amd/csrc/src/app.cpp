@@ -333,24 +333,24 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   return r;
 }
 
-// ------------------------------------------------------- CPU head start + GPU
+// ------------------------------------------------------- CPU or GPU, priced
 // `--backend auto`, the one-shot form of the reference's cuda/main.c:20-49
 // run.  A cold process spends 50-190 ms bringing the GPU up (runtime,
 // context, first queue; BASELINE.md phase tables) before its first kernel,
 // while one repetition of a 1920x2520 RGB frame takes ~0.5 ms on the
-// node's CPUs.  So the CPU starts the repetitions at once (OpenMP, the
-// bit-exact oracle path), and:
-//   * after the first, timed repetition the rest of the job is priced on the
-//     CPU; below kAutoGpuMinS the GPU is never touched (no HIP call at all:
-//     no driver open, no teardown wait for the next process);
-//   * otherwise a helper thread brings the GPU up (context, code objects,
-//     queue, frames, pinned staging, one warm-up schedule) while the CPU
-//     keeps going; at the first repetition boundary after the device is
-//     ready the newest CPU frame is uploaded and the GPU runs the rest.
-// CPU and GPU repetitions are bit-identical step by step, so the handoff
-// point never shows in the output.  A failed GPU bring-up leaves the job on
-// the CPU (reported in auto_choice).
-// CPU time left after the first repetition below which the GPU is not
+// node's CPUs.  So the job is priced on the CPU first:
+//   * stage 1, a <= 256-row sample: above kAutoGpuMinS the GPU path runs the
+//     job alone (the host never holds the image twice);
+//   * stage 2, the whole frame on the host: the first repetition is real
+//     work and re-prices the job at memory speed; if the rest is still worth
+//     a GPU it goes there, otherwise the CPU finishes without any HIP call
+//     (no driver open, no teardown wait for the next process).
+// PCONV_AUTO_HANDOFF=1 instead brings the GPU up on a helper thread while
+// the CPU keeps going and hands it the newest frame at the first repetition
+// boundary after the device is ready (bit-exact at any point: CPU and GPU
+// repetitions are identical step by step; measured slower, see run notes
+// below).  A failed GPU bring-up leaves the job on the CPU (auto_choice).
+// CPU time of the job (or of its rest) below which the GPU is not
 // started (PCONV_AUTO_GPU_MIN_S overrides; 0 = always start it).
 constexpr double kAutoGpuMinS = 0.1;
 
@@ -368,72 +368,117 @@ AppReport run_auto(const CliConfig& c) {
   const Filter f = Filter::by_name(c.filter);
   const int64_t rb = g.row_bytes();
   const FrameLayout lay = FrameLayout::make(rb, g.height, 1);
-  std::vector<uint8_t> fa(static_cast<size_t>(lay.bytes()), 0), fb(static_cast<size_t>(lay.bytes()), 0);
-  load_rows(c, g, 0, g.height, fa.data() + lay.offset(0), lay.pitch);
-  pc.mark(c.synthetic ? "synthesize" : "read");
   if (c.threads > 0)
     omp_set_num_threads(c.threads);
   else
     (void)configure_cpu_threads();  // leaves a CPU for the bring-up thread
 #pragma omp parallel
-  { (void)omp_get_thread_num(); }  // the team starts here, not inside the timed first repetition
-  uint8_t* src = fa.data();
-  uint8_t* dst = fb.data();
+  { (void)omp_get_thread_num(); }  // the team starts here, not inside a timed step
   r.output = out_path(c);
   r.kernel = "cpu-omp";
+  const double thr = auto_gpu_min_s();
+  const char* ho = std::getenv("PCONV_AUTO_HANDOFF");
+  const bool handoff_env = ho && ho[0] == '1';
+  char est[128];
+
+  // Stage 1: price from the first rows only (a frame of <= 256 rows), so a
+  // job bound for the GPU never reads or allocates the whole image on the
+  // host twice.  The fastest of up to 3 trials (stopping once 3 ms are
+  // spent): one trial on a loaded host can be a barrier's scheduling delay.
+  // The sample stays in the CPU's caches, so it can only under-price a large
+  // frame: above the threshold the job is the GPU's for sure.
+  if (c.reps > 0) {
+    const int64_t sample = std::min<int64_t>(g.height, 256);
+    const FrameLayout sl = FrameLayout::make(rb, sample, 1);
+    std::vector<uint8_t> sa(static_cast<size_t>(sl.bytes()), 0), sb(static_cast<size_t>(sl.bytes()), 0);
+    load_rows(c, g, 0, sample, sa.data() + sl.offset(0), sl.pitch);
+    double best = 1e30, spent = 0;
+    for (int t = 0; t < 3 && spent < 3e-3; ++t) {
+      const double s0 = wall_seconds();
+      cpu_step(f, g.channels, sl, sa.data(), sb.data(), 0, sample, CpuBackend::OpenMP);
+      const double dt = wall_seconds() - s0;
+      best = std::min(best, dt);
+      spent += dt;
+    }
+    r.cpu_rep_s = best * static_cast<double>(g.height) / static_cast<double>(sample);
+  }
+  pc.mark("auto_price");
+  double cpu_s = r.cpu_rep_s * c.reps;
+  std::snprintf(est, sizeof(est), "cpu estimate %.4f s", cpu_s);
+
+  // The GPU path on its own: measured faster than a CPU head start with a
+  // handoff once the job is worth a GPU (8192^2 RGB x100 0.23 vs 0.31 s,
+  // 32768^2 grey x200 0.74 vs 1.43 s: the CPU's work slows the bring-up,
+  // and the handoff adds a host copy into pinned memory; profiles/r04/).
+  // Returns false (auto_choice says why) if the GPU cannot run the job.
+  AppReport gr;
+  auto gpu_alone = [&]() -> bool {
+    try {
+      const double pre = wall_seconds() - t0;
+      gr = run_gpu1(c, nullptr);
+      gr.e2e_s += pre;  // pricing the job counts too
+      gr.cpu_reps = 0;
+      gr.gpu_reps = c.reps;
+      gr.cpu_rep_s = r.cpu_rep_s;
+      gr.gpus = 1;
+      gr.auto_choice = std::string("gpu (") + est + ")";
+      gr.phases.insert(gr.phases.begin(), {"auto_price", pre});
+      return true;
+    } catch (const std::exception& e) {
+      r.auto_choice = std::string("gpu failed (") + e.what() + "); cpu, " + est;
+      return false;
+    }
+  };
+  bool gpu_failed = false;
+  if (c.reps > 0 && cpu_s >= thr && !handoff_env) {
+    if (gpu_alone()) return gr;
+    gpu_failed = true;
+  }
+
+  // Stage 2: the whole image on the host (the CPU runs the job, or hands it
+  // off); the first repetition is timed on the full frame and re-prices it.
+  std::vector<uint8_t> fa(static_cast<size_t>(lay.bytes()), 0), fb(static_cast<size_t>(lay.bytes()), 0);
+  load_rows(c, g, 0, g.height, fa.data() + lay.offset(0), lay.pitch);
+  pc.mark(c.synthetic ? "synthesize" : "read");
+  uint8_t* src = fa.data();
+  uint8_t* dst = fb.data();
   int done = 0;
   auto cpu_rep = [&] {
     cpu_step(f, g.channels, lay, src, dst, 0, g.height, CpuBackend::OpenMP);
     std::swap(src, dst);  // newest result is always `src`
     ++done;
   };
-  // Price the job: one repetition of a row sample (its output is scratch:
-  // the first real repetition rewrites every row of `dst`).
-  const int64_t sample = std::min<int64_t>(g.height, 256);
-  if (c.reps > 0) {
-    const double s0 = wall_seconds();
-    cpu_step(f, g.channels, lay, src, dst, 0, sample, CpuBackend::OpenMP);
-    r.cpu_rep_s = (wall_seconds() - s0) * static_cast<double>(g.height) / static_cast<double>(sample);
-  }
-  const double cpu_s = r.cpu_rep_s * c.reps;
-  const bool use_gpu = c.reps > 0 && cpu_s >= auto_gpu_min_s();
-  const char* ho = std::getenv("PCONV_AUTO_HANDOFF");
-  const bool handoff = use_gpu && ho && ho[0] == '1';
-  char est[96];
-  std::snprintf(est, sizeof(est), "cpu estimate %.4f s", cpu_s);
-  if (use_gpu && !handoff) {
-    // The GPU path on its own: measured faster than a CPU head start with a
-    // handoff once the job is worth a GPU (8192^2 RGB x100 0.23 vs 0.31 s,
-    // 32768^2 grey x200 0.74 vs 1.43 s: the CPU's work slows the bring-up,
-    // and the handoff adds a host copy into pinned memory; profiles/r04/).
-    try {
+  double l0 = wall_seconds();
+  if (c.reps > 0) cpu_rep();
+  if (c.reps > 0 && !gpu_failed) {
+    const double first = wall_seconds() - l0;
+    // Only up: a full frame past the caches runs at memory speed, which the
+    // sample does not see (8192^2 RGB: sample 1.0 ms a repetition, the frame
+    // 3.7 ms).
+    if (first > r.cpu_rep_s) {
+      r.cpu_rep_s = first;
+      cpu_s = first * c.reps;
+      std::snprintf(est, sizeof(est), "cpu estimate %.4f s from the first full repetition", cpu_s);
+    }
+    if (!handoff_env && first * (c.reps - 1) >= thr) {
       std::vector<uint8_t>().swap(fa);  // the GPU path stages the image itself
       std::vector<uint8_t>().swap(fb);
-      const double pre = wall_seconds() - t0;
-      AppReport gr = run_gpu1(c, nullptr);
-      gr.e2e_s += pre;  // reading the image and pricing the job count too
-      gr.cpu_reps = 0;
-      gr.gpu_reps = c.reps;
-      gr.cpu_rep_s = r.cpu_rep_s;
-      gr.gpus = 1;
-      gr.auto_choice = std::string("gpu (") + est + ")";
-      gr.phases.insert(gr.phases.begin(), {"auto_read_and_price", pre});
-      return gr;
-    } catch (const std::exception& e) {
-      r.auto_choice = std::string("gpu failed (") + e.what() + "); cpu, " + est;
-      // back to the CPU: the frames again, from the image
-      fa.assign(static_cast<size_t>(lay.bytes()), 0);
+      if (gpu_alone()) return gr;
+      gpu_failed = true;
+      fa.assign(static_cast<size_t>(lay.bytes()), 0);  // back to the CPU: the frames again
       fb.assign(static_cast<size_t>(lay.bytes()), 0);
       load_rows(c, g, 0, g.height, fa.data() + lay.offset(0), lay.pitch);
       src = fa.data();
       dst = fb.data();
+      done = 0;
+      l0 = wall_seconds();
+      cpu_rep();
     }
-  } else {
+  }
+  const bool handoff = handoff_env && !gpu_failed && cpu_s >= thr;
+  if (!gpu_failed)
     r.auto_choice = handoff ? std::string("gpu started beside the cpu, handoff (") + est + ")"
                             : std::string("cpu only (job shorter than gpu start-up: ") + est + ")";
-  }
-  const double l0 = wall_seconds();
-  if (c.reps > 0) cpu_rep();
 
   // GPU bring-up on a helper thread; `ready` publishes the finished engine.
   struct Gpu {

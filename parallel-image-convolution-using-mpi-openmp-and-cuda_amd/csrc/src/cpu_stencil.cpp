@@ -150,7 +150,11 @@ void step_rows(const Filter& f, const FrameLayout& lay, const uint8_t* src, uint
       row_float<CH>(f, a, b, c, o, n);
   };
   if (be == CpuBackend::OpenMP) {
-#pragma omp parallel for schedule(static)
+    // Below ~32 KiB of output a step is a few microseconds on one core: the
+    // team's fork/join costs as much, and on a loaded host a preempted team
+    // member stalls the barrier for a whole scheduler slice.
+    const bool team = (r1 - r0) * n >= (int64_t{32} << 10);
+#pragma omp parallel for schedule(static) if (team)
     for (int64_t r = r0; r < r1; ++r) body(r);
   } else {
     for (int64_t r = r0; r < r1; ++r) body(r);

@@ -5,7 +5,7 @@
 # `--backend hip`, back to back and with an idle gap before each process;
 # plus a handoff run on a job long enough for the GPU to take over.
 set -o pipefail
-OUT=gpurun_out/r04/auto
+OUT=${AUTO_OUT:-gpurun_out/r04/auto}
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1
 export TMPDIR=/tmp
@@ -16,7 +16,7 @@ $T --gap 1.0 --out $OUT/cuda_auto_idle.jsonl --extra --backend auto > $OUT/cuda_
 python tools/ref_tables.py report $OUT/cuda_auto.jsonl --md $OUT/cuda_auto.md > /dev/null && tail -3 $OUT/cuda_auto.md
 python tools/ref_tables.py report $OUT/cuda_hip.jsonl --md $OUT/cuda_hip.md > /dev/null && tail -3 $OUT/cuda_hip.md
 C=parallel-image-convolution-using-mpi-openmp-and-cuda_amd/bin/conv
-for j in "1920 2520 400 rgb" "8192 8192 100 rgb" "32768 32768 200 grey"; do
+for j in "1920 2520 400 rgb" "4096 4096 60 rgb" "8192 8192 100 rgb" "32768 32768 200 grey"; do
   set -- $j
   n=handoff_${1}x${2}_${4}_$3
   timeout -k 10 300 $C /tmp/x.raw $1 $2 $3 $4 --synthetic 7 --backend auto --json --quiet --out /tmp/o.raw > $OUT/$n.json 2> $OUT/$n.err || { echo "$n failed"; tail -5 $OUT/$n.err; exit 1; }
