@@ -86,6 +86,7 @@ struct RunStats {
   double wall_ms = 0;      // host wall time of the enqueue+sync
   int launches = 0;
   int exchanges = 0;
+  int host_store_launches = 0;  // launches that stored their rows straight into pinned host memory
 };
 
 class BandEngine {

@@ -397,16 +397,44 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
          hipMemcpyHostToDevice, up);
     if (up != cs_) up_evs_[c].record(up);
   }
+  // PCONV_STREAM_FUSED_D2H=1 (A/B): the final level's launches store their
+  // rows straight into `host_out` (the SWAR kernel's separate destination
+  // pitch), so no download copy and no launch -> D2H hop is left on the
+  // image's chain.  Only where every final-level launch writes owned rows.
+  const char* fv = std::getenv("PCONV_STREAM_FUSED_D2H");  // read per image: tests flip it
+  const bool fused_env = fv && fv[0] == '1';
+  bool fused = fused_env && host_out && filter_.binomial121 && rb % 4 == 0 &&
+               (opt_.variant == KernelVariant::Auto || opt_.variant == KernelVariant::Temporal);
+  uint8_t* dev_out = host_out;  // the device's address of the pinned output
+  if (fused) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, host_out) != hipSuccess || at.type != hipMemoryTypeHost || !at.devicePointer) {
+      (void)hipGetLastError();  // pageable memory: only a copy can reach it
+      fused = false;
+    } else {
+      dev_out = static_cast<uint8_t*>(at.devicePointer);
+    }
+  }
+  for (size_t c = 0; fused && c < nc; ++c)
+    for (size_t i = 0; i < sp.chunks[c].launches.size(); ++i)
+      if (sp.chunks[c].levels[i] == sp.levels &&
+          (sp.chunks[c].launches[i].lo < 0 || sp.chunks[c].launches[i].hi > band_.rows))
+        fused = false;
   bool pending = false;  // launches not yet covered by a download-side event
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     if (up != cs_) up_evs_[c].wait_on(cs_);
     for (size_t i = 0; i < ch.launches.size(); ++i) {
-      launch_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1, nullptr, 0),
+      const bool to_host = fused && ch.levels[i] == sp.levels;
+      launch_stencil(filter_, geom_.channels,
+                     make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1, to_host ? dev_out : nullptr,
+                                 to_host ? rb : 0),
                      cs_, opt_.variant);
       ++stats_.launches;
+      stats_.host_store_launches += to_host;
       pending = true;
     }
+    if (fused) continue;
     if (ch.down_hi > ch.down_lo && host_out && down != cs_) {
       dn_evs_[c].record(cs_);
       pending = false;
@@ -415,7 +443,7 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
   // `down` finishing must mean the whole image is done (the next image of
   // these frames waits on it), also when launches follow the last download.
   if (pending && down != cs_) dn_evs_[nc].record(cs_);
-  for (size_t c = 0; c < nc; ++c) {
+  for (size_t c = 0; c < nc && !fused; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     if (!(ch.down_hi > ch.down_lo && host_out)) continue;
     if (down != cs_) dn_evs_[c].wait_on(down);

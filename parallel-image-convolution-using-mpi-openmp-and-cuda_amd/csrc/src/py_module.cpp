@@ -430,7 +430,8 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_readonly("loop_ms", &RunStats::loop_ms)
       .def_readonly("wall_ms", &RunStats::wall_ms)
       .def_readonly("launches", &RunStats::launches)
-      .def_readonly("exchanges", &RunStats::exchanges);
+      .def_readonly("exchanges", &RunStats::exchanges)
+      .def_readonly("host_store_launches", &RunStats::host_store_launches);
 
   py::class_<HaloTransport, PyHaloTransport, std::shared_ptr<HaloTransport>>(m, "HaloTransport")
       .def(py::init<>())
