@@ -397,44 +397,16 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
          hipMemcpyHostToDevice, up);
     if (up != cs_) up_evs_[c].record(up);
   }
-  // PCONV_STREAM_FUSED_D2H=1 (A/B): the final level's launches store their
-  // rows straight into `host_out` (the SWAR kernel's separate destination
-  // pitch), so no download copy and no launch -> D2H hop is left on the
-  // image's chain.  Only where every final-level launch writes owned rows.
-  const char* fv = std::getenv("PCONV_STREAM_FUSED_D2H");  // read per image: tests flip it
-  const bool fused_env = fv && fv[0] == '1';
-  bool fused = fused_env && host_out && filter_.binomial121 && rb % 4 == 0 &&
-               (opt_.variant == KernelVariant::Auto || opt_.variant == KernelVariant::Temporal);
-  uint8_t* dev_out = host_out;  // the device's address of the pinned output
-  if (fused) {
-    hipPointerAttribute_t at{};
-    if (hipPointerGetAttributes(&at, host_out) != hipSuccess || at.type != hipMemoryTypeHost || !at.devicePointer) {
-      (void)hipGetLastError();  // pageable memory: only a copy can reach it
-      fused = false;
-    } else {
-      dev_out = static_cast<uint8_t*>(at.devicePointer);
-    }
-  }
-  for (size_t c = 0; fused && c < nc; ++c)
-    for (size_t i = 0; i < sp.chunks[c].launches.size(); ++i)
-      if (sp.chunks[c].levels[i] == sp.levels &&
-          (sp.chunks[c].launches[i].lo < 0 || sp.chunks[c].launches[i].hi > band_.rows))
-        fused = false;
   bool pending = false;  // launches not yet covered by a download-side event
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     if (up != cs_) up_evs_[c].wait_on(cs_);
     for (size_t i = 0; i < ch.launches.size(); ++i) {
-      const bool to_host = fused && ch.levels[i] == sp.levels;
-      launch_stencil(filter_, geom_.channels,
-                     make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1, to_host ? dev_out : nullptr,
-                                 to_host ? rb : 0),
+      launch_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1, nullptr, 0),
                      cs_, opt_.variant);
       ++stats_.launches;
-      stats_.host_store_launches += to_host;
       pending = true;
     }
-    if (fused) continue;
     if (ch.down_hi > ch.down_lo && host_out && down != cs_) {
       dn_evs_[c].record(cs_);
       pending = false;
@@ -443,7 +415,7 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
   // `down` finishing must mean the whole image is done (the next image of
   // these frames waits on it), also when launches follow the last download.
   if (pending && down != cs_) dn_evs_[nc].record(cs_);
-  for (size_t c = 0; c < nc && !fused; ++c) {
+  for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     if (!(ch.down_hi > ch.down_lo && host_out)) continue;
     if (down != cs_) dn_evs_[c].wait_on(down);
@@ -789,9 +761,23 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
       slots_.push_back(std::make_unique<BandEngine>(geom, band, filter, o));
     }
     if (step_graphs && opt.stream_chunks > 1) {
-      // head streaming: copy streams for images submitted to an idle pipeline
-      h2d_ = Stream::create(0);
-      d2h_ = Stream::create(0);
+      // head streaming: copy streams for images submitted to an idle pipeline.
+      // PCONV_HEAD_STREAMS (A/B): "pool" (default) streams from the runtime's
+      // queue pool, "cumask" dedicated queues like the slots', "slots" the
+      // next two slots' streams (no queue beyond the slots'; >= 3 slots).
+      const char* hs = std::getenv("PCONV_HEAD_STREAMS");
+      head_mode_ = hs ? hs : "pool";
+      if (head_mode_ == "cumask") {
+        int n = 0;
+        PCONV_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, opt.device));
+        std::vector<uint32_t> mask(static_cast<size_t>((n + 31) / 32), 0u);
+        for (int cu = 0; cu < n; ++cu) mask[static_cast<size_t>(cu / 32)] |= 1u << (cu % 32);
+        h2d_ = Stream::create_cu_masked(mask);
+        d2h_ = Stream::create_cu_masked(mask);
+      } else {
+        h2d_ = Stream::create(0);
+        d2h_ = Stream::create(0);
+      }
       ev_head_ = Event::create();
       h2d_wait_ = Event::create();
       head_up_ = Event::create();
@@ -912,12 +898,15 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
       const StreamPlan sp = e.stream_plan(reps, in_r0, in_r1);
       if (!sp.chunks.empty()) {
         e.set_cur(0);  // like process_graph: the whole input is uploaded, start in frame 0
+        const bool via_slots = head_mode_ == "slots" && slots() >= 3;
+        hipStream_t up = via_slots ? computes_[static_cast<size_t>((k + 1) % slots())].get() : h2d_.get();
+        hipStream_t down = via_slots ? computes_[static_cast<size_t>((k + 2) % slots())].get() : d2h_.get();
         h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
-        h2d_wait_.wait_on(h2d_.get());
-        e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, h2d_.get(), d2h_.get());
-        head_up_.record(h2d_.get());  // every chunk upload issued first: all of them done
+        h2d_wait_.wait_on(up);
+        e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down);
+        head_up_.record(up);  // every chunk upload issued first: all of them done
         last_upload_ = &head_up_;
-        ev_head_.record(d2h_.get());
+        ev_head_.record(down);
         ev_head_.wait_on(e.compute_stream());
         idle_ = false;
         used_[k] = true;

@@ -430,8 +430,7 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_readonly("loop_ms", &RunStats::loop_ms)
       .def_readonly("wall_ms", &RunStats::wall_ms)
       .def_readonly("launches", &RunStats::launches)
-      .def_readonly("exchanges", &RunStats::exchanges)
-      .def_readonly("host_store_launches", &RunStats::host_store_launches);
+      .def_readonly("exchanges", &RunStats::exchanges);
 
   py::class_<HaloTransport, PyHaloTransport, std::shared_ptr<HaloTransport>>(m, "HaloTransport")
       .def(py::init<>())

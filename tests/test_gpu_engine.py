@@ -109,6 +109,26 @@ def test_cli_hip(pconv_mod, tmp_path, rng):
         assert np.array_equal(out, pconv_mod.numpy_convolve(img, 11))
 
 
+@pytest.mark.parametrize("typ,filt,chunk", [("rgb", "gaussian", 100000), ("grey", "gaussian", 5000),
+                                            ("rgb", "edge", 65536), ("grey", "box", 1)])
+def test_cli_hip_ring_staging(pconv_mod, tmp_path, rng, typ, filt, chunk):
+    """One-shot run through a ring of small pinned chunks (read chunk k+1 ||
+    upload chunk k; download chunk k+1 || write chunk k): chunk sizes that
+    leave a remainder, one row per chunk, a file input (not synthetic)."""
+    c = 3 if typ == "rgb" else 1
+    w, h = 203, 311
+    img = rng.integers(0, 256, size=(h, w, c) if c > 1 else (h, w), dtype=np.uint8)
+    pconv_mod.write_raw(str(tmp_path / "img.raw"), img)
+    env = dict(os.environ, PCONV_RING_CHUNK_BYTES=str(chunk))
+    r = subprocess.run([CONV_BIN, "img.raw", str(w), str(h), "13", typ, "--filter", filt, "--json"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    meta = json.loads(r.stdout.strip().splitlines()[-1])
+    assert "read_and_h2d" in meta["phases_s"] and "d2h_and_write" in meta["phases_s"], meta["phases_s"]
+    out = pconv_mod.read_raw(str(tmp_path / "blur_img.raw"), w, h, typ)
+    assert np.array_equal(out, pconv_mod.numpy_convolve(img, 13, filt))
+
+
 @pytest.mark.parametrize("transport,extra", [
     ("shm", ["--gpus", "2"]),
     ("shm", ["--gpus", "3", "--exchange-halo"]),

@@ -83,32 +83,20 @@ def test_streamed_preloaded_bands(pconv_mod, rng, mode, world, rank):
     _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps)
 
 
-@pytest.mark.parametrize("w,h,ch,reps,chunks,fuse", [(64, 133, "grey", 40, 4, 0), (1920, 252, "rgb", 40, 4, 0),
-                                                    (50, 71, "rgba", 13, 3, 0), (36, 37, "grey", 41, 9, 8),
-                                                    (67, 45, "rgb", 9, 3, 0)])
-def test_streamed_fused_host_stores(pconv_mod, rng, monkeypatch, w, h, ch, reps, chunks, fuse):
-    """PCONV_STREAM_FUSED_D2H=1: the final level's launches store their rows
-    straight into the pinned output (no download copies); a row width that is
-    not a multiple of 4 bytes (67 RGB) keeps the copies.  Bit-exact either way."""
-    monkeypatch.setenv("PCONV_STREAM_FUSED_D2H", "1")
-    kw = dict(fuse=fuse, halo=fuse) if fuse else {}
-    blur = _blur(w, h, ch, "gaussian", reps, chunks, slots=1, **kw)
-    _run_images(pconv_mod, rng, blur, w, h, ch, "gaussian", reps)
-    rb = w * CH[ch]
-    if rb % 4 == 0:
-        assert blur.stats.host_store_launches >= 1
-    else:
-        assert blur.stats.host_store_launches == 0
-
-
-@pytest.mark.parametrize("world,rank", [(3, 1), (8, 0), (8, 7)])
-def test_streamed_fused_host_stores_bands(pconv_mod, rng, monkeypatch, world, rank):
-    monkeypatch.setenv("PCONV_STREAM_FUSED_D2H", "1")
-    w, h, reps = 64, 400, 40
-    blur = _blur(w, h, "rgb", "gaussian", reps, 3, slots=1, rank=rank, world=world, preload_halo=True,
-                 transport="none")
-    _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps)
-    assert blur.stats.host_store_launches >= 1
+@pytest.mark.parametrize("streams", ["cumask", "slots"])
+@pytest.mark.parametrize("slots", [2, 3, 4])
+def test_head_stream_modes(pconv_mod, rng, monkeypatch, streams, slots):
+    """PCONV_HEAD_STREAMS: the streamed head image's copies on dedicated
+    queues, or on the next two slots' streams (falls back below 3 slots);
+    bursts and single images (blur.step) bit-exact."""
+    monkeypatch.setenv("PCONV_HEAD_STREAMS", streams)
+    w, h, reps = 96, 120, 40
+    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=slots, mode="head")
+    _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps, rounds=3)
+    img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+    blur.load_image(img)
+    for _ in range(3):
+        assert np.array_equal(blur.step(reps).reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps))
 
 
 @pytest.mark.parametrize("mode", ["direct", "head"])
