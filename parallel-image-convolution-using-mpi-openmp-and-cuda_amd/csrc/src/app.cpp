@@ -308,7 +308,7 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   const int64_t rb = g.row_bytes();
   const int64_t ring_rows = std::max<int64_t>(1, ring_chunk_bytes() / rb);
   const bool ring = !cache && !c.check && c.checkpoint_every == 0 && ring_staging_enabled() &&
-                    g.height >= kRingSlots * ring_rows;
+                    g.height > (kRingSlots - 1) * ring_rows;  // >= kRingSlots chunks
   PinnedBuffer own_host;
   uint8_t* host = nullptr;
   if (cache) {

@@ -109,7 +109,7 @@ def test_cli_hip(pconv_mod, tmp_path, rng):
         assert np.array_equal(out, pconv_mod.numpy_convolve(img, 11))
 
 
-@pytest.mark.parametrize("typ,filt,chunk", [("rgb", "gaussian", 100000), ("grey", "gaussian", 5000),
+@pytest.mark.parametrize("typ,filt,chunk", [("rgb", "gaussian", 30000), ("grey", "gaussian", 5000),
                                             ("rgb", "edge", 65536), ("grey", "box", 1)])
 def test_cli_hip_ring_staging(pconv_mod, tmp_path, rng, typ, filt, chunk):
     """One-shot run through a ring of small pinned chunks (read chunk k+1 ||
