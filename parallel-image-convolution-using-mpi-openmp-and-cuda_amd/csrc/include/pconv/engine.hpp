@@ -325,7 +325,7 @@ class BandPipeline {
   const Event* last_upload_ = nullptr;  // upload-done event of the burst's previous image
   Event head_up_;                       // a streamed head image's uploads done
   Event ev_head_, h2d_wait_;
-  std::string head_mode_ = "pool";      // head streaming's copy streams (PCONV_HEAD_STREAMS)
+  std::string head_mode_ = "slots";      // head streaming's copy streams (PCONV_HEAD_STREAMS)
   std::vector<bool> used_;
   int64_t count_ = 0;
   std::vector<Event> trace_ev_;  // 4 per traced image

@@ -233,30 +233,6 @@ bool ring_staging_enabled() {
   return !(v && v[0] == '0');
 }
 
-// Rows [y0, y0 + n) of a packed image into the output file, split over a few
-// threads: one thread copies into the page cache at ~5 GB/s (32768^2 grey:
-// 0.196 s for the 1 GB result).
-void write_rows_parallel(const std::string& path, const ImageGeom& g, int64_t y0, int64_t n, const uint8_t* src) {
-  const int64_t rb = g.row_bytes();
-  const int parts = static_cast<int>(std::min<int64_t>(4, std::max<int64_t>(1, n * rb / (int64_t(4) << 20))));
-  if (parts <= 1) return write_rows(path, g, y0, n, src, rb);
-  std::vector<std::thread> ts;
-  std::vector<std::string> errors(static_cast<size_t>(parts));
-  for (int p = 0; p < parts; ++p) {
-    const int64_t a = n * p / parts, b = n * (p + 1) / parts;
-    ts.emplace_back([&, p, a, b] {
-      try {
-        write_rows(path, g, y0 + a, b - a, src + a * rb, rb);
-      } catch (const std::exception& e) {
-        errors[static_cast<size_t>(p)] = e.what();
-      }
-    });
-  }
-  for (auto& t : ts) t.join();
-  for (const auto& e : errors)
-    if (!e.empty()) PCONV_FAIL(e);
-}
-
 AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   AppReport r;
   const double t0 = wall_seconds();
@@ -302,7 +278,8 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   // of one pinned copy of the whole image: pinning costs ~0.24 ms per MB
   // (32768^2 grey: 0.244 s of a 0.69 s run, profiles/r04/trace20/), and the
   // ring overlaps reading chunk k+1 with the upload of chunk k, and the
-  // download of chunk k+1 with writing chunk k.  The full buffer stays for
+  // download of chunk k+1 with writing chunk k (one writer: writes of
+  // several threads into one file measured slower, 0.20 vs 0.13 s for 1 GB).  The full buffer stays for
   // --check / checkpoints (they need the whole result in host memory) and for
   // the resident server (its staging is allocated once).
   const int64_t rb = g.row_bytes();
@@ -402,7 +379,7 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
       const int slot = static_cast<int>(k % kRingSlots);
       ring_ev[slot].sync();
       const int64_t r0 = k * ring_rows, n = std::min(ring_rows, g.height - r0);
-      write_rows_parallel(r.output, g, r0, n, host + slot * ring_rows * rb);
+      write_rows(r.output, g, r0, n, host + slot * ring_rows * rb, rb);
       if (k + kRingSlots < nchunks) issue(k + kRingSlots);
     }
     pc.mark("d2h_and_write");

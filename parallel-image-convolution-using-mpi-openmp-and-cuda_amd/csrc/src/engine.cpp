@@ -762,11 +762,14 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
     }
     if (step_graphs && opt.stream_chunks > 1) {
       // head streaming: copy streams for images submitted to an idle pipeline.
-      // PCONV_HEAD_STREAMS (A/B): "pool" (default) streams from the runtime's
-      // queue pool, "cumask" dedicated queues like the slots', "slots" the
-      // next two slots' streams (no queue beyond the slots'; >= 3 slots).
+      // With >= 3 slots the head's upload and download run on the next two
+      // slots' streams (idle when the pipeline is): no hardware queue beyond
+      // the slots'.  Two more queues from the runtime's pool made one image
+      // 0.77 ms with 4 slots, dedicated (CU-masked) ones 0.85 ms, the slots'
+      // streams 0.56 ms (profiles/r04/head/).  Fewer slots: pool streams.
+      // PCONV_HEAD_STREAMS = slots | pool | cumask (A/B).
       const char* hs = std::getenv("PCONV_HEAD_STREAMS");
-      head_mode_ = hs ? hs : "pool";
+      head_mode_ = hs ? hs : "slots";
       if (head_mode_ == "cumask") {
         int n = 0;
         PCONV_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, opt.device));
