@@ -397,21 +397,6 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
          hipMemcpyHostToDevice, up);
     if (up != cs_) up_evs_[c].record(up);
   }
-  // PCONV_STREAM_LAST_CU=1 (A/B): the last chunk's rows come back by a CU
-  // copy kernel on the compute stream, right behind its launches, instead of
-  // an SDMA copy behind a launch -> D2H hop on the download stream.
-  const char* lv = std::getenv("PCONV_STREAM_LAST_CU");
-  bool last_cu = lv && lv[0] == '1' && host_out && down != cs_;
-  uint8_t* dev_out = host_out;  // the device's address of the pinned output
-  if (last_cu) {
-    hipPointerAttribute_t at{};
-    if (hipPointerGetAttributes(&at, host_out) != hipSuccess || at.type != hipMemoryTypeHost || !at.devicePointer) {
-      (void)hipGetLastError();  // pageable memory: only an SDMA copy can reach it
-      last_cu = false;
-    } else {
-      dev_out = static_cast<uint8_t*>(at.devicePointer);
-    }
-  }
   bool pending = false;  // launches not yet covered by a download-side event
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
@@ -421,13 +406,6 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
                      cs_, opt_.variant);
       ++stats_.launches;
       pending = true;
-    }
-    if (last_cu && c + 1 == nc) {
-      if (ch.down_hi > ch.down_lo)
-        launch_copy_rows(out_frame + ch.down_lo * p, p, dev_out + ch.down_lo * rb, rb, rb, ch.down_hi - ch.down_lo,
-                         cs_);
-      pending = true;  // `down` still waits for it (dn_evs_[nc] below)
-      continue;
     }
     if (ch.down_hi > ch.down_lo && host_out && down != cs_) {
       dn_evs_[c].record(cs_);
@@ -439,7 +417,7 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
   if (pending && down != cs_) dn_evs_[nc].record(cs_);
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
-    if (!(ch.down_hi > ch.down_lo && host_out) || (last_cu && c + 1 == nc)) continue;
+    if (!(ch.down_hi > ch.down_lo && host_out)) continue;
     if (down != cs_) dn_evs_[c].wait_on(down);
     copy(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, ch.down_hi - ch.down_lo, hipMemcpyDeviceToHost,
          down);

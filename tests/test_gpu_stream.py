@@ -100,24 +100,6 @@ def test_head_stream_modes(pconv_mod, rng, monkeypatch, streams, slots):
 
 
 @pytest.mark.parametrize("mode", ["direct", "head"])
-@pytest.mark.parametrize("w,h,ch,reps,chunks", [(64, 133, "grey", 40, 4), (67, 45, "rgb", 9, 3),
-                                               (33, 37, "grey", 41, 9)])
-def test_streamed_last_chunk_cu_download(pconv_mod, rng, monkeypatch, mode, w, h, ch, reps, chunks):
-    """PCONV_STREAM_LAST_CU=1: the last chunk's rows come back by a CU copy
-    on the compute stream (no launch -> D2H hop); bit-exact, bursts and
-    single images."""
-    monkeypatch.setenv("PCONV_STREAM_LAST_CU", "1")
-    blur = _blur(w, h, ch, "gaussian", reps, chunks, slots=3, mode=mode)
-    _run_images(pconv_mod, rng, blur, w, h, ch, "gaussian", reps)
-    c = CH[ch]
-    img = rng.integers(0, 256, size=(h, w, c), dtype=np.uint8)
-    blur.load_image(img)
-    ref = pconv_mod.numpy_convolve(img if c > 1 else img[..., 0], reps).reshape(h, -1)
-    for _ in range(2):
-        assert np.array_equal(blur.step(reps).reshape(h, -1), ref)
-
-
-@pytest.mark.parametrize("mode", ["direct", "head"])
 def test_streamed_step_and_reps_zero(pconv_mod, rng, mode):
     """blur.step (one image alone: streamed in both modes) and reps = 0
     (nothing to stream: the whole-image path) through a streaming pipeline."""
