@@ -373,13 +373,9 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
   while (dn_evs_.size() < nc + 1) dn_evs_.push_back(Event::create());
   // Host issue order: every upload first (the H2D stream then runs them back
   // to back instead of waiting for the host to issue the next one behind the
-  // previous chunk's launches), then per chunk its launches behind its
-  // upload's event and at once its download behind its launches' event.
-  // Issuing every download after every launch left the first download ~100
-  // us behind its chunk's launches while the host issued the rest
-  // (profiles/r04/api_trace/); PCONV_STREAM_ISSUE=late restores that order
-  // (A/B).  One event per chunk and direction (no re-recorded event is
-  // waited on).
+  // previous chunk's launches), then each chunk's launches behind its
+  // upload's event, then each download behind its chunk's event.  One event
+  // per chunk and direction (no re-recorded event is waited on).
   // PCONV_STREAM_COPIES=kernel (A/B): chunk copies as CU kernels (a capped
   // grid beside the launches) instead of SDMA.
   static const int kcopy_blocks = [] {
@@ -401,15 +397,6 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
          hipMemcpyHostToDevice, up);
     if (up != cs_) up_evs_[c].record(up);
   }
-  const char* iv = std::getenv("PCONV_STREAM_ISSUE");
-  const bool early = down != cs_ && !(iv && std::string(iv) == "late");
-  auto download = [&](size_t c) {
-    const StreamChunk& ch = sp.chunks[c];
-    if (!(ch.down_hi > ch.down_lo && host_out)) return;
-    if (down != cs_) dn_evs_[c].wait_on(down);
-    copy(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, ch.down_hi - ch.down_lo, hipMemcpyDeviceToHost,
-         down);
-  };
   bool pending = false;  // launches not yet covered by a download-side event
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
@@ -424,12 +411,17 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
       dn_evs_[c].record(cs_);
       pending = false;
     }
-    if (early) download(c);
   }
   // `down` finishing must mean the whole image is done (the next image of
   // these frames waits on it), also when launches follow the last download.
   if (pending && down != cs_) dn_evs_[nc].record(cs_);
-  for (size_t c = 0; c < nc && !early; ++c) download(c);
+  for (size_t c = 0; c < nc; ++c) {
+    const StreamChunk& ch = sp.chunks[c];
+    if (!(ch.down_hi > ch.down_lo && host_out)) continue;
+    if (down != cs_) dn_evs_[c].wait_on(down);
+    copy(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, ch.down_hi - ch.down_lo, hipMemcpyDeviceToHost,
+         down);
+  }
   if (pending && down != cs_) dn_evs_[nc].wait_on(down);
   cur_ = (c0 + sp.levels) & 1;
   halo_valid_ = false;
