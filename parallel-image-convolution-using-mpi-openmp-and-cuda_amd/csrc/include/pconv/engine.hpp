@@ -326,21 +326,6 @@ class BandPipeline {
   Event head_up_;                       // a streamed head image's uploads done
   Event ev_head_, h2d_wait_;
   std::string head_mode_ = "slots";      // head streaming's copy streams (PCONV_HEAD_STREAMS)
-  // Tail streaming: the newest image is issued by the next submit (as a step
-  // graph) or by drain() (streamed).
-  struct Deferred {
-    bool valid = false;
-    int k = 0, pos = 0;
-    const uint8_t* in = nullptr;
-    int64_t r0 = 0, r1 = 0;
-    uint8_t* out = nullptr;
-    int reps = 0;
-  };
-  Deferred deferred_;
-  bool defer_tail_ = false;
-  bool stream_on_slots(int k, const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps);
-  void issue_graph(int k, int pos, const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
-                   int reps);
   std::vector<bool> used_;
   int64_t count_ = 0;
   std::vector<Event> trace_ev_;  // 4 per traced image

@@ -784,10 +784,6 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
       ev_head_ = Event::create();
       h2d_wait_ = Event::create();
       head_up_ = Event::create();
-      // Tail streaming (PCONV_TAIL_STREAM=0 turns it off): needs the slots'
-      // streams for the tail's copies, so >= 3 slots in "slots" mode.
-      const char* ts = std::getenv("PCONV_TAIL_STREAM");
-      defer_tail_ = !(ts && ts[0] == '0') && head_mode_ == "slots" && slots >= 3;
     }
     used_.assign(slots, false);
     // PCONV_WAVE_ALL=1 (A/B, with stream_chunks -1): every image a wave
@@ -846,40 +842,6 @@ void BandPipeline::set_transport(std::shared_ptr<HaloTransport> t) {
   for (auto& s : slots_) s->set_transport(t);
 }
 
-bool BandPipeline::stream_on_slots(int k, const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
-                                   int reps) {
-  BandEngine& e = *slots_[k];
-  const StreamPlan sp = e.stream_plan(reps, in_r0, in_r1);
-  if (sp.chunks.empty()) return false;
-  e.set_cur(0);  // like process_graph: the whole input is uploaded, start in frame 0
-  const bool via_slots = head_mode_ == "slots" && slots() >= 3;
-  hipStream_t up = via_slots ? computes_[static_cast<size_t>((k + 1) % slots())].get() : h2d_.get();
-  hipStream_t down = via_slots ? computes_[static_cast<size_t>((k + 2) % slots())].get() : d2h_.get();
-  h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
-  h2d_wait_.wait_on(up);
-  e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down);
-  head_up_.record(up);  // every chunk upload issued first: all of them done
-  last_upload_ = &head_up_;
-  ev_head_.record(down);
-  ev_head_.wait_on(e.compute_stream());
-  return true;
-}
-
-void BandPipeline::issue_graph(int k, int pos, const uint8_t* host_in, int64_t in_r0, int64_t in_r1,
-                               uint8_t* host_out, int reps) {
-  BandEngine& e = *slots_[k];
-  if (stagger_ && pos > 0 && pos < slots() && last_upload_) {
-    // Head of a burst: start this upload when the previous image's is done
-    // (one cross-stream wait per image, first `slots` images only).  All
-    // slots uploading at once would split the link three ways and move the
-    // slots in lockstep — no download beside an upload until the whole
-    // first group is in (the driver's 20-image window pays that).
-    last_upload_->wait_on(e.compute_stream());
-  }
-  e.process_graph(host_in, in_r0, in_r1, host_out, reps);
-  last_upload_ = stagger_ ? &e.upload_event() : nullptr;
-}
-
 void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
   TraceRange tr("pconv.pipeline.submit");
   const int k = static_cast<int>(count_ % static_cast<int64_t>(slots_.size()));
@@ -912,11 +874,6 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   }
   if (graphs_) {
     PCONV_CHECK(trace_ev_.empty(), "pipeline trace needs directly issued images (graph capture off)");
-    if (deferred_.valid) {  // the previous image is not the tail: a step graph
-      const Deferred d = deferred_;
-      deferred_.valid = false;
-      issue_graph(d.k, d.pos, d.in, d.r0, d.r1, d.out, d.reps);
-    }
     if (idle_) {
       burst_ = 0;
       last_upload_ = nullptr;
@@ -941,25 +898,35 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
       // and every single image (latency).  Images behind it run as step
       // graphs; the slot's stream waits for the streamed image's last
       // download before its next graph touches these frames.
-      if (stream_on_slots(k, host_in, in_r0, in_r1, host_out, reps)) {
+      const StreamPlan sp = e.stream_plan(reps, in_r0, in_r1);
+      if (!sp.chunks.empty()) {
+        e.set_cur(0);  // like process_graph: the whole input is uploaded, start in frame 0
+        const bool via_slots = head_mode_ == "slots" && slots() >= 3;
+        hipStream_t up = via_slots ? computes_[static_cast<size_t>((k + 1) % slots())].get() : h2d_.get();
+        hipStream_t down = via_slots ? computes_[static_cast<size_t>((k + 2) % slots())].get() : d2h_.get();
+        h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
+        h2d_wait_.wait_on(up);
+        e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down);
+        head_up_.record(up);  // every chunk upload issued first: all of them done
+        last_upload_ = &head_up_;
+        ev_head_.record(down);
+        ev_head_.wait_on(e.compute_stream());
         idle_ = false;
         used_[k] = true;
         ++count_;
         return;
       }
     }
-    if (defer_tail_) {
-      // Tail streaming: hold this image back until the next submit (which
-      // issues it as a step graph) or drain() (which streams it: the last
-      // image of a burst then downloads its rows while its later chunks
-      // still upload and compute, instead of one whole D2H after its loop).
-      deferred_ = Deferred{true, k, pos, host_in, in_r0, in_r1, host_out, reps};
-      idle_ = false;
-      used_[k] = true;
-      ++count_;
-      return;
+    if (stagger_ && pos > 0 && pos < slots() && last_upload_) {
+      // Head of a burst: start this upload when the previous image's is done
+      // (one cross-stream wait per image, first `slots` images only).  All
+      // slots uploading at once would split the link three ways and move the
+      // slots in lockstep — no download beside an upload until the whole
+      // first group is in (the driver's 20-image window pays that).
+      last_upload_->wait_on(e.compute_stream());
     }
-    issue_graph(k, pos, host_in, in_r0, in_r1, host_out, reps);
+    e.process_graph(host_in, in_r0, in_r1, host_out, reps);
+    last_upload_ = stagger_ ? &e.upload_event() : nullptr;
     idle_ = false;
     used_[k] = true;
     ++count_;
@@ -1037,11 +1004,6 @@ std::vector<std::vector<double>> BandPipeline::trace() {
 }
 
 void BandPipeline::drain() {
-  if (deferred_.valid) {  // the tail of the burst: streamed if it can be
-    const Deferred d = deferred_;
-    deferred_.valid = false;
-    if (!stream_on_slots(d.k, d.in, d.r0, d.r1, d.out, d.reps)) issue_graph(d.k, d.pos, d.in, d.r0, d.r1, d.out, d.reps);
-  }
   if (h2d_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(h2d_.get()));
   for (auto& s : slots_) s->synchronize();
   if (d2h_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(d2h_.get()));

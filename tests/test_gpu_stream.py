@@ -99,29 +99,6 @@ def test_head_stream_modes(pconv_mod, rng, monkeypatch, streams, slots):
         assert np.array_equal(blur.step(reps).reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps))
 
 
-@pytest.mark.parametrize("tail", ["1", "0"])
-@pytest.mark.parametrize("slots", [3, 4])
-@pytest.mark.parametrize("n", [1, 2, 5, 9])
-def test_tail_streaming_bursts(pconv_mod, rng, monkeypatch, tail, slots, n):
-    """Bursts submitted back to back (no load between them, as the bench
-    does): the head image is streamed, the middle ones run as step graphs, the
-    last one is held back and streamed by drain() (PCONV_TAIL_STREAM=0: a step
-    graph too).  Every output bit-exact, bursts of 1 .. 3x the slots."""
-    monkeypatch.setenv("PCONV_TAIL_STREAM", tail)
-    w, h, reps = 96, 120, 40
-    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=slots, mode="head")
-    img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
-    blur.load_image(img)  # every slot
-    ref = pconv_mod.numpy_convolve(img, reps).reshape(h, -1)
-    for _ in range(3):
-        for o in blur.outputs:
-            o[:] = 0xAB
-        ks = [blur.submit(reps) for _ in range(n)]
-        blur.drain()
-        for k in set(ks):
-            assert np.array_equal(blur.outputs[k].reshape(h, -1), ref), (k, ks)
-
-
 @pytest.mark.parametrize("mode", ["direct", "head"])
 def test_streamed_step_and_reps_zero(pconv_mod, rng, mode):
     """blur.step (one image alone: streamed in both modes) and reps = 0
