@@ -376,20 +376,11 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
   // previous chunk's launches), then each chunk's launches behind its
   // upload's event, then each download behind its chunk's event.  One event
   // per chunk and direction (no re-recorded event is waited on).
-  // PCONV_STREAM_COPIES=kernel (A/B): chunk copies as CU kernels (a capped
-  // grid beside the launches) instead of SDMA.
-  static const int kcopy_blocks = [] {
-    const char* v = std::getenv("PCONV_STREAM_COPIES");
-    return v && std::string(v).rfind("kernel", 0) == 0 ? std::max(8, std::atoi(v + 6) > 0 ? std::atoi(v + 6) : 128)
-                                                        : 0;
-  }();
+  // Chunk copies are SDMA copies: CU copy kernels beside the launches
+  // measured slower (0.76-1.02 vs 0.55 ms per image, profiles/r04/verify/).
   auto copy = [&](uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, int64_t rows, hipMemcpyKind kind,
                   hipStream_t s) {
-    if (rows <= 0) return;
-    if (kcopy_blocks > 0)
-      launch_copy_rows(src, spitch, dst, dpitch, rb, rows, s, kcopy_blocks);
-    else
-      PCONV_HIP_CHECK(hipMemcpy2DAsync(dst, dpitch, src, spitch, rb, rows, kind, s));
+    if (rows > 0) PCONV_HIP_CHECK(hipMemcpy2DAsync(dst, dpitch, src, spitch, rb, rows, kind, s));
   };
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
