@@ -144,6 +144,18 @@ def parse():
                    help="after timing (outside the timed region), compare every rank's newest image, and every halo "
                         "mode's at N>1, with the CPU oracle; 'mismatches' in the JSON line (default on)")
     p.add_argument("--no-check", dest="check", action="store_false", help="skip the oracle check (sweeps)")
+    p.add_argument("--no-stagger", dest="stagger", action="store_false", default=True,
+                   help="the first images of a burst upload all at once (default: one after another)")
+    p.add_argument("--pool-queues", dest="cu_mask_queues", action="store_false", default=True,
+                   help="slot streams from the runtime's queue pool (default: each on its own CU-masked hardware "
+                        "queue, profiles/r04/slots_c/)")
+    p.add_argument("--head-pool-streams", dest="head_on_slot_streams", action="store_false", default=True,
+                   help="a streamed head image's copies on two pool streams (default: the next two slots' streams)")
+    p.add_argument("--ipc-pull", choices=["grid", "single", "sdma"], default="grid",
+                   help="halo mode ipc: how a rank pulls its neighbours' rows (grid: one dispatch of many "
+                        "workgroups; single: one workgroup; sdma: flag kernels around SDMA peer copies)")
+    p.add_argument("--numa-bind", choices=["on", "off"], default="on",
+                   help="restrict each rank to its GPU's NUMA node (default on)")
     p.add_argument("--native", action="store_true",
                    help="run the same serving step on the native stack: the in-tree `conv --bench` (ROCm's HIP "
                         "runtime, no torch; its fork launcher for N > 1) and print its JSON line")
@@ -192,6 +204,16 @@ def gather_floats(v: float):
     return [float(x) for x in out]
 
 
+def gather_ints(v: int):
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [int(v)]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, int(v))
+    return [int(x) for x in out]
+
+
 # Halo modes timed after the pre-loaded headline at N>1 (each with the same K
 # steps, barriers and device syncs as the headline):
 #   slot_exchange: each image on its slot's own stream with its own
@@ -220,9 +242,16 @@ def mode_transport(mode: str, transport: str) -> str:
     return "ipc" if mode == "ipc" else transport
 
 
+def policy_kwargs(a) -> dict:
+    """Pipeline policy flags -> DistributedBlur / native EngineOptions (echoed in the JSON config)."""
+    return dict(stagger=getattr(a, "stagger", True), cu_mask_queues=getattr(a, "cu_mask_queues", True),
+                head_on_slot_streams=getattr(a, "head_on_slot_streams", True),
+                ipc_pull=getattr(a, "ipc_pull", "grid"))
+
+
 def mode_kwargs(a, mode: str, fuse: int) -> dict:
     kw = dict(preload_halo=False, slots=a.slots, variant=a.variant, fuse=a.fuse, overlap=not a.no_overlap,
-              halo=a.halo, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent])
+              halo=a.halo, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent], **policy_kwargs(a))
     if mode in ("slot_exchange", "slot_exchange_direct", "ipc"):
         kw["slot_exchange"] = True
         kw["graph_capture"] = mode != "slot_exchange_direct"
@@ -269,11 +298,13 @@ def measure_mode(a, mode, ref_rows, world, rank, device, transport, fuse, oracle
         if oracle is not None:
             res["mismatches"] = mismatching_bytes(got, oracle)
         per_rank = gather_floats(mine)
+        h2d_b, d2h_b = gather_ints(xb.h2d_bytes_per_image), gather_ints(xb.d2h_bytes_per_image)
         st = xb.stats
         px = a.width * a.height * a.reps
         res.update(steps=a.steps, ms_per_step=round(elapsed / a.steps * 1e3, 4),
                    value=round(px * a.steps / elapsed / 1e6, 2), mismatches_vs_headline=int(bad),
                    per_rank_ms_per_step=[round(t / a.steps * 1e3, 4) for t in per_rank],
+                   h2d_bytes_per_step=h2d_b, d2h_bytes_per_step=d2h_b,
                    halo_depth=int(xb.engine.halo), fuse=int(xb.engine.fuse),
                    launches_per_step=int(st.launches), exchanges_per_step=int(st.exchanges),
                    slot_streams=bool(xb.pipe.graphs), step_graphs=bool(xb.pipe.step_graphs),
@@ -375,6 +406,10 @@ def run_native(a) -> int:
         cmd.append("--check")
     if a.transport == "gloo-host":
         cmd += ["--transport", "shm"]  # rehearsal: ranks may share one GPU
+    cmd += [] if a.stagger else ["--no-stagger"]
+    cmd += [] if a.cu_mask_queues else ["--pool-queues"]
+    cmd += [] if a.head_on_slot_streams else ["--head-pool-streams"]
+    cmd += [] if a.numa_bind == "on" else ["--no-numa-bind"]
     if a.emulate:
         cmd[cmd.index("--gpus") + 1] = "1"
         cmd += ["--emulate", a.emulate]  # one rank of a WORLD-way split, alone (per-rank proxy)
@@ -439,7 +474,7 @@ def main():
     device = ctx.local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     # host thread + first-touch pinned buffers on the GPU's own socket
-    cpu_bind = bind_to_device_numa(device)
+    cpu_bind = bind_to_device_numa(device, enabled=a.numa_bind == "on")
 
     if a.emulate and a.emulate_halo != "preload":
         fuse0 = a.fuse if a.fuse is not None else DistributedBlur(
@@ -454,7 +489,8 @@ def main():
                                preload_halo=a.preload_halo, slots=a.slots, variant=a.variant,
                                transport=head_transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
                                step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
-                               graph_capture=a.graph_capture == "on", stream_chunks=a.stream_chunks)
+                               graph_capture=a.graph_capture == "on", stream_chunks=a.stream_chunks,
+                               **policy_kwargs(a))
     blur.load_synthetic(a.seed)
     # --emulate-rccl: hold a (1-rank) RCCL communicator through the timed
     # region, as every real N>1 rank of the exchange path does.
@@ -481,6 +517,9 @@ def main():
     mine = time.perf_counter() - t0
     elapsed = max_over_ranks(mine)
     per_rank = gather_floats(mine)  # diagnostics: load balance across ranks
+    # PCIe bytes per image of every rank (band + pre-loaded ghost rows in, owned rows out): whether an N>1
+    # line is link-bound or host-memory-bound
+    h2d_bytes, d2h_bytes = gather_ints(blur.h2d_bytes_per_image), gather_ints(blur.d2h_bytes_per_image)
     stats = blur.stats
     # ---- oracle check of the newest image (not timed): every rank compares
     # its owned rows with the CPU oracle of its dependency cone.  Not with
@@ -587,6 +626,11 @@ def main():
                 "preload_halo": bool(blur.preload_halo),
                 "launches_per_step": int(stats.launches),
                 "exchanges_per_step": int(stats.exchanges),
+                "stagger": bool(a.stagger),
+                "cu_mask_queues": bool(a.cu_mask_queues),
+                "head_on_slot_streams": bool(a.head_on_slot_streams),
+                "ipc_pull": a.ipc_pull,
+                "numa_bind": a.numa_bind == "on",
             },
             "latency_ms": round(latency_ms, 4),
             "copy_floor": {"h2d_ms": round(h2d_ms, 4), "d2h_ms": round(d2h_ms, 4),
@@ -605,6 +649,8 @@ def main():
             "headline_transport": head_transport if world > 1 else None,
             "pconv": pconv.__version__,
             "per_rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in per_rank],
+            "h2d_bytes_per_step": h2d_bytes,
+            "d2h_bytes_per_step": d2h_bytes,
             "rank0_cpus_bound": cpu_bind,
         }
         if mismatches is not None:
@@ -707,7 +753,8 @@ def main():
                 r = ok[pick]
                 adopted = dict(out)
                 adopted.update(value=r["value"], ms_per_step=r["ms_per_step"], headline_transport=transport,
-                               per_rank_ms_per_step=r["per_rank_ms_per_step"])
+                               per_rank_ms_per_step=r["per_rank_ms_per_step"],
+                               h2d_bytes_per_step=r["h2d_bytes_per_step"], d2h_bytes_per_step=r["d2h_bytes_per_step"])
                 if adopted["vs_baseline"] is not None:
                     adopted["vs_baseline"] = round(r["value"] / BASELINE_MPIX, 2)
                 adopted["config"] = dict(out["config"], halo_mode=pick, preload_halo=False,

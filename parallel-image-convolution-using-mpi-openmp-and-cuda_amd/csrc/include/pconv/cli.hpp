@@ -17,10 +17,9 @@
 
 namespace pconv {
 
-// Auto (one-shot, 1 GPU): the job is priced on the CPU from a row sample;
-// short jobs run on the CPU and never touch the GPU, the rest on the GPU
-// path alone (app.cpp run_auto; the CPU-head-start handoff is opt-in,
-// PCONV_AUTO_HANDOFF=1).
+// Auto (one-shot, 1 GPU): the job is priced on the CPU from a row sample
+// (then from its first full repetition); short jobs run on the CPU and never
+// touch the GPU, the rest on the GPU path alone (app.cpp run_auto).
 enum class Backend { Hip, Cpu, Omp, Auto };
 enum class TimeFormat { Auto, Cuda, Mpi, Both };
 
@@ -63,6 +62,15 @@ struct CliConfig {
   // (its band + pre-loaded ghost rows): the per-rank proxy of bench.py
   // --emulate, on the native stack.  0 = off.
   int emulate_world = 0, emulate_rank = 0;
+  // ---- policy knobs (no environment variables; echoed in the JSON lines)
+  int tune = -1;                          // SWAR tile tuning: -1 auto (one-shot off, server on), 0 off, 1 on
+  int64_t ring_chunk_bytes = int64_t(32) << 20;  // one-shot ring staging chunk (0: one pinned image)
+  double auto_gpu_min_s = 0.1;            // --backend auto: CPU seconds above which the GPU runs the job
+  bool stagger = true;                    // --bench: burst stagger of the first uploads
+  bool cu_mask_queues = true;             // --bench: slot streams on dedicated (CU-masked) queues
+  bool head_on_slot_streams = true;       // --bench: streamed head image's copies on the next slots' streams
+  std::string ipc_pull = "grid";          // --transport ipc: pull form (grid | single | sdma)
+  bool numa_bind = true;                  // N > 1: each rank on its GPU's NUMA node
 };
 
 // Parse argv.  Throws pconv::Error with the message to print on bad input.

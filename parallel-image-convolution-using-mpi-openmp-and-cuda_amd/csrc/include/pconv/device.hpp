@@ -43,8 +43,8 @@ struct HipRuntimeInfo {
 };
 HipRuntimeInfo hip_runtime_info();
 // Restrict the calling process to the CPUs local to `device` (sysfs
-// local_cpulist of its PCI function, intersected with the current affinity);
-// PCONV_NUMA_BIND=0 disables.  Returns the CPUs kept, 0 if nothing changed.
+// local_cpulist of its PCI function, intersected with the current affinity).
+// Returns the CPUs kept, 0 if nothing changed.
 int bind_to_device_numa(int device);
 
 // PCIe floor of one pipelined step on this box: `iters` pitched (2-D) H2D

@@ -72,13 +72,24 @@ struct EngineOptions {
   // image overlap on three streams.  0 / 1: whole-image chain.  Issued
   // directly (BandPipeline's event-ordered mode): captured as one graph with
   // fork/join branches it measured 1.4-4.3x slower per image
-  // (profiles/r04/stream_a/).  -1: the image is ONE persistent launch
-  // instead (enqueue_wave, kernels/stencil_wave.hip): copies by the CUs and
-  // every level in one grid, device-side hand-offs, no cross-stream hop.
+  // (profiles/r04/stream_a/).
   int stream_chunks = 0;
   // Step graphs record an event right after their upload (upload_event()):
   // a pipeline staggers the first images of a burst on it (BandPipeline).
   bool upload_event = false;
+  // ---- serving-pipeline policy (BandPipeline, slot-stream mode) ----
+  // Burst stagger: the first `slots` images of a burst start their uploads
+  // one after another (on the previous image's upload event) instead of all
+  // at once.
+  bool stagger = true;
+  // Slot streams on dedicated hardware queues (created with an all-CU mask):
+  // from the runtime's shared pool, 4 slot streams landed on queues of which
+  // two ran every launch ~5x longer (profiles/r04/slots_c/).
+  bool cu_mask_queues = true;
+  // A streamed head image's upload / download run on the next two slots'
+  // streams (idle while the pipeline is) instead of two more pool streams
+  // (0.56 vs 0.77 ms per image with 4 slots, profiles/r04/head/).
+  bool head_on_slot_streams = true;
 };
 
 struct RunStats {
@@ -171,18 +182,6 @@ class BandEngine {
   // chunk).  The caller orders `up` after any earlier use of these frames.
   void enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
                         const StreamPlan& sp, hipStream_t up, hipStream_t down);
-  // Wave image: the same serving step as ONE persistent launch on `stream`
-  // (default: the compute stream) — loads from pinned host memory, every
-  // level and stores to pinned host memory by one resident grid taking
-  // plan_wave's tasks in ticket order.  wave_able() says whether this
-  // image can (exchange-free gaussian plan, whole dwords per row, a task
-  // list of bounded size); enqueue_wave throws otherwise.  A dependency
-  // wait that times out inside the kernel raises at synchronize().
-  bool wave_able(int reps, int64_t in_r0, int64_t in_r1) const;
-  void enqueue_wave(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps,
-                    hipStream_t stream = nullptr);
-  // Tasks of the cached wave plan for these rows (tests / diagnostics; 0 if none).
-  int wave_tasks(int reps, int64_t in_r0, int64_t in_r1) const;
   // With options().upload_event: recorded by every step graph once its
   // upload is done.
   const Event& upload_event() const { return ev_uploaded_; }
@@ -239,18 +238,6 @@ class BandEngine {
   // entries the stream is drained and the cache is emptied.
   void trim_graph_caches();
   std::map<std::tuple<int, int, const uint8_t*, int64_t, int64_t, uint8_t*>, StepGraph> step_graphs_;
-  // wave images: task list + per-level table on the device per (reps, in_r0, in_r1)
-  struct WaveDev {
-    int ntasks = 0, levels = 0;
-    int nload = 0, ncomp = 0, nstore = 0, counters = 0;
-    bool dynamic = true;
-    DeviceBuffer tasks, table;
-  };
-  std::map<std::tuple<int, int64_t, int64_t>, WaveDev> waves_;
-  DeviceBuffer wave_ctl_;  // ticket, abort, tile counters (zeroed by every launch)
-  PinnedBuffer wave_err_;  // set by the kernel when a dependency wait timed out
-  uint64_t wave_timeout_ticks_ = 0;
-  const WaveDev& wave_dev(int reps, int64_t in_r0, int64_t in_r1);
 };
 
 // Serving pipeline: S band engines ("slots") so that the H2D copy of image
@@ -316,16 +303,16 @@ class BandPipeline {
   // step-graph mode with stream_chunks > 1: images submitted while nothing is
   // in flight (after construction / drain) are row-streamed (head streaming)
   bool idle_ = true;
-  bool wave_all_ = false;  // stream_chunks -1: every image a wave launch (A/B), not only the head
   // Burst stagger (step-graph mode): image i < slots of a burst (counted from
   // the last drain) starts its upload only when image i-1's upload is done,
   // instead of all slots uploading at once and moving in lockstep.
   bool stagger_ = true;
+  bool head_streaming_ = false;  // stream_chunks > 1 with step graphs
+  bool head_on_slots_ = false;   // the head's copies on the next two slots' streams
   int burst_ = 0;
   const Event* last_upload_ = nullptr;  // upload-done event of the burst's previous image
   Event head_up_;                       // a streamed head image's uploads done
   Event ev_head_, h2d_wait_;
-  std::string head_mode_ = "slots";      // head streaming's copy streams (PCONV_HEAD_STREAMS)
   std::vector<bool> used_;
   int64_t count_ = 0;
   std::vector<Event> trace_ev_;  // 4 per traced image

@@ -9,10 +9,25 @@
 // rows with device copies — no communication library kernel, no host
 // staging, nothing on the host path after set-up.
 //
-// One dispatch per exchange by default (k_ipc_exchange: the three steps in
-// one workgroup; the rows a neighbour reads always come from an earlier
-// kernel of its stream, whose end-of-kernel release wrote them back on every
-// XCD); PCONV_IPC_KERNELS=3 splits it into three dispatches.
+// Three pull forms (IpcPull, chosen per transport; docs/PERFORMANCE.md has
+// the measurements that pick the default):
+//   * Grid (default): ONE dispatch of G workgroups.  Every workgroup's
+//     thread 0 waits for the neighbours' level flags with its own
+//     system-scope acquire (so each CU's and each XCD's caches are
+//     invalidated for the rows it reads), the workgroup copies its slice,
+//     and the workgroups meet on a device-memory arrival counter; the last
+//     one to arrive publishes `count` / `ack` and waits for the neighbours'
+//     acks.  G workgroups keep G times the single form's bytes in flight —
+//     what a pull over xGMI (microseconds per round trip) needs.
+//   * Single: the same in ONE workgroup (round 4's form: one acquire
+//     covers it; latency-bound on a remote source).
+//   * Sdma: a one-thread signal / wait kernel, the rows moved by SDMA
+//     (hipMemcpyAsync peer copies, no CU involved), a one-thread ack / wait
+//     kernel.  The copies cannot be skipped after a timed-out wait: a
+//     neighbour that stalls (but keeps its frames mapped) yields stale
+//     rows and the raised error, as in the other forms.
+// The rows a neighbour reads always come from an earlier kernel of its
+// stream, whose end-of-kernel release wrote them back on every XCD.
 // Ordering across processes is device-side, through flag words in a shared
 // host-memory segment (POSIX shm, registered with hipHostRegister so every
 // rank's GPU reads and writes it with system-scope atomics).  Per (rank,
@@ -58,25 +73,37 @@ static_assert(sizeof(IpcFlags) == 64, "one cache line per flag block");
 void ipc_create_segment(const std::string& name, int world, int slots);
 void ipc_unlink_segment(const std::string& name);
 
-// Device kernels of the protocol (kernels/ipc_flags.hip).  `flags` is the
-// device pointer of the segment's block array.
-void launch_ipc_signal_wait(IpcFlags* flags, int me, int up, int down, uint64_t timeout_ticks, hipStream_t s);
-void launch_ipc_ack_wait(IpcFlags* flags, int me, int up, int down, uint64_t timeout_ticks, hipStream_t s);
-// Copy `bytes` from each neighbour's rows into this rank's ghost rows (null
-// source: no neighbour on that side); a no-op once this rank's wait timed out.
-void launch_ipc_pull(const IpcFlags* flags, int me, uint8_t* dst_up, const uint8_t* src_up, uint8_t* dst_down,
-                     const uint8_t* src_down, int64_t bytes, hipStream_t s);
-// Signal + wait, pull and ack + wait as ONE single-workgroup dispatch (the
-// default; PCONV_IPC_KERNELS=3 issues the three kernels above instead).
-void launch_ipc_exchange(IpcFlags* flags, int me, int up, int down, uint64_t timeout_ticks, uint8_t* dst_up,
-                         const uint8_t* src_up, uint8_t* dst_down, const uint8_t* src_down, int64_t bytes,
-                         hipStream_t s);
+enum class IpcPull { Grid, Single, Sdma };
+IpcPull parse_ipc_pull(const std::string& s);  // "grid" | "single" | "sdma"
+const char* ipc_pull_name(IpcPull p);
+
+// One exchange in stream order on `s` (kernels/ipc_flags.hip).  `flags` is
+// the device pointer of the segment's block array; dst_* are this rank's
+// ghost rows, src_* the neighbours' boundary rows (null: no neighbour on that
+// side), `bytes` per side, a multiple of 16.  Grid needs `arrive` (one zeroed
+// device word per transport, left zeroed by every exchange) and uses
+// `workgroups` (0: chosen from the size).
+void launch_ipc_exchange(IpcPull form, IpcFlags* flags, uint32_t* arrive, int me, int up, int down,
+                         uint64_t timeout_ticks, uint8_t* dst_up, const uint8_t* src_up, uint8_t* dst_down,
+                         const uint8_t* src_down, int64_t bytes, hipStream_t s, int workgroups = 0);
+// Workgroups the Grid form uses for `bytes` per side.
+int ipc_grid_workgroups(int64_t bytes);
+
+// Cost of one exchange of each pull form without a neighbour process: a flag
+// block in pinned host memory (self-neighbour protocol, up = down = me),
+// `bytes` per side pulled from a pinned HOST buffer (host_source: the
+// stand-in for a peer GPU's HBM behind xGMI — PCIe round trips of
+// microseconds) or from this GPU's HBM; ms per exchange over `iters`
+// back-to-back exchanges on one stream.
+double ipc_pull_probe(const std::string& form, int64_t bytes, bool host_source, int iters, int device,
+                      int workgroups = 0);
 
 class IpcHaloTransport : public HaloTransport {
  public:
   // The engine's frames are exported; `slot` selects this transport's flag
   // blocks (slot k of every rank exchanges with slot k of its neighbours).
-  IpcHaloTransport(BandEngine& e, const std::string& segment, int slot, int slots, double timeout_s = 30.0);
+  IpcHaloTransport(BandEngine& e, const std::string& segment, int slot, int slots, double timeout_s = 30.0,
+                   IpcPull pull = IpcPull::Grid);
   ~IpcHaloTransport() override;
   IpcHaloTransport(const IpcHaloTransport&) = delete;
   IpcHaloTransport& operator=(const IpcHaloTransport&) = delete;
@@ -89,6 +116,7 @@ class IpcHaloTransport : public HaloTransport {
 
   void exchange(BandEngine& e, int64_t depth, hipStream_t stream) override;
   const char* name() const override { return "ipc"; }
+  IpcPull pull() const { return pull_; }
   bool capturable() const override { return true; }
 
   // Exchanges enqueued so far; the device-side count after the stream drained.
@@ -111,7 +139,8 @@ class IpcHaloTransport : public HaloTransport {
   FrameLayout lay_up_, lay_down_;
   bool connected_ = false;
   bool own_ = false;  // a neighbour is this engine itself (one-process emulation)
-  bool split_kernels_ = false;  // PCONV_IPC_KERNELS=3: signal / pull / ack as three dispatches
+  IpcPull pull_ = IpcPull::Grid;
+  DeviceBuffer arrive_;  // Grid form: the workgroups' arrival counter
   uint8_t* own_base_[2] = {nullptr, nullptr};  // this engine's frames (the destructor never touches the engine)
   int64_t enqueued_ = 0;
 };

@@ -13,8 +13,8 @@
 //     reproducing the float32 reference;
 //   * each lane marches down RPT rows keeping the horizontal sums of the last
 //     two rows in registers (every input row is loaded and unpacked once);
-//   * the temporal-blocked kernel fuses `steps` repetitions in one launch
-//     (see stencil_temporal in kernels.hip).
+//   * the temporal-blocked SWAR kernel fuses `steps` repetitions in one
+//     launch (kernels/stencil_swar.hip).
 // The frame's zero pad (image.hpp) provides the boundary; no edge branches.
 #pragma once
 
@@ -50,7 +50,6 @@ enum class KernelVariant : int {
   Temporal = 2,  // SWAR-32 gaussian, `steps` fused in registers (production)
   Int9 = 3,      // generic int-exact 9-tap
   Float9 = 4,    // generic float32 9-tap (reference rounding)
-  TemporalPk = 5,  // packed-u16 (VOP3P) fused gaussian, kept for A/B measurements
   FloatTemporal = 6,  // any 3x3 filter, float32 reference rounding, `steps` fused in registers
 };
 
@@ -75,6 +74,9 @@ void launch_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a,
 // graph capture); clear the cache of tuned shapes.
 void prepare_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream);
 void clear_float_tuning();
+// Force the float kernel's tile (m rows per wave, nw waves; m = 0: the model
+// / tuner again).  An unknown shape is ignored.
+void set_float_shape(int m, int nw);
 
 // Whether `v` (or Auto) can fuse `steps` > 1 for this filter.
 bool supports_fusion(const Filter& f, KernelVariant v);
@@ -99,44 +101,6 @@ void launch_copy_rows(const uint8_t* src, int64_t sp, uint8_t* dst, int64_t dp, 
                       hipStream_t stream, int max_blocks = 0);
 // Zero `bytes` (a multiple of 16, 16-byte aligned) with a kernel of this module.
 void launch_fill_zero(uint8_t* p, int64_t bytes, hipStream_t stream);
-// ONE persistent launch for a whole serving step (kernels/stencil_wave.hip;
-// task list from schedule.hpp plan_wave, gaussian only).
-struct WaveTask;
-struct WaveLaunch {
-  // device copy of WavePlan::tasks partitioned by kind — loads, level tiles,
-  // stores — each part in ticket order
-  const WaveTask* tasks = nullptr;
-  int nload = 0, ncomp = 0, nstore = 0;
-  int loaders = 0, storers = 0;     // workgroups dedicated to loads / stores (0: grid / 8 each)
-  int levels = 0;                   // L
-  int channels = 1;
-  const int* levels_dev = nullptr;  // device, 8 ints per level 0..L: {steps, arrivals, counter_base, qbase, qcount}
-  uint32_t* ctl = nullptr;          // zeroed by every launch: 8 control words (tickets, abort), then tile counters
-  int64_t ctl_bytes = 0;            // a multiple of 16, >= 32 + 4 x counters
-  uint32_t* err = nullptr;          // pinned host word, set to 1 when a wait timed out
-  const uint8_t* host_in = nullptr; // pinned, input rows [in_r0, in_r1) contiguous
-  int64_t in_r0 = 0;
-  uint8_t* host_out = nullptr;      // pinned, owned rows contiguous
-  uint8_t* frame0 = nullptr;        // device frames at (row 0, column 0)
-  uint8_t* frame1 = nullptr;
-  int64_t pitch = 0, row_bytes = 0, g_row0 = 0, height = 0;
-  uint64_t timeout_ticks = 0;       // wall-clock ticks a dependency wait may take
-  int max_workgroups = 0;           // 0: the resident grid
-  int poll_sleep = 2;               // s_sleep(8) (~0.2 us) between two polls of an incomplete counter
-  uint64_t* trace = nullptr;        // device, 4 x u64 per task (claimed, ready, done, wg | xcc << 32); nullable
-  bool write_through = true;        // hand-offs by sc1 stores (no release fence per task) vs plain + release
-  // Level tiles claimed only when ready, deepest level first (the level-tile
-  // section grouped by level, levels_dev carrying each level's range); else
-  // (default) one ticket queue in topological order.
-  bool dynamic = false;
-  int ncounters = 0;                // tile counters in ctl (the per-level heads follow them)
-};
-void launch_wave_image(const WaveLaunch& w, hipStream_t stream);
-// Rows one wave-kernel tile computes at `max_steps` steps (the plan's tile_rows).
-int wave_tile_rows(int max_steps);
-// Column groups (strip pairs) of one wave-kernel level tile; 0 = steps too deep.
-int wave_col_groups(int channels, int steps, int64_t row_bytes);
-
 // Load the code object of the temporal / copy kernels now (a one-shot process
 // calls it from a helper thread while it creates its first hardware queue).
 void preload_kernel_module();

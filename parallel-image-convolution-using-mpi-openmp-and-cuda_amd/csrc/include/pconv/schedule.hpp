@@ -105,73 +105,6 @@ std::vector<int64_t> stream_cuts(int64_t in_lo, int64_t in_hi, int chunks);
 StreamPlan plan_streamed(const std::vector<Phase>& plan, int64_t in_lo, int64_t in_hi, int64_t owned_rows,
                          const std::vector<int64_t>& cuts);
 
-// ---------------------------------------------------------------------------
-// Wave plan: ONE persistent launch per image (kernels/stencil_wave.hip).
-//
-// The streamed image above still pays the runtime's cross-stream hand-offs
-// (an event between two SDMA copies, an H2D -> launch or launch -> D2H hop:
-// 15-22 us each, profiles/r04/stream_c/).  Here the whole image — H2D by the
-// CUs, every level, D2H by the CUs — is a list of small tasks that the
-// workgroups of one resident grid take in ticket order; a task waits only
-// for the tiles it reads, through device-side counters (agent-scope
-// release / acquire), so loads, levels and stores of ONE image run at once
-// with hand-offs of a few microseconds.
-//
-//   * level 0 = the input rows [in_lo, in_hi) (load tasks, host -> frame 0);
-//     level j = plan launch j (rows [lo_j, hi_j), s_j steps, frame j % 2);
-//     stores copy the owned rows of level L to the host;
-//   * every level is cut into row tiles of `tile_rows` rows from its first
-//     row; a load / store tile is split into `parts` row parts and a level
-//     tile into `col_groups[j]` column groups, each one task;
-//   * a task waits for tiles [dep_lo, dep_hi] of one level, each complete
-//     when its counter reaches that level's task count (`arrivals`): for a
-//     level tile, the tiles of level j-1 it reads (rows [a - s_j, b + s_j))
-//     AND the tiles of level j-1 that still read the level-(j-2) rows it
-//     overwrites (two frames: level j is written over level j-2);
-//   * tickets are topological: a task's rank is one more than its latest
-//     dependency's (loads: their tile index), ties by level; every task a
-//     workgroup can wait on was claimed earlier by a running workgroup, so
-//     the queue cannot deadlock whatever the residency.
-struct WaveTask {
-  int32_t kind = 0;       // 0 load (host -> frame 0), 1 level tile, 2 store (frame L % 2 -> host)
-  int32_t level = 0;      // 0 loads, 1..L level tiles, L+1 stores
-  int32_t a = 0, b = 0;   // rows [a, b) (frame-local)
-  int32_t part = 0;       // column group (kind 1) / row part (kinds 0, 2)
-  int32_t tile = 0;       // this task's row tile of its level (the counter it arrives on)
-  // Tiles [dep_lo, dep_hi] of level `level - 1` must be complete (kinds 1, 2;
-  // loads wait for nothing).
-  int32_t dep_lo = 0, dep_hi = -1;
-  int dep_level() const { return kind == 0 ? -1 : level - 1; }
-};
-static_assert(sizeof(WaveTask) == 32, "two 16-byte loads per task descriptor");
-
-struct WavePlan {
-  int levels = 0;                   // L
-  int tile_rows = 0;
-  std::vector<int> steps;           // [0..L]: steps of level j (steps[0] = 0)
-  std::vector<int64_t> lo, hi;      // [0..L]: rows of level j
-  std::vector<int> tiles;           // [0..L]: row tiles of level j
-  std::vector<int> arrivals;        // [0..L]: tasks per tile of level j
-  std::vector<int> counter_base;    // [0..L]: first counter of level j
-  int counters = 0;                 // total counters
-  std::vector<WaveTask> tasks;      // in ticket order
-};
-
-// col_groups[j] (j = 1..L; [0] ignored): column groups of level j's tiles.
-// tile_rows: rows of one tile, at most what one workgroup tile computes at
-// the level with the most steps.
-// load_lead: loads take their tickets this many ranks before the level
-// tiles that first need them (more uploads in flight early).  level_gap: a
-// level tile's rank is its latest dependency's plus this (1: tiles of all
-// levels interleave along the upload front; larger: the lower levels run
-// further ahead of the higher ones, closer to level after level).
-WavePlan plan_wave(const std::vector<Phase>& plan, int64_t in_lo, int64_t in_hi, int64_t owned_rows,
-                   int tile_rows, const std::vector<int>& col_groups, int load_parts, int store_parts,
-                   int load_lead = 2, int level_gap = 1);
-// Throws unless every dependency of every task has all its arrivals earlier
-// in ticket order (tests and the launcher's debug check).
-void check_wave_order(const WavePlan& wp);
-
 // Clamp a requested halo depth / fuse to what the band layout allows.
 PlanConfig normalize_plan_config(PlanConfig cfg, int64_t min_band_rows, int max_fuse);
 

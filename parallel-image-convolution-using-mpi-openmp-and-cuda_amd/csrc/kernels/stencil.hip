@@ -220,212 +220,6 @@ __global__ __launch_bounds__(256) void k_generic9(const uint8_t* __restrict__ sr
   *reinterpret_cast<uint4*>(dst + static_cast<int64_t>(r) * pitch + x) = o;
 }
 
-// ---------------------------------------------------------------------------
-// Temporal-blocked gaussian: `steps` repetitions fused in one launch.
-//
-// Tile = one workgroup of NW waves.  The 64 lanes of a wave lie along the row
-// (16 bytes each: a 1024-byte strip); the NW waves are stacked vertically and
-// wave w keeps tile rows [w*M, (w+1)*M) in registers as packed u16 pairs for
-// the whole launch — the image is read from memory once and written once per
-// `steps` repetitions.  Per step:
-//   * horizontal neighbours across lanes come from DPP wave_shr/wave_shl
-//     (v_mov_b32_dpp) + v_alignbit_b32 — no LDS;
-//   * vertical neighbours across waves: each wave publishes its top/bottom
-//     row in LDS (double-buffered by step parity, one s_barrier per step);
-//   * the vertical [1,2,1] runs as a rolling window down the wave's rows;
-//   * rows / columns outside the image are forced to zero after every step
-//     (zero-padding semantics), the tile's own halo (`steps` rows at the top
-//     and bottom, ceil(steps*CH/16) lanes at each side) absorbs the garbage
-//     that enters from outside the tile, one row / CH bytes per step.
-// Arithmetic is compiler-visible (ext_vector u16x2 -> v_pk_add_u16 /
-// v_pk_mad_u16 / v_pk_lshrrev_b16) so hazards and scheduling stay with hipcc.
-// ---------------------------------------------------------------------------
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ u16x2 as_v(u32 x) { return __builtin_bit_cast(u16x2, x); }
-__device__ __forceinline__ u32 as_u(u16x2 x) { return __builtin_bit_cast(u32, x); }
-
-// Horizontal [1,2,1] at distance CH on a row held as pairs X[k] = (b_k, b_{k+8}).
-template <int CH>
-__device__ __forceinline__ void horiz_pairs(const u32 (&X)[8], u16x2 two, u16x2 (&H)[8]) {
-  u32 Q[8 + 2 * CH];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) Q[CH + k] = X[k];
-#pragma unroll
-  for (int j = 1; j <= CH; ++j) {
-    // (b_{-j}, b_{8-j}): left lane's byte 16-j sits in its X[8-j].hi
-    const u32 l = __builtin_amdgcn_mov_dpp(X[8 - j], 0x138, 0xf, 0xf, true);  // wave_shr:1
-    Q[CH - j] = __builtin_amdgcn_alignbit(X[8 - j], l, 16);
-  }
-#pragma unroll
-  for (int j = 0; j < CH; ++j) {
-    // (b_{8+j}, b_{16+j}): right lane's byte j sits in its X[j].lo
-    const u32 r = __builtin_amdgcn_mov_dpp(X[j], 0x130, 0xf, 0xf, true);  // wave_shl:1
-    Q[CH + 8 + j] = __builtin_amdgcn_alignbit(r, X[j], 16);
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) H[k] = as_v(Q[CH + k]) * two + (as_v(Q[k]) + as_v(Q[2 * CH + k]));
-}
-
-template <int CH, int M, int NW>
-__global__ __launch_bounds__(64 * NW) void k_temporal(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                      int64_t pitch, int row_bytes, int r0, int r1, int steps,
-                                                      int g_row0, int height, u32 two_bits) {
-  __shared__ uint4 lds[2][NW][2][2][64];  // [parity][wave][top/bottom][half][lane]
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave index: scalar
-  const int hl = (steps * CH + 15) >> 4;  // halo lanes per side
-  const int vlanes = 64 - 2 * hl;
-  const int chunk = blockIdx.x * vlanes - hl + lane;  // 16-byte column chunk of this lane
-  const int x = chunk * 16;
-  const int nchunks = (row_bytes + 15) >> 4;
-  const bool col_in = chunk >= 0 && chunk < nchunks;
-  const int vrows = NW * M - 2 * steps;              // valid output rows per tile
-  const int tile_r0 = r0 + static_cast<int>(blockIdx.y) * vrows;  // first output row of the tile
-  const int row_base = tile_r0 - steps + w * M;      // frame row of this wave's row 0
-  const u16x2 two = as_v(two_bits);                  // runtime (2,2): keeps v_pk_mad_u16
-
-  // Column mask: lanes outside the image are zero; the partial last chunk
-  // keeps only bytes < row_bytes.  Pair k = (byte k, byte k+8).
-  u32 cmask[8];
-  const int valid = col_in ? min(row_bytes - x, 16) : 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) cmask[k] = (k < valid ? 0xffffu : 0u) | (k + 8 < valid ? 0xffff0000u : 0u);
-  const bool edge_strip = blockIdx.x == 0 || static_cast<int>(blockIdx.x) * vlanes - hl + 64 >= nchunks;
-
-  // ---- load M rows (frame rows outside [r0-steps, r1+steps) or outside the image read as zero)
-  u32 D[M][8];
-  const int lo_ok = max(r0 - steps, -g_row0), hi_ok = min(r1 + steps, height - g_row0);
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    const int fr = row_base + i;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (col_in && fr >= lo_ok && fr < hi_ok) v = *reinterpret_cast<const uint4*>(src + static_cast<int64_t>(fr) * pitch + x);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      D[i][k] = perm(v.z, v.x, pair_sel(k));
-      D[i][4 + k] = perm(v.w, v.y, pair_sel(k));
-    }
-  }
-  // Rows of this wave that lie outside the image (always zero).
-  const int out_top = min(max(-g_row0 - row_base, 0), M);          // rows i < out_top are above the image
-  const int out_bot = min(max(height - g_row0 - row_base, 0), M);  // rows i >= out_bot are below it
-
-  for (int s = 0; s < steps; ++s) {
-    const int par = s & 1;
-    // publish boundary rows
-    lds[par][w][0][0][lane] = make_uint4(D[0][0], D[0][1], D[0][2], D[0][3]);
-    lds[par][w][0][1][lane] = make_uint4(D[0][4], D[0][5], D[0][6], D[0][7]);
-    lds[par][w][1][0][lane] = make_uint4(D[M - 1][0], D[M - 1][1], D[M - 1][2], D[M - 1][3]);
-    lds[par][w][1][1][lane] = make_uint4(D[M - 1][4], D[M - 1][5], D[M - 1][6], D[M - 1][7]);
-    __syncthreads();
-    u32 A[8], B[8];
-    {
-      const int wa = w > 0 ? w - 1 : 0;        // wave 0: tile top halo, value irrelevant
-      const int wb = w < NW - 1 ? w + 1 : w;   // last wave: tile bottom halo
-      const uint4 a0 = lds[par][wa][1][0][lane], a1 = lds[par][wa][1][1][lane];
-      const uint4 b0 = lds[par][wb][0][0][lane], b1 = lds[par][wb][0][1][lane];
-      A[0] = a0.x; A[1] = a0.y; A[2] = a0.z; A[3] = a0.w; A[4] = a1.x; A[5] = a1.y; A[6] = a1.z; A[7] = a1.w;
-      B[0] = b0.x; B[1] = b0.y; B[2] = b0.z; B[3] = b0.w; B[4] = b1.x; B[5] = b1.y; B[6] = b1.z; B[7] = b1.w;
-    }
-    u16x2 Hc[8], Sc[8];
-    {
-      u16x2 Ha[8];
-      horiz_pairs<CH>(A, two, Ha);
-      horiz_pairs<CH>(D[0], two, Hc);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) Sc[k] = Ha[k] + Hc[k];
-    }
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      u16x2 Hn[8];
-      if (i + 1 < M)
-        horiz_pairs<CH>(D[i + 1], two, Hn);
-      else
-        horiz_pairs<CH>(B, two, Hn);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const u16x2 Sn = Hc[k] + Hn[k];
-        D[i][k] = as_u((Sc[k] + Sn) >> (u16x2){4, 4});
-        Sc[k] = Sn;
-        Hc[k] = Hn[k];
-      }
-    }
-    // zero padding: rows and columns outside the image stay zero
-    if (edge_strip) {
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) D[i][k] &= cmask[k];
-    }
-    if (out_top > 0 || out_bot < M) {
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-        if (i < out_top || i >= out_bot)
-#pragma unroll
-          for (int k = 0; k < 8; ++k) D[i][k] = 0;
-    }
-  }
-
-  // ---- store the valid rows / lanes
-  const bool lane_ok = col_in && lane >= hl && lane < 64 - hl;
-  const int st_lo = max(tile_r0, r0), st_hi = min(min(tile_r0 + vrows, r1), height - g_row0);
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    const int fr = row_base + i;
-    if (lane_ok && fr >= st_lo && fr < st_hi) {
-      const u32 t0 = perm(D[i][1], D[i][0], 0x06020400u);
-      const u32 t1 = perm(D[i][3], D[i][2], 0x06020400u);
-      const u32 t2 = perm(D[i][5], D[i][4], 0x06020400u);
-      const u32 t3 = perm(D[i][7], D[i][6], 0x06020400u);
-      uint4 o;
-      o.x = perm(t1, t0, 0x05040100u);
-      o.y = perm(t3, t2, 0x05040100u);
-      o.z = perm(t1, t0, 0x07060302u);
-      o.w = perm(t3, t2, 0x07060302u);
-      *reinterpret_cast<uint4*>(dst + static_cast<int64_t>(fr) * pitch + x) = o;
-    }
-  }
-}
-
-// Temporal tile shapes (rows per wave M, waves per tile NW).
-struct TemporalShape {
-  int m, nw;
-};
-
-template <int CH>
-void launch_temporal(const StencilLaunch& a, hipStream_t s, TemporalShape sh) {
-  const int steps = a.steps;
-  const int hl = (steps * CH + 15) / 16;
-  const int vlanes = 64 - 2 * hl;
-  const int nchunks = static_cast<int>(ceil_div<int64_t>(a.row_bytes, 16));
-  const int vrows = sh.m * sh.nw - 2 * steps;
-  PCONV_CHECK(vlanes > 0 && vrows > 0, "temporal kernel: steps too large for the tile");
-  const dim3 grid(ceil_div(nchunks, vlanes), ceil_div(static_cast<int>(a.r1 - a.r0), vrows));
-  const u32 two = 0x00020002u;
-  const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
-#define PCONV_TEMPORAL(M_, NW_)                                                                                 \
-  if (sh.m == M_ && sh.nw == NW_) {                                                                             \
-    k_temporal<CH, M_, NW_><<<grid, dim3(64 * NW_), 0, s>>>(a.src, a.dst, a.pitch, static_cast<int>(a.row_bytes), \
-                                                            static_cast<int>(a.r0), static_cast<int>(a.r1), steps, \
-                                                            static_cast<int>(a.g_row0), static_cast<int>(hmax), two); \
-    return;                                                                                                     \
-  }
-  PCONV_TEMPORAL(8, 4)
-  PCONV_TEMPORAL(8, 8)
-  PCONV_TEMPORAL(12, 4)
-  PCONV_TEMPORAL(16, 4)
-#undef PCONV_TEMPORAL
-  PCONV_FAIL("temporal kernel: unsupported tile shape");
-}
-
-// Tile shape: smallest tile whose halo overhead is acceptable for `steps`.
-TemporalShape pick_temporal_shape(int steps) {
-  if (steps <= 4) return {8, 4};    // 32-row tile, >= 24 valid
-  if (steps <= 8) return {8, 8};    // 64-row tile, >= 48 valid
-  return {16, 4};                   // 64-row tile, >= 32 valid
-}
-
 constexpr int kRowsPerLane = 4;
 
 template <int CH>
@@ -466,7 +260,6 @@ const char* kernel_variant_name(KernelVariant v) {
     case KernelVariant::Temporal: return "temporal";
     case KernelVariant::Int9: return "int9";
     case KernelVariant::Float9: return "float9";
-    case KernelVariant::TemporalPk: return "temporal_pk";
     case KernelVariant::FloatTemporal: return "float_temporal";
   }
   return "?";
@@ -474,7 +267,7 @@ const char* kernel_variant_name(KernelVariant v) {
 
 bool supports_fusion(const Filter& f, KernelVariant v) {
   if (f.binomial121)
-    return v == KernelVariant::Auto || v == KernelVariant::Temporal || v == KernelVariant::TemporalPk;
+    return v == KernelVariant::Auto || v == KernelVariant::Temporal;
   // any other filter: the float temporal kernel (reference float32 semantics)
   return v == KernelVariant::Auto || v == KernelVariant::FloatTemporal;
 }
@@ -535,22 +328,13 @@ void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hip
   }
   PCONV_CHECK(!own_dst_pitch || (v == KernelVariant::Temporal && a.dst_pitch >= a.row_bytes && a.dst_pitch % 4 == 0),
               "launch_stencil: a separate destination pitch needs the SWAR temporal kernel");
-  PCONV_CHECK(a.steps == 1 || v == KernelVariant::Temporal || v == KernelVariant::TemporalPk,
+  PCONV_CHECK(a.steps == 1 || v == KernelVariant::Temporal,
               "launch_stencil: fused steps not supported by kernel '" + std::string(kernel_variant_name(v)) + "'");
-  if (v == KernelVariant::Temporal || v == KernelVariant::TemporalPk) {
+  if (v == KernelVariant::Temporal) {
     PCONV_CHECK(f.binomial121, "temporal kernel requires the gaussian filter");
     PCONV_CHECK(a.steps <= kMaxFusedSteps, "temporal kernel: too many fused steps");
     PCONV_CHECK(a.height < (int64_t(1) << 30) && a.g_row0 < (int64_t(1) << 30), "temporal kernel: rows exceed 2^30");
-    if (v == KernelVariant::Temporal) {
-      launch_swar(a, ch, stream);
-    } else {
-      const TemporalShape sh = pick_temporal_shape(a.steps);
-      switch (ch) {
-        case Channels::Grey: launch_temporal<1>(a, stream, sh); break;
-        case Channels::Rgb: launch_temporal<3>(a, stream, sh); break;
-        case Channels::Rgba: launch_temporal<4>(a, stream, sh); break;
-      }
-    }
+    launch_swar(a, ch, stream);
     PCONV_HIP_CHECK(hipGetLastError());
     return;
   }

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -239,14 +240,15 @@ struct FtShape {
 // full.  Fits the sweep (gpurun_out/r03/g/float_sweep.jsonl): 1920x2520 RGB
 // at 4 steps -> 16x8 (252 workgroups: 8.0 us/rep, best), at 8 steps -> 16x4
 // (9.5, best 9.5); grey at 8 steps -> 16x4 (3.6, best 3.5); 8192^2 RGB ->
-// 16x8 (best).  PCONV_FLOAT_SHAPE="M,NW" forces one.
+// 16x8 (best).  set_float_shape(M, NW) forces one.
+std::atomic<int> g_ft_force_m{0}, g_ft_force_nw{0};
+
 FtShape pick_ft_shape(int steps, int ch, int64_t rows, int64_t row_bytes) {
   static const FtShape cands[] = {{16, 8}, {16, 4}, {8, 8}, {8, 4}, {4, 8}};  // largest tiles first
-  if (const char* e = std::getenv("PCONV_FLOAT_SHAPE")) {
-    int m = 0, nw = 0;
-    if (std::sscanf(e, "%d,%d", &m, &nw) == 2)
-      for (const auto& c : cands)
-        if (c.m == m && c.nw == nw) return c;
+  if (const int fm = g_ft_force_m.load(std::memory_order_relaxed)) {
+    const int fnw = g_ft_force_nw.load(std::memory_order_relaxed);
+    for (const auto& c : cands)
+      if (c.m == fm && c.nw == fnw) return c;
   }
   static int cus = [] {
     int dev = 0, n = 0;
@@ -331,7 +333,7 @@ bool capturing_ft(hipStream_t s) {
 template <int CH, bool UNIFORM>
 FtShape tuned_ft_shape(const StencilLaunch& a, const FloatTaps& tp, hipStream_t s) {
   const FtShape model = pick_ft_shape(a.steps, CH, a.r1 - a.r0, a.row_bytes);
-  if (std::getenv("PCONV_FLOAT_SHAPE") || !shape_tuning_enabled()) return model;
+  if (g_ft_force_m.load(std::memory_order_relaxed) || !shape_tuning_enabled()) return model;
   const FtKey key{CH, UNIFORM, a.steps, a.r1 - a.r0, a.row_bytes};
   {
     std::lock_guard<std::mutex> lk(g_ft_mu);
@@ -408,6 +410,11 @@ void launch_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a,
 
 void prepare_float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream) {
   float_temporal(f, ch, a, stream, false);
+}
+
+void set_float_shape(int m, int nw) {
+  g_ft_force_m.store(m > 0 ? m : 0, std::memory_order_relaxed);
+  g_ft_force_nw.store(m > 0 ? nw : 0, std::memory_order_relaxed);
 }
 
 void clear_float_tuning() {

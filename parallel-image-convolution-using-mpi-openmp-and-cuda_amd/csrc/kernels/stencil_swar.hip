@@ -152,32 +152,24 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
   }
 }
 
-// Buffer-op form of k_swar (4-byte lanes), optionally persistent.
+// Buffer-op form of k_swar (4-byte lanes), one workgroup per tile.
 //   Every row load and store is a raw buffer op; rows and lanes outside the
 // frame get an offset past the descriptor's range, so the hardware returns
 // zeros / drops the store instead of the branches k_swar takes around each
-// chunk, and every wave issues exactly 2M loads and 2M stores per tile.  One
-// workgroup per tile is the form the tuner times against k_swar (4-8 %
-// faster on RGB frames, e.g. the headline 3.47 -> 3.19 us/rep; slower on
-// grey ones, where its ALT form needs far more VGPRs:
-// profiles/r02/prefetch_kernel.md).
-//   Persistent form (opt-in, set_prefetch_mode(mode, cap != 0)): a resident
-// grid in which each workgroup walks a run of tiles and issues the NEXT
-// tile's row loads before the current tile's steps (the steps' barriers wait
-// on LDS only, s_waitcnt lgkmcnt), the loop rotated so the next tile is
-// unpacked right after this tile's stores (the compiler's wait there is
-// vmcnt(2M): the loads, not the stores still draining; gfx950 counts both in
-// vmcnt, in issue order).  Tiles are dealt to the 8 XCDs in contiguous runs
-// (workgroup b runs on XCD b % 8).  Measured 10-40 % SLOWER than relaunching
-// k_swar on 32768^2 grey (one workgroup per CU at the prefetch's VGPR cost
-// leaves the per-step barrier bubbles unhidden), so the tuner never picks it.
+// chunk, and every wave issues exactly 2M loads and 2M stores per tile.  The
+// tuner times it against k_swar (4-8 % faster on RGB frames, e.g. the
+// headline 3.47 -> 3.19 us/rep; slower on grey ones, where its ALT form needs
+// far more VGPRs: profiles/r02/prefetch_kernel.md).  A persistent form that
+// walked several tiles per workgroup with the next tile's loads in flight
+// measured 10-40 % slower on 32768^2 grey and was removed (round 5; numbers
+// in docs/PERFORMANCE.md).
 //   Contract (checked at launch): row_bytes % 4 == 0, source and destination
 // ranges under 2 GiB.
 template <int CH, int M, int NW, bool ALT>
 __global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                      int pitch, int dst_pitch, int row_bytes, int r0, int r1,
                                                      int steps, int g_row0, int height, int nstrips, int pair_stride,
-                                                     int row_tiles) {
+                                                     int row_tiles, int xcd_swizzle) {
   constexpr int LW = 4, NP = 4, NQ = 1;
   constexpr u32 kOut = 0x80000000u;  // offset past every descriptor's range
   __shared__ uint4 lds[2][NW][2][NQ][64];
@@ -193,97 +185,61 @@ __global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__
       const_cast<uint8_t*>(src) + static_cast<int64_t>(lo_ok) * pitch, 0, max(hi_ok - lo_ok, 0) * pitch, 0x00020000);
   const auto drsrc = __builtin_amdgcn_make_buffer_rsrc(dst + static_cast<int64_t>(r0) * dst_pitch, 0,
                                                        max(st_end - r0, 0) * dst_pitch, 0x00020000);
-
-  const int ntiles = pair_stride * row_tiles;
-  const int nwg = static_cast<int>(gridDim.x), b = static_cast<int>(blockIdx.x);
-  // With fewer than 8 workgroups only XCDs 0..nwg-1 hold one: the tiles are
-  // split over those.
-  const int nx = min(nwg, 8);
-  const int xcd = b & 7, local = b >> 3;
-  const int t_step = (nwg - xcd + 7) >> 3;  // workgroups on this XCD
-  const int t_end = static_cast<int>((int64_t(xcd) + 1) * ntiles / nx);
-  int tile = static_cast<int>(int64_t(xcd) * ntiles / nx) + local;
-  if (tile >= t_end) return;  // whole workgroup (uniform)
-
-  // Per tile: lane byte offsets of strips A / B (or kOut), first frame row of
-  // this wave, and whether edge columns need masking.
-  int xA, xB, row_base;
-  bool needs_mask;
-  auto geo = [&](int t, int& ga, int& gb, int& grow, bool& gmask) {
-    const int col = t / row_tiles, rtile = t - col * row_tiles;
-    const int sB = col + pair_stride;
-    const int baseA = col * vbytes - hl * LW, baseB = sB * vbytes - hl * LW;
-    const int pa = baseA + lane * LW, pb = baseB + lane * LW;
-    ga = (pa >= 0 && pa < row_bytes) ? pa : -1;
-    gb = (sB < nstrips && pb >= 0 && pb < row_bytes) ? pb : -1;
-    gmask = baseA < 0 || baseA + 64 * LW > row_bytes || sB >= nstrips || baseB + 64 * LW > row_bytes;
-    grow = r0 + rtile * vrows - steps + w * M;
-  };
-  u32 pa[M], pb[M];
-  auto fetch = [&](int ga, int gb, int grow) {
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      const int fr = grow + i;
-      const bool rok = fr >= lo_ok && fr < hi_ok;
-      const u32 ro = static_cast<u32>(fr - lo_ok) * static_cast<u32>(pitch);
-      pa[i] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, (rok && ga >= 0) ? ro + ga : kOut, 0, 0);
-      pb[i] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, (rok && gb >= 0) ? ro + gb : kOut, 0, 0);
-    }
-  };
-  geo(tile, xA, xB, row_base, needs_mask);
-  fetch(xA, xB, row_base);
+  // XCD-aware tile order (as k_swar): each XCD gets one contiguous run of
+  // tiles walked down a column strip, so vertically adjacent tiles (which
+  // read each other's halo rows) share an L2.
+  int tile = static_cast<int>(blockIdx.x);
+  if (xcd_swizzle) {
+    const int nwg = static_cast<int>(gridDim.x);
+    const int q = nwg >> 3, rem = nwg & 7, xcd = tile & 7, local = tile >> 3;
+    tile = xcd * q + min(xcd, rem) + local;
+  }
+  const int col = tile / row_tiles, rtile = tile - col * row_tiles;
+  const int sB = col + pair_stride;
+  const int baseA = col * vbytes - hl * LW, baseB = sB * vbytes - hl * LW;
+  const int pa0 = baseA + lane * LW, pb0 = baseB + lane * LW;
+  const int xA = (pa0 >= 0 && pa0 < row_bytes) ? pa0 : -1;
+  const int xB = (sB < nstrips && pb0 >= 0 && pb0 < row_bytes) ? pb0 : -1;
+  const bool needs_mask = baseA < 0 || baseA + 64 * LW > row_bytes || sB >= nstrips || baseB + 64 * LW > row_bytes;
+  const int row_base = r0 + rtile * vrows - steps + w * M;
   u32 D[M][NP];
 #pragma unroll
-  for (int i = 0; i < M; ++i) unpack<NP>(pa[i], pb[i], D[i]);
-  while (true) {
-    const int next = tile + t_step;
-    const bool more = next < t_end;
-    int nA = -1, nB = -1, nrow = 0;
-    bool nmask = false;
-    if (more) {  // wave-uniform; never taken with one workgroup per tile
-      geo(next, nA, nB, nrow, nmask);
-      fetch(nA, nB, nrow);  // in flight during this tile's steps
-    }
-    u32 cm[NP];
+  for (int i = 0; i < M; ++i) {
+    const int fr = row_base + i;
+    const bool rok = fr >= lo_ok && fr < hi_ok;
+    const u32 ro = static_cast<u32>(fr - lo_ok) * static_cast<u32>(pitch);
+    const u32 a = __builtin_amdgcn_raw_buffer_load_b32(srsrc, (rok && xA >= 0) ? ro + xA : kOut, 0, 0);
+    const u32 b = __builtin_amdgcn_raw_buffer_load_b32(srsrc, (rok && xB >= 0) ? ro + xB : kOut, 0, 0);
+    unpack<NP>(a, b, D[i]);
+  }
+  u32 cm[NP];
 #pragma unroll
-    for (int k = 0; k < NP; ++k)
-      cm[k] = (xA >= 0 && xA + k < row_bytes ? 0xffffu : 0u) | (xB >= 0 && xB + k < row_bytes ? 0xffff0000u : 0u);
-    const int out_top = min(max(-g_row0 - row_base, 0), M);
-    const int out_bot = min(max(height - g_row0 - row_base, 0), M);
-    if constexpr (ALT) {
-      int s = 0;
-      for (; s + 2 <= steps; s += 2) {
-        swar_step<CH, NP, M, NW, 1>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
-        swar_step<CH, NP, M, NW, 2>(D, lds, 1, w, lane, needs_mask, cm, out_top, out_bot);
-      }
-      if (s < steps) swar_step<CH, NP, M, NW, 0>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
-    } else {
-      for (int s = 0; s < steps; ++s) swar_step<CH, NP, M, NW, 0>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
+  for (int k = 0; k < NP; ++k)
+    cm[k] = (xA >= 0 && xA + k < row_bytes ? 0xffffu : 0u) | (xB >= 0 && xB + k < row_bytes ? 0xffff0000u : 0u);
+  const int out_top = min(max(-g_row0 - row_base, 0), M);
+  const int out_bot = min(max(height - g_row0 - row_base, 0), M);
+  if constexpr (ALT) {
+    int s = 0;
+    for (; s + 2 <= steps; s += 2) {
+      swar_step<CH, NP, M, NW, 1>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+      swar_step<CH, NP, M, NW, 2>(D, lds, 1, w, lane, needs_mask, cm, out_top, out_bot);
     }
-    const bool lane_in = lane >= hl && lane < 64 - hl;
-    const int tile_r0 = row_base + steps - w * M;
-    const int st_lo = max(tile_r0, r0), st_hi = min(tile_r0 + vrows, st_end);
+    if (s < steps) swar_step<CH, NP, M, NW, 0>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+  } else {
+    for (int s = 0; s < steps; ++s) swar_step<CH, NP, M, NW, 0>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
+  }
+  const bool lane_in = lane >= hl && lane < 64 - hl;
+  const int tile_r0 = row_base + steps - w * M;
+  const int st_lo = max(tile_r0, r0), st_hi = min(tile_r0 + vrows, st_end);
 #pragma unroll
-    for (int i = 0; i < M; ++i) {
-      const int fr = row_base + i;
-      const bool rst = fr >= st_lo && fr < st_hi;
-      const u32 ro = static_cast<u32>(fr - r0) * static_cast<u32>(dst_pitch);
-      u32 a, bb;
-      pack<NP>(D[i], a, bb);
-      __builtin_amdgcn_raw_buffer_store_b32(a, drsrc, (rst && lane_in && xA >= 0) ? ro + xA : kOut, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(bb, drsrc, (rst && lane_in && xB >= 0) ? ro + xB : kOut, 0, 0);
-    }
-    if (!more) break;
-    tile = next;
-    xA = nA;
-    xB = nB;
-    row_base = nrow;
-    needs_mask = nmask;
-#pragma unroll
-    for (int i = 0; i < M; ++i) unpack<NP>(pa[i], pb[i], D[i]);
-    // The next tile's first step overwrites LDS parity 0, which the slowest
-    // wave of this tile may still be reading (its last step's boundary rows).
-    __syncthreads();
+  for (int i = 0; i < M; ++i) {
+    const int fr = row_base + i;
+    const bool rst = fr >= st_lo && fr < st_hi;
+    const u32 ro = static_cast<u32>(fr - r0) * static_cast<u32>(dst_pitch);
+    u32 a, bb;
+    pack<NP>(D[i], a, bb);
+    __builtin_amdgcn_raw_buffer_store_b32(a, drsrc, (rst && lane_in && xA >= 0) ? ro + xA : kOut, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(bb, drsrc, (rst && lane_in && xB >= 0) ? ro + xB : kOut, 0, 0);
   }
 }
 
@@ -296,29 +252,16 @@ constexpr SwarShape kShapes[] = {
     {4, 20, 8},
 };
 
-std::atomic<int> g_xcd_swizzle{-1};  // -1: from PCONV_XCD_SWIZZLE on first use (default on)
+// Process-wide kernel settings (set_xcd_swizzle / set_swar_alt /
+// set_prefetch_mode / set_swar_shape / set_autotune / set_tune_candidates;
+// no environment variables).
+std::atomic<int> g_xcd_swizzle{1};  // XCD-aware tile order (neutral +-2 %, kept on)
 
-bool xcd_swizzle_enabled() {
-  int v = g_xcd_swizzle.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = std::getenv("PCONV_XCD_SWIZZLE");
-    v = (e && e[0] == '0') ? 0 : 1;
-    g_xcd_swizzle.store(v, std::memory_order_relaxed);
-  }
-  return v != 0;
-}
+bool xcd_swizzle_enabled() { return g_xcd_swizzle.load(std::memory_order_relaxed) != 0; }
 
-std::atomic<int> g_alt_mode{-2};  // -2: PCONV_SWAR_ALT on first use; -1 tune, 0 off, 1 on
+std::atomic<int> g_alt_mode{-1};  // -1 tune, 0 off, 1 on
 
-int alt_mode() {
-  int v = g_alt_mode.load(std::memory_order_relaxed);
-  if (v == -2) {
-    const char* e = std::getenv("PCONV_SWAR_ALT");
-    v = !e ? -1 : e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
-    g_alt_mode.store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
+int alt_mode() { return g_alt_mode.load(std::memory_order_relaxed); }
 
 // Step form when nothing was tuned (graph capture, autotune off): the paired
 // form is faster in most measured geometries.
@@ -380,8 +323,7 @@ void launch_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh, bool alt) {
   PCONV_FAIL("swar temporal kernel: unsupported tile shape");
 }
 
-// Persistent prefetching launches (k_swar_pf): shapes instantiated, and the
-// grid = resident workgroups (occupancy x CUs), never more than the tiles.
+// Buffer-op tile kernel (k_swar_pf): shapes instantiated.
 constexpr SwarShape kPfShapes[] = {
     {4, 8, 8}, {4, 12, 4}, {4, 16, 4}, {4, 12, 8}, {4, 16, 8}, {4, 20, 8},
 };
@@ -392,49 +334,9 @@ bool known_pf_shape(const SwarShape& s) {
   return false;
 }
 
-std::atomic<int> g_pf_mode{-2};  // -2: PCONV_PREFETCH on first use; -1 tune, 0 off, 1 forced
-// 0: one workgroup per tile (the tuned form); < 0: persistent, the resident
-// workgroup count (A/B); > 0: persistent, at most this many (tests: many
-// tiles per workgroup)
-std::atomic<int> g_pf_grid_cap{0};
+std::atomic<int> g_pf_mode{-1};  // -1 tune, 0 off, 1 forced
 
-int pf_mode() {
-  int v = g_pf_mode.load(std::memory_order_relaxed);
-  if (v == -2) {
-    const char* e = std::getenv("PCONV_PREFETCH");
-    v = !e ? -1 : e[0] == '0' ? 0 : e[0] == '1' ? 1 : -1;
-    g_pf_mode.store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
-
-template <int CH, int M, int NW>
-const void* pf_fn(bool alt) {
-  return alt ? reinterpret_cast<const void*>(&k_swar_pf<CH, M, NW, true>)
-             : reinterpret_cast<const void*>(&k_swar_pf<CH, M, NW, false>);
-}
-
-int cu_count() {
-  int dev = 0, n = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-    (void)hipGetLastError();
-    return 256;
-  }
-  return n > 0 ? n : 256;
-}
-
-int pf_resident_wgs(const void* fn, int threads) {
-  static std::mutex mu;
-  static std::map<const void*, int> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find(fn);
-  if (it != cache.end()) return it->second;
-  int per_cu = 0;
-  PCONV_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0));
-  const int n = std::max(1, per_cu) * cu_count();
-  cache.emplace(fn, n);
-  return n;
-}
+int pf_mode() { return g_pf_mode.load(std::memory_order_relaxed); }
 
 // Launches the prefetch kernel can take: 4-byte lanes, whole dwords per row,
 // source and destination ranges under 2 GiB (32-bit buffer offsets).
@@ -456,23 +358,18 @@ void launch_pf_one(const StencilLaunch& a, hipStream_t s, bool alt) {
   const int row_tiles = ceil_div(static_cast<int>(a.r1 - a.r0), vrows);
   const int64_t ntiles = int64_t(pair_stride) * row_tiles;
   PCONV_CHECK(ntiles < (int64_t(1) << 31), "swar prefetch kernel: too many tiles");
-  const int cap = g_pf_grid_cap.load(std::memory_order_relaxed);
-  int64_t wgs = ntiles;
-  if (cap != 0) {
-    wgs = pf_resident_wgs(pf_fn<CH, M, NW>(alt), 64 * NW);
-    if (cap > 0) wgs = std::min<int64_t>(wgs, cap);
-  }
-  const int grid = static_cast<int>(std::min<int64_t>(ntiles, wgs));
+  const int grid = static_cast<int>(ntiles);
+  const int xs = xcd_swizzle_enabled() ? 1 : 0;
   const int hmax = static_cast<int>(std::min<int64_t>(a.height, int64_t(1) << 30));
   const int dp = static_cast<int>(a.dst_pitch ? a.dst_pitch : a.pitch);
   if (alt)
     k_swar_pf<CH, M, NW, true><<<dim3(grid), dim3(64 * NW), 0, s>>>(
         a.src, a.dst, static_cast<int>(a.pitch), dp, static_cast<int>(a.row_bytes), static_cast<int>(a.r0),
-        static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), hmax, nstrips, pair_stride, row_tiles);
+        static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), hmax, nstrips, pair_stride, row_tiles, xs);
   else
     k_swar_pf<CH, M, NW, false><<<dim3(grid), dim3(64 * NW), 0, s>>>(
         a.src, a.dst, static_cast<int>(a.pitch), dp, static_cast<int>(a.row_bytes), static_cast<int>(a.r0),
-        static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), hmax, nstrips, pair_stride, row_tiles);
+        static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), hmax, nstrips, pair_stride, row_tiles, xs);
 }
 
 // Tiles of a launch and the workgroups the prefetch kernel keeps resident.
@@ -502,25 +399,13 @@ bool known_shape(const SwarShape& s) {
   return false;
 }
 
-// Shape override (tuning / tests): set_swar_shape(), initialised once from
-// PCONV_SWAR_SHAPE="lw,m,nw".
+// Shape override (tuning / tests): set_swar_shape().
 std::mutex g_shape_mu;
-bool g_shape_init = false;
 bool g_have_shape = false;
 SwarShape g_shape;
 
 bool override_shape(SwarShape& out) {
   std::lock_guard<std::mutex> lk(g_shape_mu);
-  if (!g_shape_init) {
-    g_shape_init = true;
-    if (const char* e = std::getenv("PCONV_SWAR_SHAPE")) {
-      SwarShape s;
-      if (std::sscanf(e, "%d,%d,%d", &s.lw, &s.m, &s.nw) == 3 && known_shape(s)) {
-        g_shape = s;
-        g_have_shape = true;
-      }
-    }
-  }
   if (g_have_shape) out = g_shape;
   return g_have_shape;
 }
@@ -529,7 +414,6 @@ bool override_shape(SwarShape& out) {
 
 void set_swar_shape(int lw, int m, int nw) {
   std::lock_guard<std::mutex> lk(g_shape_mu);
-  g_shape_init = true;
   if (lw == 0) {
     g_have_shape = false;
     return;
@@ -624,10 +508,7 @@ KernelRes kernel_res(SwarShape sh, int ch, bool alt) {
 // best shape in 6 of 6 configurations of the current kernel.
 void set_xcd_swizzle(bool on) { g_xcd_swizzle.store(on ? 1 : 0, std::memory_order_relaxed); }
 void set_swar_alt(int mode) { g_alt_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
-void set_prefetch_mode(int mode, int grid_cap) {
-  g_pf_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed);
-  g_pf_grid_cap.store(grid_cap, std::memory_order_relaxed);
-}
+void set_prefetch_mode(int mode) { g_pf_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
 std::vector<SwarShape> swar_prefetch_shapes() { return std::vector<SwarShape>(std::begin(kPfShapes), std::end(kPfShapes)); }
 
 SwarResources swar_resources(SwarShape s, int ch) {
@@ -717,24 +598,16 @@ struct TuneKey {
 };
 std::mutex g_tune_mu;
 std::map<TuneKey, SwarChoice> g_tuned;
-std::atomic<int> g_autotune{-1};
+std::atomic<int> g_autotune{1};
+std::atomic<int> g_tune_candidates{6};  // model-ranked shapes timed per launch geometry
 
-bool autotune_enabled() {
-  int v = g_autotune.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = std::getenv("PCONV_AUTOTUNE");
-    v = (e && e[0] == '0') ? 0 : 1;
-    g_autotune.store(v, std::memory_order_relaxed);
-  }
-  return v != 0;
-}
+bool autotune_enabled() { return g_autotune.load(std::memory_order_relaxed) != 0; }
 
 bool capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
 }
 
-constexpr int kTuneCandidates = 6;
 constexpr int kTuneRepeats = 3;
 constexpr int kTunePasses = 2;
 
@@ -786,8 +659,8 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   }
   PCONV_CHECK(!ranked.empty(), "swar temporal kernel: steps too large for every tile shape");
   std::sort(ranked.begin(), ranked.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-  size_t keep = kTuneCandidates;  // PCONV_TUNE_CANDIDATES widens the timed set (A/B of the model's ranking)
-  if (const char* e = std::getenv("PCONV_TUNE_CANDIDATES")) keep = static_cast<size_t>(std::max(1, std::atoi(e)));
+  // set_tune_candidates widens the timed set (A/B of the model's ranking)
+  const size_t keep = static_cast<size_t>(std::max(1, g_tune_candidates.load(std::memory_order_relaxed)));
   if (ranked.size() > keep) ranked.resize(keep);
   std::vector<SwarChoice> cands;
   for (const auto& r : ranked)
@@ -834,6 +707,7 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
 }  // namespace
 
 void set_autotune(bool on) { g_autotune.store(on ? 1 : 0, std::memory_order_relaxed); }
+void set_tune_candidates(int n) { g_tune_candidates.store(std::max(1, n), std::memory_order_relaxed); }
 bool set_shape_tuning(bool on) {
   const bool prev = autotune_enabled();
   set_autotune(on);

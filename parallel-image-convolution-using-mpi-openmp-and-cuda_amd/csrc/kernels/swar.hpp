@@ -21,13 +21,15 @@ double swar_launch_cycles(SwarShape s, int steps, int ch, int64_t rows, int64_t 
 SwarShape pick_swar_shape(int steps, int ch, int64_t rows, int64_t row_bytes);
 
 // Enqueue the fused gaussian for `a.steps` repetitions.  Shape: forced
-// (PCONV_SWAR_SHAPE="lw,m,nw" / set_swar_shape), else tuned on first use
-// (the model's best candidates timed on this launch; PCONV_AUTOTUNE=0: model
-// only), else the model's pick while a graph is being captured.
+// (set_swar_shape), else tuned on first use (the model's best candidates
+// timed on this launch; set_autotune(false): model only), else the model's
+// pick while a graph is being captured.
 void launch_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
 // Tune (if needed) without enqueueing the launch — before a graph capture.
 void prepare_swar(const StencilLaunch& a, Channels ch, hipStream_t stream);
 void set_autotune(bool on);
+// How many of the model's best shapes the tuner times (default 6).
+void set_tune_candidates(int n);
 void clear_swar_tuning();
 // Tuned entries: ({channels, steps, rows, row_bytes, paired_form, prefetch}, shape); prefetch = 1: the
 // buffer-op tile kernel k_swar_pf won.
@@ -44,18 +46,15 @@ struct SwarResources {
   bool measured = false;
 };
 SwarResources swar_resources(SwarShape s, int ch);
-// XCD-aware tile order of the SWAR kernel (default on; PCONV_XCD_SWIZZLE=0).
+// XCD-aware tile order of the SWAR kernels (default on).
 void set_xcd_swizzle(bool on);
 // Step form: -1 tuned per launch geometry (default), 0 truncate every step,
-// 1 steps in pairs with a scale-16 intermediate (PCONV_SWAR_ALT=0/1).
+// 1 steps in pairs with a scale-16 intermediate.
 void set_swar_alt(int mode);
 // Buffer-op tile kernel (k_swar_pf): -1 among the tuned candidates
-// (default), 0 never, 1 forced (PCONV_PREFETCH=-1/0/1); with the mode forced,
-// a shape set by set_swar_shape that it instantiates is used as is (tests).
-// grid_cap 0: one workgroup per tile (the tuned form); < 0: persistent
-// workgroups (the resident count) walking tiles with the next tile's loads
-// in flight; > 0: persistent, at most that many workgroups (tests).
-void set_prefetch_mode(int mode, int grid_cap = 0);
+// (default), 0 never, 1 forced; with the mode forced, a shape set by
+// set_swar_shape that it instantiates is used as is (tests).
+void set_prefetch_mode(int mode);
 std::vector<SwarShape> swar_prefetch_shapes();
 
 }  // namespace pconv

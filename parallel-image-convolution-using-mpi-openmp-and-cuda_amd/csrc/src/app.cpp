@@ -218,20 +218,10 @@ void delete_job_cache(JobCache* c) { delete c; }
 
 namespace {
 
-// Ring staging of large one-shot images (run_gpu1).  PCONV_RING=0 turns it
-// off (A/B); PCONV_RING_CHUNK_BYTES sets the chunk (tests use small ones).
+// Ring staging of large one-shot images (run_gpu1): kRingSlots pinned
+// chunks of CliConfig::ring_chunk_bytes (--ring-chunk-bytes; 0 = one pinned
+// copy of the whole image).
 constexpr int kRingSlots = 3;
-
-int64_t ring_chunk_bytes() {
-  const char* v = std::getenv("PCONV_RING_CHUNK_BYTES");
-  const int64_t b = v && *v ? std::strtoll(v, nullptr, 10) : 0;
-  return b > 0 ? b : int64_t(32) << 20;
-}
-
-bool ring_staging_enabled() {
-  const char* v = std::getenv("PCONV_RING");
-  return !(v && v[0] == '0');
-}
 
 AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   AppReport r;
@@ -248,12 +238,10 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
     pc.mark("hip_init");
     // The kernels' code object (~6 ms to load on first use) loads on a helper
     // thread while this one allocates staging, reads the image and creates
-    // the first hardware queue (~20 ms).  PCONV_PRELOAD=0 disables (A/B).
-    const char* pe = std::getenv("PCONV_PRELOAD");
-    if (!(pe && pe[0] == '0'))
-      preload = std::thread([device] {
-        if (hipSetDevice(device) == hipSuccess) preload_kernel_module();
-      });
+    // the first hardware queue (~20 ms).
+    preload = std::thread([device] {
+      if (hipSetDevice(device) == hipSuccess) preload_kernel_module();
+    });
   }
   struct Joiner {
     std::thread& t;
@@ -263,17 +251,17 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   } join_preload{preload};
   // One-shot process: the model's tile shape, no timing of candidates (2-4 ms
   // of tuning launches against a 0.03-0.7 ms loop; profiles/r02/raw/startup/
-  // cli_modes.jsonl).  PCONV_AUTOTUNE in the environment keeps its setting.
+  // cli_modes.jsonl) unless --tune on; a resident server tunes unless
+  // --tune off.
   struct TuneScope {
     bool active = false, prev = true;
     ~TuneScope() {
       if (active) (void)set_shape_tuning(prev);
     }
   } tune_scope;
-  if (!cache && !std::getenv("PCONV_AUTOTUNE")) {
-    tune_scope.active = true;
-    tune_scope.prev = set_shape_tuning(false);
-  }
+  const bool tune = c.tune < 0 ? cache != nullptr : c.tune == 1;
+  tune_scope.active = true;
+  tune_scope.prev = set_shape_tuning(tune);
   // Large one-shot images go through a small ring of pinned chunks instead
   // of one pinned copy of the whole image: pinning costs ~0.24 ms per MB
   // (32768^2 grey: 0.244 s of a 0.69 s run, profiles/r04/trace20/), and the
@@ -283,8 +271,8 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
   // --check / checkpoints (they need the whole result in host memory) and for
   // the resident server (its staging is allocated once).
   const int64_t rb = g.row_bytes();
-  const int64_t ring_rows = std::max<int64_t>(1, ring_chunk_bytes() / rb);
-  const bool ring = !cache && !c.check && c.checkpoint_every == 0 && ring_staging_enabled() &&
+  const int64_t ring_rows = std::max<int64_t>(1, c.ring_chunk_bytes / rb);
+  const bool ring = !cache && !c.check && c.checkpoint_every == 0 && c.ring_chunk_bytes > 0 &&
                     g.height > (kRingSlots - 1) * ring_rows;  // >= kRingSlots chunks
   PinnedBuffer own_host;
   uint8_t* host = nullptr;
@@ -406,26 +394,18 @@ AppReport run_gpu1(const CliConfig& c, JobCache* cache) {
 // context, first queue; BASELINE.md phase tables) before its first kernel,
 // while one repetition of a 1920x2520 RGB frame takes ~0.5 ms on the
 // node's CPUs.  So the job is priced on the CPU first:
-//   * stage 1, a <= 256-row sample: above kAutoGpuMinS the GPU path runs the
-//     job alone (the host never holds the image twice);
+//   * stage 1, a <= 256-row sample: above CliConfig::auto_gpu_min_s
+//     (--auto-gpu-min, default 0.1 s) the GPU path runs the job alone (the
+//     host never holds the image twice);
 //   * stage 2, the whole frame on the host: the first repetition is real
 //     work and re-prices the job at memory speed; if the rest is still worth
 //     a GPU it goes there, otherwise the CPU finishes without any HIP call
 //     (no driver open, no teardown wait for the next process).
-// PCONV_AUTO_HANDOFF=1 instead brings the GPU up on a helper thread while
-// the CPU keeps going and hands it the newest frame at the first repetition
-// boundary after the device is ready (bit-exact at any point: CPU and GPU
-// repetitions are identical step by step; measured slower, see run notes
-// below).  A failed GPU bring-up leaves the job on the CPU (auto_choice).
-// CPU time of the job (or of its rest) below which the GPU is not
-// started (PCONV_AUTO_GPU_MIN_S overrides; 0 = always start it).
-constexpr double kAutoGpuMinS = 0.1;
-
-double auto_gpu_min_s() {
-  const char* v = std::getenv("PCONV_AUTO_GPU_MIN_S");
-  return v && *v ? std::strtod(v, nullptr) : kAutoGpuMinS;
-}
-
+// A failed GPU bring-up leaves the job on the CPU (auto_choice says why).
+// Measured and removed (round 5): a CPU head start handing the newest frame
+// to a GPU brought up on a helper thread — bit-exact, but slower whenever the
+// job is worth a GPU (8192^2 RGB x100 0.31 vs 0.23 s, 32768^2 grey x200 1.43
+// vs 0.74 s: the CPU team and the bring-up compete for the host).
 AppReport run_auto(const CliConfig& c) {
   AppReport r;
   const double t0 = wall_seconds();
@@ -438,14 +418,12 @@ AppReport run_auto(const CliConfig& c) {
   if (c.threads > 0)
     omp_set_num_threads(c.threads);
   else
-    (void)configure_cpu_threads();  // leaves a CPU for the bring-up thread
+    (void)configure_cpu_threads();
 #pragma omp parallel
   { (void)omp_get_thread_num(); }  // the team starts here, not inside a timed step
   r.output = out_path(c);
   r.kernel = "cpu-omp";
-  const double thr = auto_gpu_min_s();
-  const char* ho = std::getenv("PCONV_AUTO_HANDOFF");
-  const bool handoff_env = ho && ho[0] == '1';
+  const double thr = c.auto_gpu_min_s;
   char est[128];
 
   // Stage 1: price from the first rows only (a frame of <= 256 rows), so a
@@ -473,11 +451,8 @@ AppReport run_auto(const CliConfig& c) {
   double cpu_s = r.cpu_rep_s * c.reps;
   std::snprintf(est, sizeof(est), "cpu estimate %.4f s", cpu_s);
 
-  // The GPU path on its own: measured faster than a CPU head start with a
-  // handoff once the job is worth a GPU (8192^2 RGB x100 0.23 vs 0.31 s,
-  // 32768^2 grey x200 0.74 vs 1.43 s: the CPU's work slows the bring-up,
-  // and the handoff adds a host copy into pinned memory; profiles/r04/).
-  // Returns false (auto_choice says why) if the GPU cannot run the job.
+  // The GPU path on its own; false (auto_choice says why) if the GPU cannot
+  // run the job.
   AppReport gr;
   auto gpu_alone = [&]() -> bool {
     try {
@@ -497,13 +472,13 @@ AppReport run_auto(const CliConfig& c) {
     }
   };
   bool gpu_failed = false;
-  if (c.reps > 0 && cpu_s >= thr && !handoff_env) {
+  if (c.reps > 0 && cpu_s >= thr) {
     if (gpu_alone()) return gr;
     gpu_failed = true;
   }
 
-  // Stage 2: the whole image on the host (the CPU runs the job, or hands it
-  // off); the first repetition is timed on the full frame and re-prices it.
+  // Stage 2: the whole image on the host; the first repetition is timed on
+  // the full frame and re-prices the job.
   std::vector<uint8_t> fa(static_cast<size_t>(lay.bytes()), 0), fb(static_cast<size_t>(lay.bytes()), 0);
   load_rows(c, g, 0, g.height, fa.data() + lay.offset(0), lay.pitch);
   pc.mark(c.synthetic ? "synthesize" : "read");
@@ -527,7 +502,7 @@ AppReport run_auto(const CliConfig& c) {
       cpu_s = first * c.reps;
       std::snprintf(est, sizeof(est), "cpu estimate %.4f s from the first full repetition", cpu_s);
     }
-    if (!handoff_env && first * (c.reps - 1) >= thr) {
+    if (first * (c.reps - 1) >= thr) {
       std::vector<uint8_t>().swap(fa);  // the GPU path stages the image itself
       std::vector<uint8_t>().swap(fb);
       if (gpu_alone()) return gr;
@@ -542,100 +517,19 @@ AppReport run_auto(const CliConfig& c) {
       cpu_rep();
     }
   }
-  const bool handoff = handoff_env && !gpu_failed && cpu_s >= thr;
-  if (!gpu_failed)
-    r.auto_choice = handoff ? std::string("gpu started beside the cpu, handoff (") + est + ")"
-                            : std::string("cpu only (job shorter than gpu start-up: ") + est + ")";
-
-  // GPU bring-up on a helper thread; `ready` publishes the finished engine.
-  struct Gpu {
-    std::atomic<int> state{0};  // 0 pending, 1 ready, 2 failed
-    std::string error;
-    PinnedBuffer host;
-    Stream stream;
-    std::unique_ptr<BandEngine> eng;
-    double ready_s = 0;
-  } gpu;
-  const int device = 0;
-  std::thread bring_up;
-  if (handoff) {
-    bring_up = std::thread([&] {
-      try {
-        set_device(device);
-        PCONV_HIP_CHECK(hipFree(nullptr));
-        preload_kernel_module();
-        const bool prev = std::getenv("PCONV_AUTOTUNE") ? true : set_shape_tuning(false);
-        gpu.host = PinnedBuffer(static_cast<size_t>(g.bytes()));
-        EngineOptions o = engine_options(c, g, 1, device);
-        o.kernel_copies = c.copies != 0;  // one-shot process: CU copies unless --copies sdma
-        gpu.stream = Stream::create(0);
-        o.compute_stream = gpu.stream.get();
-        gpu.eng = std::make_unique<BandEngine>(g, row_band(g.height, 1, 0), f, o);
-        // one launch of the production kernel on the zeroed frames (first-use costs)
-        for (int i = 0; i < std::max(1, c.warmup); ++i) gpu.eng->run(std::min(c.reps, gpu.eng->options().fuse));
-        gpu.eng->synchronize();
-        if (!std::getenv("PCONV_AUTOTUNE")) (void)set_shape_tuning(prev);
-        gpu.ready_s = wall_seconds() - t0;
-        gpu.state.store(1, std::memory_order_release);
-      } catch (const std::exception& e) {
-        gpu.error = e.what();
-        gpu.state.store(2, std::memory_order_release);
-      }
-    });
-  }
-  struct Joiner {
-    std::thread& t;
-    ~Joiner() {
-      if (t.joinable()) t.join();
-    }
-  } join_bring_up{bring_up};
-  // CPU repetitions until the device is ready (or the job is done).
-  while (done < c.reps && !(handoff && gpu.state.load(std::memory_order_acquire) == 1)) cpu_rep();
+  if (!gpu_failed) r.auto_choice = std::string("cpu only (job shorter than gpu start-up: ") + est + ")";
+  while (done < c.reps) cpu_rep();
   r.cpu_reps = done;
   r.gpu_reps = 0;
-  if (done < c.reps) {
-    // Handoff: the newest CPU frame -> pinned staging -> device, the rest on the GPU.
-    pc.mark("cpu_loop");
-    set_device(device);
-    BandEngine& eng = *gpu.eng;
-    uint8_t* host = gpu.host.data();
-#pragma omp parallel for schedule(static)
-    for (int64_t y = 0; y < g.height; ++y) std::memcpy(host + y * rb, src + lay.offset(y), static_cast<size_t>(rb));
-    eng.upload_rows(host, rb, 0, g.height);
-    eng.run(c.reps - done);
-    eng.download_rows(host, rb, 0, g.height);
-    eng.synchronize();
-    r.launches = eng.last_stats().launches;
-    r.gpu_reps = c.reps - done;
-    r.loop_s = wall_seconds() - l0;
-    pc.mark("gpu_loop");
-    r.halo = eng.options().halo_depth;
-    r.fuse = eng.options().fuse;
-    r.kernel = std::string("cpu-omp+") + kernel_variant_name(eng.options().variant);
-    r.copies = eng.options().kernel_copies ? "kernel" : "sdma";
-    r.auto_choice += "; gpu ready at " + std::to_string(gpu.ready_s) + " s";
-    write_image(r.output, g, host);
-    pc.mark("write");
-    r.e2e_s = wall_seconds() - t0;
-    if (c.check) r.mismatches = compare_with_oracle(c, g, host);
-  } else {
-    r.loop_s = wall_seconds() - l0;
-    pc.mark("cpu_loop");
-    std::vector<uint8_t> img(static_cast<size_t>(g.bytes()));
-    for (int64_t y = 0; y < g.height; ++y) std::memcpy(img.data() + y * rb, src + lay.offset(y), static_cast<size_t>(rb));
-    write_image(r.output, g, img.data());
-    pc.mark("write");
-    if (handoff) {
-      // The CPU finished first: the bring-up still has to end before the
-      // process may (its time is in e2e_s).
-      bring_up.join();
-      pc.mark("gpu_join");
-      r.auto_choice += gpu.state.load() == 2 ? "; gpu bring-up failed: " + gpu.error : "; cpu finished first";
-    }
-    r.e2e_s = wall_seconds() - t0;
-    if (c.check) r.mismatches = compare_with_oracle(c, g, img.data());
-  }
-  r.gpus = r.gpu_reps > 0 ? 1 : 0;
+  r.loop_s = wall_seconds() - l0;
+  pc.mark("cpu_loop");
+  std::vector<uint8_t> img(static_cast<size_t>(g.bytes()));
+  for (int64_t y = 0; y < g.height; ++y) std::memcpy(img.data() + y * rb, src + lay.offset(y), static_cast<size_t>(rb));
+  write_image(r.output, g, img.data());
+  pc.mark("write");
+  r.e2e_s = wall_seconds() - t0;
+  if (c.check) r.mismatches = compare_with_oracle(c, g, img.data());
+  r.gpus = 0;
   r.since_exec_s = seconds_since_exec();
   return r;
 }
@@ -723,7 +617,7 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
               "need " + std::to_string(world) + " GPUs, " + std::to_string(ndev) + " visible (try --transport shm)");
   const int device = rank % ndev;
   set_device(device);
-  if (world > 1) (void)bind_to_device_numa(device);  // this rank's host work on its GPU's socket
+  if (world > 1 && c.numa_bind) (void)bind_to_device_numa(device);  // this rank's host work on its GPU's socket
   const Filter f = Filter::by_name(c.filter);
   const Band b = row_band(g.height, world, rank);
   const EngineOptions o = engine_options(c, g, world, device);
@@ -748,7 +642,7 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
   } else if (ipc) {
     // Device-side pulls of the neighbours' rows (ipc_halo.hpp): export this
     // rank's frames, meet, open the neighbours' frames, meet.
-    ipct = std::make_shared<IpcHaloTransport>(eng, sh->ipc_segment, 0, 1, c.timeout_s);
+    ipct = std::make_shared<IpcHaloTransport>(eng, sh->ipc_segment, 0, 1, c.timeout_s, parse_ipc_pull(c.ipc_pull));
     const auto h = ipct->local_handles();
     std::memcpy(sh->ipc_handles[rank], h.data(), h.size());
     shm_barrier(sh, world, c.timeout_s);
@@ -929,6 +823,8 @@ struct BenchShared {
   double sec[kMaxRanks];     // timed region per rank
   double lat_ms[kMaxRanks];  // median single-image latency per rank
   double pair_ms[kMaxRanks];
+  int64_t h2d_bytes[kMaxRanks];  // per image: band + pre-loaded ghost rows
+  int64_t d2h_bytes[kMaxRanks];  // per image: owned rows
   int launches, halo, fuse, hip_version;
   char hip_path[512];
 };
@@ -948,10 +844,13 @@ void bench_rank(const CliConfig& c, BenchShared* sh, uint8_t* image, int rank) {
               "bench ranks share one GPU)");
   const int device = emu ? 0 : rank % ndev;
   set_device(device);
-  if (world > 1) (void)bind_to_device_numa(device);
+  if (world > 1 && c.numa_bind) (void)bind_to_device_numa(device);
   const Filter f = Filter::by_name(c.filter);
   const Band b = row_band(g.height, world, rank);
   EngineOptions o = engine_options(c, g, world, device);
+  o.stagger = c.stagger;
+  o.cu_mask_queues = c.cu_mask_queues;
+  o.head_on_slot_streams = c.head_on_slot_streams;
   // Pre-loaded ghost zone deep enough for every repetition (exchange-free
   // images, like bench.py's headline): rows of the band's dependency cone.
   if (world > 1 && c.halo == 0 && c.reps <= g.height / world) o.halo_depth = std::max(c.reps, o.fuse);
@@ -988,6 +887,8 @@ void bench_rank(const CliConfig& c, BenchShared* sh, uint8_t* image, int rank) {
   shm_barrier(&sh->st, ndev_ranks, c.timeout_s);
   const int slot = emu ? 0 : rank;  // shared-state index of this process
   sh->sec[slot] = t1 - t0;
+  sh->h2d_bytes[slot] = in_rows * rb;
+  sh->d2h_bytes[slot] = b.rows * rb;
   // one image alone (nothing else queued): the reference GPU_convolution() scope
   std::vector<double> lat;
   int last = 0;
@@ -1081,12 +982,14 @@ std::string run_bench_impl(const CliConfig& c) {
     PCONV_FAIL("bench failed: " + err);
   }
   double sec = 0, lat = 0, pair = 0;
-  std::ostringstream per;
+  std::ostringstream per, h2d, d2h;
   for (int r = 0; r < c.gpus; ++r) {
     sec = std::max(sec, sh->sec[r]);
     lat = std::max(lat, sh->lat_ms[r]);
     pair = std::max(pair, sh->pair_ms[r]);
     per << (r ? ", " : "") << sh->sec[r] / c.bench_steps * 1e3;
+    h2d << (r ? ", " : "") << sh->h2d_bytes[r];
+    d2h << (r ? ", " : "") << sh->d2h_bytes[r];
   }
   int64_t mism = -1;
   if (c.check && c.emulate_world > 0) {
@@ -1122,7 +1025,10 @@ std::string run_bench_impl(const CliConfig& c) {
      << c.reps << " reps\", \"global_batch\": 1, \"seq_len\": " << c.height << ", \"parallelism\": \"rowband"
      << c.gpus << "\", \"step\": \"H2D + reps + D2H per image (reference GPU_convolution scope)\", \"halo_mode\": \""
      << (c.gpus > 1 || c.emulate_world > 1 ? "preload" : "none") << "\", \"images_in_flight\": " << c.slots
-     << ", \"stream_chunks\": " << c.stream_chunks << ", \"halo_depth\": " << sh->halo << ", \"fuse\": " << sh->fuse
+     << ", \"stream_chunks\": " << c.stream_chunks << ", \"stagger\": " << (c.stagger ? "true" : "false")
+     << ", \"cu_mask_queues\": " << (c.cu_mask_queues ? "true" : "false")
+     << ", \"head_on_slot_streams\": " << (c.head_on_slot_streams ? "true" : "false")
+     << ", \"numa_bind\": " << (c.numa_bind ? "true" : "false") << ", \"halo_depth\": " << sh->halo << ", \"fuse\": " << sh->fuse
      << ", \"launches_per_step\": " << sh->launches << "}, \"latency_ms\": " << lat
      << ", \"copy_floor\": {\"pair_ms\": " << pair << "}";
   if (mism >= 0)
@@ -1134,7 +1040,8 @@ std::string run_bench_impl(const CliConfig& c) {
           "measurement)\"";
   os << ", \"runtime\": {\"stack\": \"native conv (no torch)\", \"hip_runtime_version\": " << sh->hip_version
      << ", \"hip_runtime_path\": \"" << json_escape(sh->hip_path) << "\", \"rccl_version\": null}"
-     << ", \"per_rank_ms_per_step\": [" << per.str() << "]}";
+     << ", \"per_rank_ms_per_step\": [" << per.str() << "]"
+     << ", \"h2d_bytes_per_step\": [" << h2d.str() << "], \"d2h_bytes_per_step\": [" << d2h.str() << "]}";
   munmap(im, static_cast<size_t>(g.bytes()));
   munmap(mem, sizeof(BenchShared));
   return os.str();

@@ -31,9 +31,11 @@ std::string usage_text(const std::string& prog) {
 std::string help_text(const std::string& prog) {
   return "usage: " + prog +
          " image.raw width height repetitions {grey,rgb,rgba} [options]\n"
-         "  --backend {hip,cpu,omp,auto}  compute backend (default hip; auto: the CPU starts the repetitions\n"
-         "                            at once while the GPU initialises, the GPU takes over the rest; jobs\n"
-         "                            shorter on the CPU than the GPU's start-up never touch the GPU)\n"
+         "  --backend {hip,cpu,omp,auto}  compute backend (default hip; auto: the job is priced on the CPU from\n"
+         "                            a row sample, then from its first full repetition; above --auto-gpu-min\n"
+         "                            seconds of CPU time the GPU runs it alone, otherwise the CPU runs it and\n"
+         "                            the GPU is never touched)\n"
+         "  --auto-gpu-min S          --backend auto: CPU seconds above which the GPU runs the job (default 0.1)\n"
          "  --gpus N                  row-band decomposition over N GPUs, one process each (RCCL halos)\n"
          "  --filter {gaussian,box,edge}  3x3 filter (default gaussian)\n"
          "  --halo D                  ghost rows exchanged at once (default: auto)\n"
@@ -63,9 +65,17 @@ std::string help_text(const std::string& prog) {
          "  --bench K                 serving bench: K timed images (H2D + reps + D2H each) per rank after\n"
          "                            --warmup untimed ones; prints bench.py's JSON line (native stack)\n"
          "  --slots S                 --bench: images in flight (default 4)\n"
-         "  --stream-chunks C         --bench: rows of each image streamed in C chunks (0 = off; -1 = one\n"
-         "                            persistent wave launch per image, stencil_wave.hip)\n"
+         "  --stream-chunks C         --bench: rows of each image streamed in C chunks (0 = off)\n"
          "  --emulate W:R             --bench: time rank R of a W-way split alone (per-rank proxy)\n"
+         "  --no-stagger              --bench: the first images of a burst upload all at once\n"
+         "  --pool-queues             --bench: slot streams from the runtime's queue pool (default: each on\n"
+         "                            its own CU-masked hardware queue)\n"
+         "  --head-pool-streams       --bench: a streamed head image's copies on two pool streams (default:\n"
+         "                            the next two slots' streams)\n"
+         "  --ipc-pull {grid,single,sdma}  --transport ipc: pull form (default grid: many workgroups)\n"
+         "  --tune {auto,on,off}      SWAR tile-shape tuning (auto: off for a one-shot run, on in a server)\n"
+         "  --ring-chunk-bytes B      one-shot staging ring chunk (default 32 MiB; 0 = one pinned image)\n"
+         "  --no-numa-bind            N > 1: leave each rank's CPU affinity alone\n"
          "\n"
          "       " + prog + " --serve SOCKET [--device D] [--idle-timeout S] [--max-engines N]\n"
          "                            resident service: initialise the GPU once, then run jobs sent by\n"
@@ -116,7 +126,6 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       if (v == "auto") c.variant = KernelVariant::Auto;
       else if (v == "binomial") c.variant = KernelVariant::Binomial;
       else if (v == "temporal") c.variant = KernelVariant::Temporal;
-      else if (v == "temporal_pk") c.variant = KernelVariant::TemporalPk;
       else if (v == "int9") c.variant = KernelVariant::Int9;
       else if (v == "float9") c.variant = KernelVariant::Float9;
       else if (v == "float_temporal") c.variant = KernelVariant::FloatTemporal;
@@ -171,7 +180,32 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       c.emulate_world = static_cast<int>(parse_int(v.substr(0, colon), "--emulate world", 1, 64));
       c.emulate_rank = static_cast<int>(parse_int(v.substr(colon + 1), "--emulate rank", 0, c.emulate_world - 1));
     } else if (a == "--stream-chunks") {
-      c.stream_chunks = static_cast<int>(parse_int(next("--stream-chunks"), "--stream-chunks", -1, 4096));
+      c.stream_chunks = static_cast<int>(parse_int(next("--stream-chunks"), "--stream-chunks", 0, 4096));
+    } else if (a == "--no-stagger") {
+      c.stagger = false;
+    } else if (a == "--pool-queues") {
+      c.cu_mask_queues = false;
+    } else if (a == "--head-pool-streams") {
+      c.head_on_slot_streams = false;
+    } else if (a == "--ipc-pull") {
+      c.ipc_pull = next("--ipc-pull");
+      if (c.ipc_pull != "grid" && c.ipc_pull != "single" && c.ipc_pull != "sdma")
+        PCONV_FAIL("invalid --ipc-pull '" + c.ipc_pull + "' (grid|single|sdma)");
+    } else if (a == "--tune") {
+      const std::string v = next("--tune");
+      if (v == "auto") c.tune = -1;
+      else if (v == "on") c.tune = 1;
+      else if (v == "off") c.tune = 0;
+      else PCONV_FAIL("invalid --tune '" + v + "' (auto|on|off)");
+    } else if (a == "--ring-chunk-bytes") {
+      c.ring_chunk_bytes = parse_int(next("--ring-chunk-bytes"), "--ring-chunk-bytes", 0, int64_t(1) << 40);
+    } else if (a == "--auto-gpu-min") {
+      const std::string v = next("--auto-gpu-min");
+      char* end = nullptr;
+      c.auto_gpu_min_s = std::strtod(v.c_str(), &end);
+      if (v.empty() || *end != '\0' || !(c.auto_gpu_min_s >= 0)) PCONV_FAIL("invalid --auto-gpu-min '" + v + "'");
+    } else if (a == "--no-numa-bind") {
+      c.numa_bind = false;
     } else if (a == "--warmup") {
       c.warmup = static_cast<int>(parse_int(next("--warmup"), "--warmup", 0, 100));
     } else {

@@ -51,8 +51,6 @@ HipRuntimeInfo hip_runtime_info() {
 }
 
 int bind_to_device_numa(int device) {
-  const char* env = std::getenv("PCONV_NUMA_BIND");
-  if (env && std::string(env) == "0") return 0;
   std::ifstream f("/sys/bus/pci/devices/" + device_pci_bus_id(device) + "/local_cpulist");
   std::string text;
   if (!f || !std::getline(f, text)) return 0;

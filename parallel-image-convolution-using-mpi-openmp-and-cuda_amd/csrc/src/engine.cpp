@@ -418,193 +418,6 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
   halo_valid_ = false;
 }
 
-namespace {
-
-constexpr int kWaveMaxTasks = 1 << 17;  // beyond this the ticket counter's serial rate dominates
-constexpr int kWaveLoadParts = 2, kWaveStoreParts = 2;
-
-}  // namespace
-
-bool BandEngine::wave_able(int reps, int64_t in_r0, int64_t in_r1) const {
-  if (reps < 1 || !filter_.binomial121 || lay_.row_bytes % 4 != 0) return false;
-  if (opt_.variant != KernelVariant::Auto && opt_.variant != KernelVariant::Temporal) return false;
-  if (lay_.total_rows() * lay_.pitch >= (int64_t(1) << 31) || geom_.height >= (int64_t(1) << 30)) return false;
-  PlanConfig c = engine_plan_config(geom_, band_, filter_, opt_);
-  c.halo_preloaded = input_preloaded(in_r0, in_r1);
-  const std::vector<Phase> ph = plan_band(band_, reps, c);
-  if (!streamable(ph)) return false;
-  int smax = 0;
-  int64_t tasks = 0;
-  for (const auto& p : ph) smax = std::max(smax, p.steps);
-  const int tr = wave_tile_rows(smax);
-  if (tr < 1) return false;
-  for (const auto& p : ph) {
-    const int g = wave_col_groups(geom_.ch(), p.steps, lay_.row_bytes);
-    if (g < 1) return false;
-    tasks += (p.launches[0].hi - p.launches[0].lo + tr - 1) / tr * g;
-  }
-  return tasks <= kWaveMaxTasks;
-}
-
-const BandEngine::WaveDev& BandEngine::wave_dev(int reps, int64_t in_r0, int64_t in_r1) {
-  const auto key = std::make_tuple(reps, in_r0, in_r1);
-  auto it = waves_.find(key);
-  if (it != waves_.end()) return it->second;
-  PCONV_CHECK(wave_able(reps, in_r0, in_r1), "enqueue_wave: this image cannot run as one wave launch");
-  PlanConfig c = engine_plan_config(geom_, band_, filter_, opt_);
-  c.halo_preloaded = input_preloaded(in_r0, in_r1);
-  const std::vector<Phase> ph = plan_band(band_, reps, c);
-  int smax = 0;
-  for (const auto& p : ph) smax = std::max(smax, p.steps);
-  std::vector<int> groups(ph.size() + 1, 0);
-  for (size_t j = 0; j < ph.size(); ++j) groups[j + 1] = wave_col_groups(geom_.ch(), ph[j].steps, lay_.row_bytes);
-  // A/B knobs: PCONV_WAVE_PARTS (row parts per load / store tile), PCONV_WAVE_LEAD
-  const char* pe = std::getenv("PCONV_WAVE_PARTS");
-  const char* le = std::getenv("PCONV_WAVE_LEAD");
-  const int parts = pe ? std::max(1, std::atoi(pe)) : kWaveLoadParts;
-  const WavePlan wp = plan_wave(ph, in_r0, in_r1, band_.rows, wave_tile_rows(smax), groups, parts,
-                                pe ? parts : kWaveStoreParts, le ? std::atoi(le) : 2,
-                                std::getenv("PCONV_WAVE_GAP") ? std::atoi(std::getenv("PCONV_WAVE_GAP")) : 8);
-  WaveDev d;
-  d.ntasks = static_cast<int>(wp.tasks.size());
-  d.levels = wp.levels;
-  // loads | level tiles | stores, each in ticket order (the kernel's roles);
-  // PCONV_WAVE_DYN=1 (A/B): the level tiles grouped by level, each level in
-  // tile order, claimed only when ready — measured 6x slower than one ticket
-  // queue: every idle workgroup re-scans the per-level heads and their
-  // dependency counters and they contend on one compare-and-swap word per
-  // level (profiles/r04/wave7/)
-  const char* dy = std::getenv("PCONV_WAVE_DYN");
-  d.dynamic = dy && dy[0] == '1';
-  std::vector<WaveTask> part;
-  part.reserve(wp.tasks.size());
-  for (const auto& k : wp.tasks)
-    if (k.kind == 0) part.push_back(k);
-  std::vector<int> qbase(wp.levels + 1, 0), qcount(wp.levels + 1, 0);
-  if (d.dynamic) {
-    const size_t c0 = part.size();
-    for (int j = 1; j <= wp.levels; ++j) {
-      qbase[j] = static_cast<int>(part.size() - c0);
-      for (const auto& k : wp.tasks)
-        if (k.kind == 1 && k.level == j) part.push_back(k);
-      qcount[j] = static_cast<int>(part.size() - c0) - qbase[j];
-    }
-  } else {
-    for (const auto& k : wp.tasks)
-      if (k.kind == 1) part.push_back(k);
-  }
-  for (const auto& k : wp.tasks)
-    if (k.kind == 2) part.push_back(k);
-  for (const auto& k : wp.tasks) (k.kind == 0 ? d.nload : k.kind == 1 ? d.ncomp : d.nstore) += 1;
-  d.counters = wp.counters;
-  d.tasks = DeviceBuffer(part.size() * sizeof(WaveTask));
-  PCONV_HIP_CHECK(hipMemcpy(d.tasks.data(), part.data(), part.size() * sizeof(WaveTask), hipMemcpyHostToDevice));
-  std::vector<int> table(8 * (wp.levels + 1), 0);
-  for (int j = 0; j <= wp.levels; ++j) {
-    table[8 * j] = wp.steps[j];
-    table[8 * j + 1] = wp.arrivals[j];
-    table[8 * j + 2] = wp.counter_base[j];
-    table[8 * j + 3] = qbase[j];
-    table[8 * j + 4] = qcount[j];
-  }
-  d.table = DeviceBuffer(table.size() * sizeof(int));
-  PCONV_HIP_CHECK(hipMemcpy(d.table.data(), table.data(), table.size() * sizeof(int), hipMemcpyHostToDevice));
-  const size_t ctl = static_cast<size_t>(32 + 4 * (wp.counters + wp.levels + 1) + 15) / 16 * 16;
-  if (wave_ctl_.size() < ctl) {
-    PCONV_HIP_CHECK(hipStreamSynchronize(cs_));  // an earlier wave may still use the old block
-    wave_ctl_ = DeviceBuffer(ctl);
-  }
-  if (!wave_err_.data()) {
-    wave_err_ = PinnedBuffer(64);
-    std::memset(wave_err_.data(), 0, 64);
-    int khz = 0;
-    PCONV_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, opt_.device));
-    double s = 2.0;  // a whole image is milliseconds; a stuck wait gives up after this
-    if (const char* t = std::getenv("PCONV_WAVE_TIMEOUT_S")) s = std::max(1e-7, std::atof(t));
-    wave_timeout_ticks_ = static_cast<uint64_t>(s * static_cast<double>(khz > 0 ? khz : 100000) * 1000.0);
-  }
-  return waves_.emplace(key, std::move(d)).first->second;
-}
-
-int BandEngine::wave_tasks(int reps, int64_t in_r0, int64_t in_r1) const {
-  auto it = waves_.find(std::make_tuple(reps, in_r0, in_r1));
-  return it == waves_.end() ? 0 : it->second.ntasks;
-}
-
-void BandEngine::enqueue_wave(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps,
-                              hipStream_t stream) {
-  TraceRange tr("pconv.wave_image");
-  PCONV_CHECK(host_in && host_out, "enqueue_wave: pinned host buffers required");
-  PCONV_CHECK(band_.y0 + in_r0 >= 0 && band_.y0 + in_r1 <= geom_.height && in_r0 >= -lay_.halo &&
-                  in_r1 <= lay_.rows + lay_.halo,
-              "enqueue_wave: input rows outside frame / image");
-  const WaveDev& d = wave_dev(reps, in_r0, in_r1);
-  WaveLaunch w;
-  w.tasks = static_cast<const WaveTask*>(static_cast<const void*>(d.tasks.data()));
-  w.nload = d.nload;
-  w.ncomp = d.ncomp;
-  w.nstore = d.nstore;
-  w.dynamic = d.dynamic;
-  w.ncounters = d.counters;
-  if (const char* v = std::getenv("PCONV_WAVE_LOADERS")) w.loaders = std::atoi(v);
-  if (const char* v = std::getenv("PCONV_WAVE_STORERS")) w.storers = std::atoi(v);
-  w.levels = d.levels;
-  w.channels = geom_.ch();
-  w.levels_dev = static_cast<const int*>(static_cast<const void*>(d.table.data()));
-  w.ctl = static_cast<uint32_t*>(static_cast<void*>(wave_ctl_.data()));
-  w.ctl_bytes = static_cast<int64_t>(wave_ctl_.size());
-  w.err = static_cast<uint32_t*>(static_cast<void*>(wave_err_.data()));
-  w.host_in = host_in;
-  w.in_r0 = in_r0;
-  w.host_out = host_out;
-  w.frame0 = frame_at(0);
-  w.frame1 = frame_at(1);
-  w.pitch = lay_.pitch;
-  w.row_bytes = lay_.row_bytes;
-  w.g_row0 = band_.y0;
-  w.height = geom_.height;
-  w.timeout_ticks = wave_timeout_ticks_;
-  if (const char* g = std::getenv("PCONV_WAVE_GRID")) w.max_workgroups = std::atoi(g);
-  if (const char* z = std::getenv("PCONV_WAVE_SLEEP")) w.poll_sleep = std::max(1, std::atoi(z));
-  if (const char* x = std::getenv("PCONV_WAVE_WT")) w.write_through = x[0] != '0';
-  // PCONV_WAVE_TRACE=file: per-task wall-clock timeline of the next few wave
-  // images appended to `file` as JSON lines (diagnostics: the host waits for
-  // each traced image)
-  const char* trace_path = std::getenv("PCONV_WAVE_TRACE");
-  static std::atomic<int> traced{0};
-  DeviceBuffer trace;
-  if (trace_path && traced.load() < 4) {
-    trace = DeviceBuffer(static_cast<size_t>(d.ntasks) * 32);
-    PCONV_HIP_CHECK(hipMemsetAsync(trace.data(), 0, trace.size(), stream ? stream : cs_));
-    w.trace = static_cast<uint64_t*>(static_cast<void*>(trace.data()));
-  }
-  launch_wave_image(w, stream ? stream : cs_);
-  if (w.trace) {
-    ++traced;
-    PCONV_HIP_CHECK(hipStreamSynchronize(stream ? stream : cs_));
-    std::vector<uint64_t> t(static_cast<size_t>(d.ntasks) * 4);
-    std::vector<WaveTask> tasks(static_cast<size_t>(d.ntasks));
-    PCONV_HIP_CHECK(hipMemcpy(t.data(), trace.data(), trace.size(), hipMemcpyDeviceToHost));
-    PCONV_HIP_CHECK(hipMemcpy(tasks.data(), d.tasks.data(), d.tasks.size(), hipMemcpyDeviceToHost));
-    if (FILE* f = std::fopen(trace_path, "a")) {
-      std::fprintf(f, "{\"row_bytes\": %lld, \"rows\": %lld, \"levels\": %d, \"tasks\": [",
-                   static_cast<long long>(lay_.row_bytes), static_cast<long long>(band_.rows), d.levels);
-      for (size_t i = 0; i < tasks.size(); ++i) {
-        const WaveTask& k = tasks[i];
-        std::fprintf(f, "%s[%d,%d,%d,%d,%d,%d,%llu,%llu,%llu,%llu]", i ? "," : "", k.kind, k.level, k.a, k.b, k.part,
-                     k.tile, static_cast<unsigned long long>(t[4 * i]), static_cast<unsigned long long>(t[4 * i + 1]),
-                     static_cast<unsigned long long>(t[4 * i + 2]), static_cast<unsigned long long>(t[4 * i + 3]));
-      }
-      std::fprintf(f, "]}\n");
-      std::fclose(f);
-    }
-  }
-  stats_ = RunStats{};
-  stats_.launches = 1;
-  cur_ = d.levels & 1;
-  halo_valid_ = false;
-}
-
 void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
   TraceRange tr("pconv.step_graph");
   PCONV_CHECK(reps >= 0, "repetitions must be >= 0");
@@ -642,7 +455,10 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     prepare(ph);  // tile-shape tuning cannot run inside the capture
     PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
     upload_rows(host_in, rb, in_r0, in_r1, cs_);
-    if (opt_.upload_event) ev_uploaded_.record(cs_);  // an event record node: the upload is done
+    // The upload-done event as an EXTERNAL event-record node: a plain
+    // hipEventRecord inside a capture only orders nodes of this graph, and
+    // replays of the instantiated graph would never record the event.
+    if (opt_.upload_event) PCONV_HIP_CHECK(hipEventRecordWithFlags(ev_uploaded_.get(), cs_, hipEventRecordExternal));
     if (zone_first) {
       transport_->exchange(*this, lay_.halo, cs_);  // stream order: after the upload, before the launches
       ++stats_.exchanges;
@@ -681,13 +497,6 @@ void BandEngine::exec_compute(const Phase& p) {
 void BandEngine::synchronize() {
   PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
   if (ms_ != cs_) PCONV_HIP_CHECK(hipStreamSynchronize(ms_));
-  if (wave_err_.data()) {
-    auto* e = reinterpret_cast<volatile uint32_t*>(wave_err_.data());
-    if (*e != 0) {
-      *e = 0;
-      PCONV_FAIL("wave image: a dependency wait timed out inside the kernel (results of that image are invalid)");
-    }
-  }
   if (timing_pending_) {
     stats_.loop_ms = Event::elapsed_ms(ev_t0_, ev_t1_);
     stats_.wall_ms = (wall_seconds() - wall_t0_) * 1e3;
@@ -716,31 +525,24 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
     // no split launches.  With it, each slot's exchanges run on the slot's
     // own communication stream beside the interior launch.
     o.overlap = slot_comm && opt.overlap;
-    // PCONV_STAGGER=0 (A/B): every slot of a burst uploads at once
-    const char* st = std::getenv("PCONV_STAGGER");
-    stagger_ = step_graphs && !(st && st[0] == '0');
+    stagger_ = step_graphs && opt.stagger;
     o.upload_event = stagger_;
-    // Slot streams on dedicated hardware queues: a stream created with a CU
-    // mask (all CUs) gets its own HSA queue instead of one from the
-    // runtime's round-robin pool.  From the pool, 4 slot streams landed on
-    // queues of which two ran every stencil launch ~5x longer (p50 47 vs
-    // 9.6 us; the 8-way proxy step 0.106 vs 0.055 ms at 3 slots); with
-    // CU-masked queues 4 slots run at 0.053 ms (docs/PERFORMANCE.md §2,
-    // profiles/r04/slots_b/).  PCONV_SLOT_STREAMS: "cumask" (default),
-    // "plain" (the pool), "cusplit" (CUs split evenly between the slots),
-    // "prio" (pool, alternating high / normal priority).
-    const char* sm = std::getenv("PCONV_SLOT_STREAMS");
-    const std::string mode = sm ? sm : "cumask";
+    // Slot streams on dedicated hardware queues (opt.cu_mask_queues): a
+    // stream created with a CU mask (all CUs) gets its own HSA queue instead
+    // of one from the runtime's round-robin pool.  From the pool, 4 slot
+    // streams landed on queues of which two ran every stencil launch ~5x
+    // longer (p50 47 vs 9.6 us; the 8-way proxy step 0.106 vs 0.055 ms at 3
+    // slots); with CU-masked queues 4 slots run at 0.053 ms
+    // (docs/PERFORMANCE.md §2, profiles/r04/slots_b/).
     for (int i = 0; i < slots; ++i) {
-      if (mode == "cumask" || mode == "cusplit") {
-        int n = 0, dev = opt.device;
-        PCONV_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+      if (opt.cu_mask_queues) {
+        int n = 0;
+        PCONV_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, opt.device));
         std::vector<uint32_t> mask(static_cast<size_t>((n + 31) / 32), 0u);
-        for (int cu = 0; cu < n; ++cu)
-          if (mode == "cumask" || cu % slots == i) mask[static_cast<size_t>(cu / 32)] |= 1u << (cu % 32);
+        for (int cu = 0; cu < n; ++cu) mask[static_cast<size_t>(cu / 32)] |= 1u << (cu % 32);
         computes_.push_back(Stream::create_cu_masked(mask));
       } else {
-        computes_.push_back(Stream::create(mode == "prio" && (i & 1) ? -1 : 0));
+        computes_.push_back(Stream::create(0));
       }
       o.compute_stream = computes_.back().get();
       if (slot_comm) {
@@ -753,34 +555,23 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
     }
     if (step_graphs && opt.stream_chunks > 1) {
       // head streaming: copy streams for images submitted to an idle pipeline.
-      // With >= 3 slots the head's upload and download run on the next two
-      // slots' streams (idle when the pipeline is): no hardware queue beyond
-      // the slots'.  Two more queues from the runtime's pool made one image
-      // 0.77 ms with 4 slots, dedicated (CU-masked) ones 0.85 ms, the slots'
-      // streams 0.56 ms (profiles/r04/head/).  Fewer slots: pool streams.
-      // PCONV_HEAD_STREAMS = slots | pool | cumask (A/B).
-      const char* hs = std::getenv("PCONV_HEAD_STREAMS");
-      head_mode_ = hs ? hs : "slots";
-      if (head_mode_ == "cumask") {
-        int n = 0;
-        PCONV_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, opt.device));
-        std::vector<uint32_t> mask(static_cast<size_t>((n + 31) / 32), 0u);
-        for (int cu = 0; cu < n; ++cu) mask[static_cast<size_t>(cu / 32)] |= 1u << (cu % 32);
-        h2d_ = Stream::create_cu_masked(mask);
-        d2h_ = Stream::create_cu_masked(mask);
-      } else {
+      // With >= 3 slots and opt.head_on_slot_streams the head's upload and
+      // download run on the next two slots' streams (idle when the pipeline
+      // is): no hardware queue beyond the slots'.  Two more queues from the
+      // runtime's pool made one image 0.77 ms with 4 slots, dedicated
+      // (CU-masked) ones 0.85 ms, the slots' streams 0.56 ms
+      // (profiles/r04/head/).  Otherwise: two pool streams.
+      head_on_slots_ = opt.head_on_slot_streams && slots >= 3;
+      if (!head_on_slots_) {
         h2d_ = Stream::create(0);
         d2h_ = Stream::create(0);
       }
       ev_head_ = Event::create();
       h2d_wait_ = Event::create();
       head_up_ = Event::create();
+      head_streaming_ = true;
     }
     used_.assign(slots, false);
-    // PCONV_WAVE_ALL=1 (A/B, with stream_chunks -1): every image a wave
-    // launch, not only the one submitted to an idle pipeline
-    const char* wa = std::getenv("PCONV_WAVE_ALL");
-    wave_all_ = wa && wa[0] == '1';
     return;
   }
   // Streams: H2D, D2H, communication (only with neighbours) and compute.
@@ -870,18 +661,7 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
       last_upload_ = nullptr;
     }
     const int pos = burst_++;
-    const bool wave = e.options().stream_chunks < 0;
-    if (wave && (idle_ || wave_all_) && e.wave_able(reps, in_r0, in_r1)) {
-      // Wave image: the whole step is ONE persistent launch on the slot's own
-      // stream (stream order covers the frames' earlier and later graphs).
-      e.enqueue_wave(host_in, in_r0, in_r1, host_out, reps, e.compute_stream());
-      last_upload_ = nullptr;  // its loads are inside the launch: nothing to stagger on
-      idle_ = false;
-      used_[k] = true;
-      ++count_;
-      return;
-    }
-    if (idle_ && h2d_.get()) {
+    if (idle_ && head_streaming_) {
       // Head streaming: nothing is in flight, so this image's rows stream
       // (chunked H2D ‖ launches ‖ D2H of finished rows, schedule.hpp
       // plan_streamed) instead of waiting for its whole upload and its
@@ -892,9 +672,8 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
       const StreamPlan sp = e.stream_plan(reps, in_r0, in_r1);
       if (!sp.chunks.empty()) {
         e.set_cur(0);  // like process_graph: the whole input is uploaded, start in frame 0
-        const bool via_slots = head_mode_ == "slots" && slots() >= 3;
-        hipStream_t up = via_slots ? computes_[static_cast<size_t>((k + 1) % slots())].get() : h2d_.get();
-        hipStream_t down = via_slots ? computes_[static_cast<size_t>((k + 2) % slots())].get() : d2h_.get();
+        hipStream_t up = head_on_slots_ ? computes_[static_cast<size_t>((k + 1) % slots())].get() : h2d_.get();
+        hipStream_t down = head_on_slots_ ? computes_[static_cast<size_t>((k + 2) % slots())].get() : d2h_.get();
         h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
         h2d_wait_.wait_on(up);
         e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down);

@@ -6,8 +6,8 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
-#include <cstdlib>
 #include <cstring>
 
 #include "pconv/trace.hpp"
@@ -40,8 +40,26 @@ void ipc_create_segment(const std::string& name, int world, int slots) {
 
 void ipc_unlink_segment(const std::string& name) { (void)::shm_unlink(shm_path(name).c_str()); }
 
-IpcHaloTransport::IpcHaloTransport(BandEngine& e, const std::string& segment, int slot, int slots, double timeout_s)
-    : eng_(&e), rank_(e.band().rank), world_(e.band().world), slot_(slot), slots_(slots), segment_(segment) {
+IpcPull parse_ipc_pull(const std::string& s) {
+  if (s == "grid") return IpcPull::Grid;
+  if (s == "single") return IpcPull::Single;
+  if (s == "sdma") return IpcPull::Sdma;
+  PCONV_FAIL("unknown IPC pull form '" + s + "' (grid|single|sdma)");
+}
+
+const char* ipc_pull_name(IpcPull p) {
+  switch (p) {
+    case IpcPull::Grid: return "grid";
+    case IpcPull::Single: return "single";
+    case IpcPull::Sdma: return "sdma";
+  }
+  return "?";
+}
+
+IpcHaloTransport::IpcHaloTransport(BandEngine& e, const std::string& segment, int slot, int slots, double timeout_s,
+                                   IpcPull pull)
+    : eng_(&e), rank_(e.band().rank), world_(e.band().world), slot_(slot), slots_(slots), segment_(segment),
+      pull_(pull) {
   PCONV_CHECK(slot >= 0 && slot < slots, "ipc transport: slot out of range");
   seg_bytes_ = segment_bytes(world_, slots_);
   const std::string p = shm_path(segment);
@@ -61,8 +79,10 @@ IpcHaloTransport::IpcHaloTransport(BandEngine& e, const std::string& segment, in
   int khz = 0;
   PCONV_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e.options().device));
   timeout_ticks_ = static_cast<uint64_t>(timeout_s * static_cast<double>(khz > 0 ? khz : 100000) * 1000.0);
-  const char* k = std::getenv("PCONV_IPC_KERNELS");
-  split_kernels_ = k && k[0] == '3';
+  if (pull_ == IpcPull::Grid) {
+    arrive_ = DeviceBuffer(64);
+    PCONV_HIP_CHECK(hipMemset(arrive_.data(), 0, arrive_.size()));
+  }
   handles_.resize(2 * sizeof(hipIpcMemHandle_t));
   for (int i = 0; i < 2; ++i) {
     hipIpcMemHandle_t h;
@@ -138,14 +158,8 @@ void IpcHaloTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream
   const uint8_t* src_down = down >= 0 ? peer_down_[par] + lay_down_.offset(0) - kPadLeft : nullptr;
   uint8_t* dst_up = mine + L.offset(-depth) - kPadLeft;
   uint8_t* dst_down = mine + L.offset(b.rows) - kPadLeft;
-  if (split_kernels_) {
-    launch_ipc_signal_wait(dflags_, me, up, down, timeout_ticks_, stream);
-    launch_ipc_pull(dflags_, me, dst_up, src_up, dst_down, src_down, static_cast<int64_t>(n), stream);
-    launch_ipc_ack_wait(dflags_, me, up, down, timeout_ticks_, stream);
-  } else {
-    launch_ipc_exchange(dflags_, me, up, down, timeout_ticks_, dst_up, src_up, dst_down, src_down,
-                        static_cast<int64_t>(n), stream);
-  }
+  launch_ipc_exchange(pull_, dflags_, reinterpret_cast<uint32_t*>(arrive_.data()), me, up, down, timeout_ticks_,
+                      dst_up, src_up, dst_down, src_down, static_cast<int64_t>(n), stream);
   ++enqueued_;
 }
 
@@ -160,6 +174,68 @@ void IpcHaloTransport::check() const {
   PCONV_CHECK(err == 0, std::string("ipc halo: rank ") + std::to_string(rank_) + " slot " + std::to_string(slot_) +
                             (err == 1 ? ": timed out waiting for a neighbour's rows"
                                       : ": timed out waiting for a neighbour to copy this rank's rows"));
+}
+
+}  // namespace pconv
+
+namespace pconv {
+
+double ipc_pull_probe(const std::string& form, int64_t bytes, bool host_source, int iters, int device,
+                      int workgroups) {
+  PCONV_CHECK(bytes > 0 && bytes % 16 == 0 && iters >= 1, "ipc_pull_probe: bytes must be a positive multiple of 16");
+  const IpcPull p = parse_ipc_pull(form);
+  set_device(device);
+  // the flag block in coherent (fine-grained) mapped host memory, like the
+  // shared segment the transport registers
+  void* fh = nullptr;
+  PCONV_HIP_CHECK(hipHostMalloc(&fh, sizeof(IpcFlags), hipHostMallocCoherent | hipHostMallocMapped));
+  struct FreeHost {
+    void* p;
+    ~FreeHost() { (void)hipHostFree(p); }
+  } free_flags{fh};
+  std::memset(fh, 0, sizeof(IpcFlags));
+  void* fd = nullptr;
+  PCONV_HIP_CHECK(hipHostGetDevicePointer(&fd, fh, 0));
+  DeviceBuffer arrive(64), dst(static_cast<size_t>(2 * bytes));
+  PCONV_HIP_CHECK(hipMemset(arrive.data(), 0, arrive.size()));
+  PinnedBuffer hsrc;
+  DeviceBuffer dsrc;
+  uint8_t* src = nullptr;
+  if (host_source) {
+    hsrc = PinnedBuffer(static_cast<size_t>(2 * bytes));
+    std::memset(hsrc.data(), 0x5a, hsrc.size());
+    void* d = nullptr;
+    PCONV_HIP_CHECK(hipHostGetDevicePointer(&d, hsrc.data(), 0));
+    src = static_cast<uint8_t*>(d);
+  } else {
+    dsrc = DeviceBuffer(static_cast<size_t>(2 * bytes));
+    PCONV_HIP_CHECK(hipMemset(dsrc.data(), 0x5a, dsrc.size()));
+    src = dsrc.data();
+  }
+  int khz = 0;
+  PCONV_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
+  const uint64_t timeout = static_cast<uint64_t>(5.0 * static_cast<double>(khz > 0 ? khz : 100000) * 1000.0);
+  Stream st = Stream::create(0);
+  auto* f = static_cast<IpcFlags*>(fd);
+  auto* arr = reinterpret_cast<uint32_t*>(arrive.data());
+  auto one = [&] {
+    launch_ipc_exchange(p, f, arr, 0, 0, 0, timeout, dst.data(), src + bytes, dst.data() + bytes, src, bytes,
+                        st.get(), workgroups);
+  };
+  for (int i = 0; i < 3; ++i) one();
+  PCONV_HIP_CHECK(hipStreamSynchronize(st.get()));
+  Event e0 = Event::create(true), e1 = Event::create(true);
+  e0.record(st.get());
+  for (int i = 0; i < iters; ++i) one();
+  e1.record(st.get());
+  PCONV_HIP_CHECK(hipStreamSynchronize(st.get()));
+  const auto* fl = reinterpret_cast<const volatile IpcFlags*>(fh);
+  PCONV_CHECK(fl->err == 0, "ipc_pull_probe: a self-neighbour wait timed out");
+  PCONV_CHECK(fl->count == static_cast<uint32_t>(iters + 3), "ipc_pull_probe: exchange count mismatch");
+  std::vector<uint8_t> back(static_cast<size_t>(2 * bytes));
+  PCONV_HIP_CHECK(hipMemcpy(back.data(), dst.data(), back.size(), hipMemcpyDeviceToHost));
+  for (uint8_t v : back) PCONV_CHECK(v == 0x5a, "ipc_pull_probe: pulled bytes differ from the source");
+  return Event::elapsed_ms(e0, e1) / iters;
 }
 
 }  // namespace pconv

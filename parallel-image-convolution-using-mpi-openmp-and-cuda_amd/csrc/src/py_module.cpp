@@ -57,7 +57,6 @@ KernelVariant parse_variant(const std::string& s) {
   if (s == "auto") return KernelVariant::Auto;
   if (s == "binomial") return KernelVariant::Binomial;
   if (s == "temporal") return KernelVariant::Temporal;
-  if (s == "temporal_pk") return KernelVariant::TemporalPk;
   if (s == "int9") return KernelVariant::Int9;
   if (s == "float9") return KernelVariant::Float9;
   if (s == "float_temporal") return KernelVariant::FloatTemporal;
@@ -184,30 +183,6 @@ PYBIND11_MODULE(_pconv_native, m) {
   m.def("stream_cuts", &stream_cuts, py::arg("in_lo"), py::arg("in_hi"), py::arg("chunks"));
   m.def("plan_streamed", &plan_streamed, py::arg("plan"), py::arg("in_lo"), py::arg("in_hi"), py::arg("owned_rows"),
         py::arg("cuts"));
-  py::class_<WaveTask>(m, "WaveTask")
-      .def_readonly("kind", &WaveTask::kind)
-      .def_readonly("level", &WaveTask::level)
-      .def_readonly("a", &WaveTask::a)
-      .def_readonly("b", &WaveTask::b)
-      .def_readonly("part", &WaveTask::part)
-      .def_readonly("tile", &WaveTask::tile)
-      .def_readonly("dep_lo", &WaveTask::dep_lo)
-      .def_readonly("dep_hi", &WaveTask::dep_hi)
-      .def_property_readonly("dep_level", &WaveTask::dep_level);
-  py::class_<WavePlan>(m, "WavePlan")
-      .def_readonly("levels", &WavePlan::levels)
-      .def_readonly("tile_rows", &WavePlan::tile_rows)
-      .def_readonly("steps", &WavePlan::steps)
-      .def_readonly("lo", &WavePlan::lo)
-      .def_readonly("hi", &WavePlan::hi)
-      .def_readonly("tiles", &WavePlan::tiles)
-      .def_readonly("arrivals", &WavePlan::arrivals)
-      .def_readonly("counter_base", &WavePlan::counter_base)
-      .def_readonly("counters", &WavePlan::counters)
-      .def_readonly("tasks", &WavePlan::tasks);
-  m.def("plan_wave", &plan_wave, py::arg("plan"), py::arg("in_lo"), py::arg("in_hi"), py::arg("owned_rows"),
-        py::arg("tile_rows"), py::arg("col_groups"), py::arg("load_parts") = 1, py::arg("store_parts") = 1,
-        py::arg("load_lead") = 2, py::arg("level_gap") = 1);
 
   // ---------------------------------------------------------------- CPU oracle
   m.def(
@@ -329,7 +304,7 @@ PYBIND11_MODULE(_pconv_native, m) {
         py::arg("rows_out"), py::arg("iters") = 8,
         "ms per pitched H2D + D2H pair issued concurrently on two streams (the pipeline's PCIe floor)");
   m.def("bind_to_device_numa", &bind_to_device_numa,
-        "Restrict this process to the CPUs local to the GPU (0: unchanged; PCONV_NUMA_BIND=0 disables)");
+        "Restrict this process to the CPUs local to the GPU (returns the CPUs kept; 0: unchanged)");
 
   py::class_<PinnedBuffer>(m, "PinnedBuffer", py::buffer_protocol())
       .def(py::init<size_t>())
@@ -388,10 +363,13 @@ PYBIND11_MODULE(_pconv_native, m) {
       out.append(py::make_tuple(py::cast(kv.first), py::make_tuple(kv.second.lw, kv.second.m, kv.second.nw)));
     return out;
   });
-  m.def("set_prefetch_mode", &set_prefetch_mode, py::arg("mode"), py::arg("grid_cap") = 0,
+  m.def("set_prefetch_mode", &set_prefetch_mode, py::arg("mode"),
         "Buffer-op tile kernel: -1 tuned against the others (default), 0 never, 1 forced (with a set_swar_shape "
-        "shape it instantiates, that shape); grid_cap 0: one workgroup per tile, < 0: persistent resident "
-        "workgroups prefetching the next tile, > 0: persistent, at most that many workgroups (tests)");
+        "shape it instantiates, that shape)");
+  m.def("set_tune_candidates", &set_tune_candidates, py::arg("n"),
+        "How many of the latency model's best SWAR tile shapes the tuner times (default 6).");
+  m.def("set_float_shape", &set_float_shape, py::arg("m") = 0, py::arg("nw") = 0,
+        "Force the float temporal kernel's tile (m rows per wave, nw waves; m=0: model / tuner).");
   m.def("swar_prefetch_shapes", []() {
     py::list out;
     for (const auto& s : swar_prefetch_shapes()) out.append(py::make_tuple(s.lw, s.m, s.nw));
@@ -474,8 +452,6 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("kernel_copies") = false, py::arg("stream_chunks") = 0)
       .def_property_readonly("band", &BandEngine::band)
       .def("stream_plan", &BandEngine::stream_plan, py::arg("reps"), py::arg("in_r0"), py::arg("in_r1"))
-      .def("wave_able", &BandEngine::wave_able, py::arg("reps"), py::arg("in_r0"), py::arg("in_r1"))
-      .def("wave_tasks", &BandEngine::wave_tasks, py::arg("reps"), py::arg("in_r0"), py::arg("in_r1"))
       .def_property_readonly("halo", [](const BandEngine& e) { return e.layout().halo; })
       .def_property_readonly("fuse", [](const BandEngine& e) { return e.options().fuse; })
       .def_property_readonly("cached_graphs", &BandEngine::cached_graphs)
@@ -598,9 +574,12 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
                        int concurrent, bool graphs, bool step_graphs, py::object band, bool slot_comm,
-                       int stream_chunks) {
+                       int stream_chunks, bool stagger, bool cu_mask_queues, bool head_on_slot_streams) {
              EngineOptions o;
              o.stream_chunks = stream_chunks;
+             o.stagger = stagger;
+             o.cu_mask_queues = cu_mask_queues;
+             o.head_on_slot_streams = head_on_slot_streams;
              o.device = device;
              o.halo_depth = halo;
              o.fuse = fuse;
@@ -616,7 +595,8 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("rank") = 0, py::arg("world") = 1, py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1,
            py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1,
            py::arg("graphs") = false, py::arg("step_graphs") = true,
-           py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0)
+           py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0,
+           py::arg("stagger") = true, py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -644,6 +624,16 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_property_readonly("concurrent", &BandPipeline::concurrent)
       .def_property_readonly("graphs", &BandPipeline::graphs)
       .def_property_readonly("step_graphs", &BandPipeline::step_graphs)
+      .def_property_readonly("options",
+                             [](BandPipeline& p) {
+                               const EngineOptions& o = p.slot(0).options();
+                               py::dict d;
+                               d["stream_chunks"] = o.stream_chunks;
+                               d["stagger"] = o.stagger;
+                               d["cu_mask_queues"] = o.cu_mask_queues;
+                               d["head_on_slot_streams"] = o.head_on_slot_streams;
+                               return d;
+                             })
       .def("enable_trace", &BandPipeline::enable_trace, py::arg("images"),
            "Time the stages of the next `images` submits (directly issued pipelines only)")
       .def("trace", &BandPipeline::trace, py::call_guard<py::gil_scoped_release>(),
@@ -678,14 +668,22 @@ PYBIND11_MODULE(_pconv_native, m) {
   // ---------------------------------------------------------------- HIP IPC halos
   m.def("ipc_create_segment", &ipc_create_segment, py::arg("name"), py::arg("world"), py::arg("slots"),
         "create the zeroed shared flag segment of an IPC halo job (one rank)");
+  m.def("ipc_pull_probe", &ipc_pull_probe, py::arg("form"), py::arg("bytes"), py::arg("host_source"),
+        py::arg("iters") = 50, py::arg("device") = 0, py::arg("workgroups") = 0,
+        py::call_guard<py::gil_scoped_release>(),
+        "ms per IPC exchange of one pull form (grid|single|sdma), `bytes` per side from a pinned host buffer "
+        "(host_source: stand-in for a peer GPU behind xGMI) or this GPU's HBM; self-neighbour flag protocol");
+  m.def("ipc_grid_workgroups", &ipc_grid_workgroups, py::arg("bytes"));
   m.def("ipc_unlink_segment", &ipc_unlink_segment, py::arg("name"),
         "remove the segment's name (mappings stay valid; call once every rank has mapped it)");
   py::class_<IpcHaloTransport, HaloTransport, std::shared_ptr<IpcHaloTransport>>(m, "IpcHaloTransport")
-      .def(py::init([](BandEngine& e, const std::string& segment, int slot, int slots, double timeout_s) {
-             return std::make_shared<IpcHaloTransport>(e, segment, slot, slots, timeout_s);
+      .def(py::init([](BandEngine& e, const std::string& segment, int slot, int slots, double timeout_s,
+                       const std::string& pull) {
+             return std::make_shared<IpcHaloTransport>(e, segment, slot, slots, timeout_s, parse_ipc_pull(pull));
            }),
            py::arg("engine"), py::arg("segment"), py::arg("slot") = 0, py::arg("slots") = 1,
-           py::arg("timeout_s") = 30.0, py::keep_alive<1, 2>())
+           py::arg("timeout_s") = 30.0, py::arg("pull") = "grid", py::keep_alive<1, 2>())
+      .def_property_readonly("pull", [](const IpcHaloTransport& t) { return std::string(ipc_pull_name(t.pull())); })
       .def("local_handles", [](const IpcHaloTransport& t) {
         const auto v = t.local_handles();
         return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());

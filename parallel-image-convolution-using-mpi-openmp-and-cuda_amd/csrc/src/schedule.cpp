@@ -138,173 +138,6 @@ StreamPlan plan_streamed(const std::vector<Phase>& plan, int64_t in_lo, int64_t 
   return sp;
 }
 
-namespace {
-
-int64_t floor_div(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
-
-}  // namespace
-
-WavePlan plan_wave(const std::vector<Phase>& plan, int64_t in_lo, int64_t in_hi, int64_t owned_rows, int tile_rows,
-                   const std::vector<int>& col_groups, int load_parts, int store_parts, int load_lead,
-                   int level_gap) {
-  PCONV_CHECK(streamable(plan), "plan_wave: the plan must be exchange-free with one launch per phase");
-  PCONV_CHECK(in_lo <= 0 && in_hi >= owned_rows && in_lo < in_hi, "plan_wave: input rows must cover the band");
-  PCONV_CHECK(tile_rows >= 1 && load_parts >= 1 && store_parts >= 1, "plan_wave: bad tiling");
-  const int L = static_cast<int>(plan.size());
-  PCONV_CHECK(static_cast<int>(col_groups.size()) >= L + 1, "plan_wave: one column-group count per level");
-  WavePlan wp;
-  wp.levels = L;
-  wp.tile_rows = tile_rows;
-  wp.steps.assign(L + 1, 0);
-  wp.lo.assign(L + 1, in_lo);
-  wp.hi.assign(L + 1, in_hi);
-  for (int j = 1; j <= L; ++j) {
-    const LaunchSpec& l = plan[j - 1].launches[0];
-    wp.steps[j] = l.steps;
-    wp.lo[j] = l.lo;
-    wp.hi[j] = l.hi;
-    PCONV_CHECK(l.hi > l.lo && col_groups[j] >= 1, "plan_wave: empty level");
-  }
-  PCONV_CHECK(wp.lo[L] <= 0 && wp.hi[L] >= owned_rows, "plan_wave: the last level must cover the owned rows");
-  const int64_t V = tile_rows;
-  wp.tiles.resize(L + 1);
-  wp.arrivals.resize(L + 1);
-  wp.counter_base.resize(L + 1);
-  for (int j = 0; j <= L; ++j) {
-    wp.tiles[j] = static_cast<int>((wp.hi[j] - wp.lo[j] + V - 1) / V);
-    wp.arrivals[j] = j == 0 ? load_parts : col_groups[j];
-    wp.counter_base[j] = wp.counters;
-    wp.counters += wp.tiles[j];
-  }
-  auto tile_a = [&](int j, int64_t t) { return wp.lo[j] + t * V; };
-  auto tile_b = [&](int j, int64_t t) { return std::min(wp.lo[j] + (t + 1) * V, wp.hi[j]); };
-  // Tiles of level j overlapping rows [r0, r1) (clipped to the level).
-  auto tiles_of = [&](int j, int64_t r0, int64_t r1, int64_t& t0, int64_t& t1) {
-    r0 = std::max(r0, wp.lo[j]);
-    r1 = std::min(r1, wp.hi[j]);
-    if (r1 <= r0) {
-      t0 = 0;
-      t1 = -1;
-      return;
-    }
-    t0 = floor_div(r0 - wp.lo[j], V);
-    t1 = floor_div(r1 - 1 - wp.lo[j], V);
-  };
-  struct Keyed {
-    int64_t rank;
-    WaveTask t;
-  };
-  std::vector<Keyed> all;
-  std::vector<std::vector<int64_t>> rank(L + 1);
-  const int64_t kLoadLead = std::max(0, load_lead);  // loads take their tickets this many ranks early
-  // rows of a tile split into `parts` row parts (empty parts dropped)
-  auto parts_of = [](int64_t a, int64_t b, int parts, int p, int64_t& pa, int64_t& pb) {
-    pa = a + (b - a) * p / parts;
-    pb = a + (b - a) * (p + 1) / parts;
-  };
-  // level 0: loads
-  rank[0].assign(wp.tiles[0], 0);
-  for (int64_t t = 0; t < wp.tiles[0]; ++t) {
-    rank[0][t] = t;
-    for (int p = 0; p < load_parts; ++p) {
-      WaveTask k;
-      int64_t pa, pb;
-      parts_of(tile_a(0, t), tile_b(0, t), load_parts, p, pa, pb);
-      k.kind = 0;
-      k.level = 0;
-      k.a = static_cast<int32_t>(pa);
-      k.b = static_cast<int32_t>(pb);
-      k.part = p;
-      k.tile = static_cast<int32_t>(t);
-      all.push_back({t - kLoadLead, k});
-    }
-  }
-  for (int j = 1; j <= L; ++j) {
-    rank[j].assign(wp.tiles[j], 0);
-    const int64_t s = wp.steps[j], sp = wp.steps[j - 1];
-    for (int64_t t = 0; t < wp.tiles[j]; ++t) {
-      const int64_t a = tile_a(j, t), b = tile_b(j, t);
-      int64_t r0, r1;
-      tiles_of(j - 1, a - s, b + s, r0, r1);  // rows it reads
-      PCONV_CHECK(r1 >= r0, "plan_wave: a level tile reads nothing of the level before");
-      if (j >= 2) {
-        // level-(j-1) tiles whose reads [a'-sp, b'+sp) reach rows [a, b) of
-        // level j-2, which this tile overwrites
-        int64_t w0, w1;
-        tiles_of(j - 1, a - sp, b + sp, w0, w1);
-        if (w1 >= w0) {
-          r0 = std::min(r0, w0);
-          r1 = std::max(r1, w1);
-        }
-      }
-      r0 = std::max<int64_t>(r0, 0);
-      r1 = std::min<int64_t>(r1, wp.tiles[j - 1] - 1);
-      int64_t rk = 0;
-      for (int64_t d = r0; d <= r1; ++d) rk = std::max(rk, rank[j - 1][d]);
-      rank[j][t] = rk + std::max(1, level_gap);
-      for (int g = 0; g < col_groups[j]; ++g) {
-        WaveTask k;
-        k.kind = 1;
-        k.level = j;
-        k.a = static_cast<int32_t>(a);
-        k.b = static_cast<int32_t>(b);
-        k.part = g;
-        k.tile = static_cast<int32_t>(t);
-        k.dep_lo = static_cast<int32_t>(r0);
-        k.dep_hi = static_cast<int32_t>(r1);
-        all.push_back({rank[j][t], k});
-      }
-    }
-  }
-  // stores: the owned rows of each level-L tile
-  for (int64_t t = 0; t < wp.tiles[L]; ++t) {
-    const int64_t a = std::max<int64_t>(tile_a(L, t), 0), b = std::min<int64_t>(tile_b(L, t), owned_rows);
-    if (b <= a) continue;
-    for (int p = 0; p < store_parts; ++p) {
-      WaveTask k;
-      int64_t pa, pb;
-      parts_of(a, b, store_parts, p, pa, pb);
-      if (pb <= pa) continue;
-      k.kind = 2;
-      k.level = L + 1;
-      k.a = static_cast<int32_t>(pa);
-      k.b = static_cast<int32_t>(pb);
-      k.part = p;
-      k.tile = static_cast<int32_t>(t);
-      k.dep_lo = k.dep_hi = static_cast<int32_t>(t);
-      all.push_back({rank[L][t] + 1, k});
-    }
-  }
-  std::stable_sort(all.begin(), all.end(), [](const Keyed& x, const Keyed& y) {
-    return x.rank != y.rank ? x.rank < y.rank : x.t.level < y.t.level;
-  });
-  wp.tasks.reserve(all.size());
-  for (const auto& k : all) wp.tasks.push_back(k.t);
-  check_wave_order(wp);
-  return wp;
-}
-
-void check_wave_order(const WavePlan& wp) {
-  // arrivals seen so far per counter, in ticket order
-  std::vector<int> seen(static_cast<size_t>(wp.counters), 0);
-  for (size_t i = 0; i < wp.tasks.size(); ++i) {
-    const WaveTask& k = wp.tasks[i];
-    const int dl = k.dep_level();
-    if (dl >= 0) {
-      PCONV_CHECK(dl <= wp.levels && k.dep_lo <= k.dep_hi, "wave plan: dependency out of range");
-      for (int d = k.dep_lo; d <= k.dep_hi; ++d) {
-        PCONV_CHECK(d >= 0 && d < wp.tiles[dl], "wave plan: dependency tile out of range");
-        PCONV_CHECK(seen[wp.counter_base[dl] + d] == wp.arrivals[dl],
-                    "wave plan: task " + std::to_string(i) + " waits on a tile whose tasks are not all earlier");
-      }
-    }
-    if (k.kind != 2) ++seen[wp.counter_base[k.level] + k.tile];
-  }
-  for (int j = 0; j <= wp.levels; ++j)
-    for (int t = 0; t < wp.tiles[j]; ++t)
-      PCONV_CHECK(seen[wp.counter_base[j] + t] == wp.arrivals[j], "wave plan: a tile misses tasks");
-}
-
 std::string describe_plan(const std::vector<Phase>& plan) {
   std::ostringstream os;
   for (size_t i = 0; i < plan.size(); ++i) {

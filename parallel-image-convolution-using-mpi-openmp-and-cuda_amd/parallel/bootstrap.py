@@ -89,7 +89,7 @@ def make_rccl_comm(device: int, group=None):
     return n.RcclComm(uid, rank, world, device)
 
 
-def make_ipc_transports(engines, timeout_s: float = 30.0, group=None):
+def make_ipc_transports(engines, timeout_s: float = 30.0, group=None, pull: str = "grid"):
     """HIP-IPC halo transports for this rank's pipeline slots (collective).
 
     Rank 0 creates the job's shared flag segment and broadcasts its name;
@@ -106,16 +106,24 @@ def make_ipc_transports(engines, timeout_s: float = 30.0, group=None):
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     slots = len(engines)
-    name = None
+    name, err = None, None
     if rank == 0:
         name = f"/pconv_ipc_{os.getpid()}_{secrets.token_hex(4)}"
-        n.ipc_create_segment(name, world, slots)
+        try:
+            n.ipc_create_segment(name, world, slots)
+        except Exception as e:  # every rank must hear of it, not wait in the broadcast
+            err, name = e, ""
+    created = False
     try:
-        name = broadcast_bytes(name.encode() if name else None, 0, group).decode()
-        ts = [n.IpcHaloTransport(e, name, k, slots, float(timeout_s)) for k, e in enumerate(engines)]
+        # an empty name tells the other ranks that rank 0 could not create the segment
+        name = broadcast_bytes(name.encode() if name is not None else None, 0, group).decode()
+        if not name:
+            raise RuntimeError(f"IPC halo segment creation failed on rank 0: {err}")
+        created = True
+        ts = [n.IpcHaloTransport(e, name, k, slots, float(timeout_s), pull) for k, e in enumerate(engines)]
     finally:
         barrier(group)
-        if rank == 0:
+        if rank == 0 and created:
             n.ipc_unlink_segment(name)
     mine = [t.local_handles() for t in ts]
     if dist.is_initialized() and world > 1:
@@ -191,11 +199,12 @@ def device_local_cpus(device: int, sysfs: str = "/sys/bus/pci/devices") -> Optio
     return cpus or None
 
 
-def bind_to_device_numa(device: int) -> Optional[int]:
+def bind_to_device_numa(device: int, enabled: bool = True) -> Optional[int]:
     """Restrict this process to the CPUs local to its GPU (intersected with
-    the CPUs it may use).  Off with PCONV_NUMA_BIND=0.  Returns the number of
-    CPUs kept, or None when nothing was changed."""
-    if os.environ.get("PCONV_NUMA_BIND", "1") == "0" or not hasattr(os, "sched_setaffinity"):
+    the CPUs it may use); `enabled=False` (bench.py --numa-bind off) leaves
+    the affinity alone.  Returns the number of CPUs kept, or None when
+    nothing was changed."""
+    if not enabled or not hasattr(os, "sched_setaffinity"):
         return None
     local = device_local_cpus(device)
     if not local:
@@ -221,8 +230,8 @@ def cpu_rank_slice(local_rank: int, local_world: int, allowed, budget: int) -> l
     return cpus[lo:lo + k]
 
 
-def bind_cpu_rank(local_rank: int, local_world: int) -> Optional[list]:
-    """Opt-in (PCONV_CPU_BIND=1): bind this CPU rank to its slice
+def bind_cpu_rank(local_rank: int, local_world: int, bind: bool = False) -> Optional[list]:
+    """Opt-in (`bind=True`, run.py --cpu-bind): bind this CPU rank to its slice
     (``cpu_rank_slice``) before its OpenMP team starts (team threads inherit
     the affinity of the thread that creates them).  Always: torch's own pools
     drop to one thread, so a rank runs its team and nothing else.
@@ -234,7 +243,7 @@ def bind_cpu_rank(local_rank: int, local_world: int) -> Optional[list]:
     were the steadiest, so binding is off by default.  Reference: one team
     per rank (open-mp/omp_convolution.c:292,297)."""
     torch.set_num_threads(1)
-    if os.environ.get("PCONV_CPU_BIND", "0") != "1" or not hasattr(os, "sched_setaffinity"):
+    if not bind or not hasattr(os, "sched_setaffinity"):
         return None
     n = require_native()
     budget = n.default_cpu_threads()

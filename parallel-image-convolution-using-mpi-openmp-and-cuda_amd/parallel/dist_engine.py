@@ -59,7 +59,14 @@ class DistributedBlur:
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
                  step_graphs: Optional[bool] = None, graph_capture: bool = True, slot_exchange: bool = False,
                  self_neighbours: bool = False, slot_comm: bool = False, stream_chunks: int = 0,
-                 ipc_timeout_s: float = 30.0):
+                 ipc_timeout_s: float = 30.0, ipc_pull: str = "grid", stagger: bool = True,
+                 cu_mask_queues: bool = True, head_on_slot_streams: bool = True):
+        """Pipeline policy (native EngineOptions, echoed by bench.py's JSON
+        config): `stagger` starts the first images of a burst one upload after
+        another; `cu_mask_queues` puts every slot stream on its own hardware
+        queue; `head_on_slot_streams` runs a streamed head image's copies on
+        the next slots' streams; `ipc_pull` is the IPC transport's pull form
+        (grid | single | sdma, ipc_halo.hpp)."""
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -76,7 +83,8 @@ class DistributedBlur:
         # that many chunks and its levels advance behind them (H2D, launches
         # and D2H of ONE image overlap; schedule.hpp plan_streamed)
         kw = dict(halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant, slots=int(slots),
-                  concurrent=int(concurrent), stream_chunks=int(stream_chunks))
+                  concurrent=int(concurrent), stream_chunks=int(stream_chunks), stagger=bool(stagger),
+                  cu_mask_queues=bool(cu_mask_queues), head_on_slot_streams=bool(head_on_slot_streams))
         if self_neighbours:
             # One-GPU emulation of rank `rank` of a `world`-way split whose halos
             # really move: its neighbours are replaced by itself (a 1-rank
@@ -156,7 +164,8 @@ class DistributedBlur:
             # by flag kernels (ipc_halo.hpp); one transport per slot
             from .bootstrap import make_ipc_transports
 
-            self.ipc = make_ipc_transports([self.pipe.slot(k) for k in range(self.slots)], ipc_timeout_s)
+            self.ipc = make_ipc_transports([self.pipe.slot(k) for k in range(self.slots)], ipc_timeout_s,
+                                           pull=ipc_pull)
             for k, t in enumerate(self.ipc):
                 self.pipe.attach_slot_transport(k, t)
         elif self.slot_exchange:
@@ -187,6 +196,18 @@ class DistributedBlur:
                 raise ValueError(f"unknown transport {transport!r} (rccl|ipc|gloo-host|none)")
 
     # ------------------------------------------------------------ inputs
+    @property
+    def h2d_bytes_per_image(self) -> int:
+        """Host-to-device bytes this rank moves per image: its band plus the
+        pre-loaded ghost rows (exchange modes upload only the band)."""
+        a, b = self.input_rows
+        return (b - a) * self.row_bytes
+
+    @property
+    def d2h_bytes_per_image(self) -> int:
+        """Device-to-host bytes per image: the owned rows."""
+        return self.band.rows * self.row_bytes
+
     @property
     def input_rows(self):
         """Global rows [first, last) held by the pinned input buffers."""

@@ -97,6 +97,11 @@ def parse(argv: List[str]) -> argparse.Namespace:
     p.add_argument("--checkpoint-every", type=int, default=0, metavar="K",
                    help="every K repetitions write the whole image to <out>.rep<N> (each rank pwrites its band); "
                         "resume = rerun on that file with the remaining repetitions")
+    p.add_argument("--cpu-bind", action="store_true",
+                   help="--backend cpu/omp: bind each rank to its own CPU slice (off by default: unbound teams "
+                        "were steadier on a shared host, profiles/r03/hybrid/)")
+    p.add_argument("--no-numa-bind", action="store_true",
+                   help="--backend hip: leave each rank's CPU affinity alone (default: the GPU's NUMA node)")
     a = p.parse_args(argv)
     if a.width < 1 or a.height < 1 or a.reps < 0 or a.checkpoint_every < 0:
         sys.stderr.write(usage(prog))
@@ -208,7 +213,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         if a.backend == "hip":
             device = ctx.local_rank % max(1, n.device_count())
             n.set_device(device)
-            if world > 1:
+            if world > 1 and not a.no_numa_bind:
                 n.bind_to_device_numa(device)
             runner = _HipBand(a, rank, world, device)
         else:
@@ -217,7 +222,7 @@ def main(argv: Optional[List[str]] = None) -> int:
             from .bootstrap import bind_cpu_rank
 
             local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
-            cpus = bind_cpu_rank(ctx.local_rank, local_world)
+            cpus = bind_cpu_rank(ctx.local_rank, local_world, a.cpu_bind)
             if a.backend == "omp":
                 n.set_cpu_threads(omp_team_size(a.threads, cpus, n.default_cpu_threads(), local_world))
             runner = _CpuBand(a, rank, world, omp=a.backend == "omp")

@@ -123,14 +123,12 @@ def test_parse_cpulist():
     assert parse_cpulist("") == set()
 
 
-def test_numa_bind_is_a_noop_without_a_gpu(pconv_mod, monkeypatch):
-    """No device (or PCONV_NUMA_BIND=0): binding changes nothing, raises nothing."""
+def test_numa_bind_is_a_noop_without_a_gpu(pconv_mod):
+    """No device (or enabled=False): binding changes nothing, raises nothing."""
     from pconv.parallel.bootstrap import bind_to_device_numa
 
     before = os.sched_getaffinity(0)
-    monkeypatch.setenv("PCONV_NUMA_BIND", "0")
-    assert bind_to_device_numa(0) is None
-    monkeypatch.setenv("PCONV_NUMA_BIND", "1")
+    assert bind_to_device_numa(0, enabled=False) is None
     assert bind_to_device_numa(0) is None  # this container has no GPU
     assert os.sched_getaffinity(0) == before
 

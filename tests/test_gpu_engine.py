@@ -119,9 +119,8 @@ def test_cli_hip_ring_staging(pconv_mod, tmp_path, rng, typ, filt, chunk):
     w, h = 203, 311
     img = rng.integers(0, 256, size=(h, w, c) if c > 1 else (h, w), dtype=np.uint8)
     pconv_mod.write_raw(str(tmp_path / "img.raw"), img)
-    env = dict(os.environ, PCONV_RING_CHUNK_BYTES=str(chunk))
-    r = subprocess.run([CONV_BIN, "img.raw", str(w), str(h), "13", typ, "--filter", filt, "--json"],
-                       cwd=tmp_path, capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run([CONV_BIN, "img.raw", str(w), str(h), "13", typ, "--filter", filt, "--json",
+                        "--ring-chunk-bytes", str(chunk)], cwd=tmp_path, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     meta = json.loads(r.stdout.strip().splitlines()[-1])
     assert "read_and_h2d" in meta["phases_s"] and "d2h_and_write" in meta["phases_s"], meta["phases_s"]
@@ -334,44 +333,15 @@ def test_copy_pair_floor(native):
         native.copy_pair_floor_ms(0, rb, 0, rows, 4)
 
 
-@pytest.mark.parametrize("typ,filt,w,h,reps", [("rgb", "gaussian", 1536, 1024, 2000), ("grey", "gaussian", 2048, 2048, 4000),
-                                               ("rgb", "box", 1024, 768, 600)])
-def test_cli_auto_backend_hands_off_to_gpu(pconv_mod, tmp_path, typ, filt, w, h, reps):
-    """`--backend auto` with the GPU brought up beside the CPU
-    (PCONV_AUTO_GPU_MIN_S=0, PCONV_AUTO_HANDOFF=1): the CPU (one thread here,
-    so it is still busy when the device is up) runs
-    repetitions while the GPU comes up, then the newest CPU frame moves to the
-    GPU, which runs the rest; the result equals the CPU oracle of all `reps`
-    bit for bit whatever the handoff point.  (Jobs of ~1-2 s on one CPU
-    thread: the GPU comes up within a few hundred ms.)"""
-    from pconv.models.filters import get_filter
-
-    env = dict(os.environ, PCONV_AUTO_GPU_MIN_S="0", PCONV_AUTO_HANDOFF="1")
-    r = subprocess.run([CONV_BIN, "s.raw", str(w), str(h), str(reps), typ, "--synthetic", "11", "--backend", "auto",
-                        "--threads", "1", "--filter", filt, "--json", "--quiet"], cwd=tmp_path, capture_output=True,
-                       text=True, timeout=300, env=env)
-    assert r.returncode == 0, r.stderr
-    meta = json.loads(r.stdout.strip().splitlines()[-1])
-    assert meta["cpu_reps"] >= 1 and meta["gpu_reps"] >= 1 and meta["cpu_reps"] + meta["gpu_reps"] == reps, meta
-    assert meta["gpus"] == 1 and meta["kernel"].startswith("cpu-omp+")
-    out = pconv_mod.read_raw(str(tmp_path / "blur_s.raw"), w, h, typ)
-    img = pconv_mod.synthetic_image(w, h, typ, seed=11)
-    ref = np.empty_like(img)
-    pconv_mod.native.cpu_convolve(img.reshape(-1), ref.reshape(-1), w, h, typ, reps, get_filter(filt).to_native(),
-                                  True, 0)
-    assert np.array_equal(out, ref)
-
-
 @pytest.mark.parametrize("typ,filt,reps", [("rgb", "gaussian", 40), ("grey", "edge", 9)])
 def test_cli_auto_backend_gpu_path(pconv_mod, tmp_path, typ, filt, reps):
     """`--backend auto` on a job priced above the GPU's start-up (forced with
-    PCONV_AUTO_GPU_MIN_S=0): the GPU path runs on its own, all repetitions on
-    the GPU, bit-exact with the oracle."""
+    --auto-gpu-min 0): the GPU path runs on its own, all repetitions on the
+    GPU, bit-exact with the oracle."""
     w, h = 320, 200
-    env = dict(os.environ, PCONV_AUTO_GPU_MIN_S="0")
     r = subprocess.run([CONV_BIN, "s.raw", str(w), str(h), str(reps), typ, "--synthetic", "3", "--backend", "auto",
-                        "--filter", filt, "--json", "--check", "--quiet"], cwd=tmp_path, capture_output=True,
-                       text=True, timeout=300, env=env)
+                        "--filter", filt, "--json", "--check", "--quiet", "--auto-gpu-min", "0"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     meta = json.loads(r.stdout.strip().splitlines()[-1])
     assert meta["gpus"] == 1 and meta["cpu_reps"] == 0 and meta["gpu_reps"] == reps and meta["mismatches"] == 0

@@ -46,7 +46,9 @@ def _worker(rank, world, port, cfg, q):
         blur = DistributedBlur(cfg["w"], cfg["h"], cfg["ch"], cfg["filter"], cfg["reps"], rank=rank, world=world,
                                device=0, halo=cfg["halo"], fuse=cfg["fuse"], slots=cfg["slots"], transport="ipc",
                                slot_exchange=True, graph_capture=cfg["graph"], slot_comm=cfg["overlap"],
-                               overlap=cfg["overlap"], ipc_timeout_s=cfg.get("timeout", 30.0))
+                               overlap=cfg["overlap"], ipc_timeout_s=cfg.get("timeout", 30.0),
+                               ipc_pull=cfg.get("pull", "grid"))
+        assert all(t.pull == cfg.get("pull", "grid") for t in blur.ipc)
         if cfg.get("stall") and rank == world - 1:
             barrier()  # set-up done; this rank then never exchanges
             q.put((rank, None, None, 0))
@@ -87,7 +89,7 @@ def _run(pconv_mod, world, cfg, timeout=300):
     return res
 
 
-@pytest.mark.parametrize("world,ch,filt,halo,fuse,reps,graph,overlap", [
+CASES = [
     (2, "rgb", "gaussian", 8, 8, 40, True, False),     # one zone exchange per image, captured
     (2, "grey", "gaussian", 4, 4, 19, True, True),     # 5 exchanges per image, split phases, captured
     (3, "rgb", "gaussian", 6, 3, 19, False, True),     # direct issue, interior || exchange
@@ -95,11 +97,21 @@ def _run(pconv_mod, world, cfg, timeout=300):
     (4, "grey", "edge", 3, 3, 11, False, False),
     (8, "rgb", "gaussian", 8, 8, 40, True, False),     # the 8-way split of the headline's shape
     (8, "grey", "gaussian", 5, 5, 23, True, True),
-])
-def test_ipc_halo_bit_exact(pconv_mod, world, ch, filt, halo, fuse, reps, graph, overlap):
+]
+
+
+@pytest.mark.parametrize("world,ch,filt,halo,fuse,reps,graph,overlap,pull",
+                         [c + ("grid",) for c in CASES] +
+                         [CASES[i] + (p,) for p in ("single", "sdma") for i in (1, 2, 3, 5, 6)])
+def test_ipc_halo_bit_exact(pconv_mod, world, ch, filt, halo, fuse, reps, graph, overlap, pull):
+    """Every pull form: grid (the default, one dispatch of >= 8 workgroups,
+    each with its own acquire), single (one workgroup) and sdma (flag kernels
+    around SDMA copies)."""
     w, h, slots = 57, 160, 2
     cfg = dict(w=w, h=h, ch=ch, filter=filt, reps=reps, halo=halo, fuse=fuse, slots=slots, graph=graph,
-               overlap=overlap, seed=11, images=slots + 2)
+               overlap=overlap, seed=11, images=slots + 2, pull=pull)
+    if pull == "grid":
+        assert pconv_mod.native.ipc_grid_workgroups(halo * 256) >= 8
     res = _run(pconv_mod, world, cfg)
     img = pconv_mod.synthetic_image(w, h, ch, seed=11)
     ref = pconv_mod.numpy_convolve(img, reps, filt).reshape(h, -1)
@@ -111,11 +123,12 @@ def test_ipc_halo_bit_exact(pconv_mod, world, ch, filt, halo, fuse, reps, graph,
         assert n_exch == per_image * cfg["images"], (rank, n_exch)
 
 
-def test_ipc_stalled_neighbour_times_out(pconv_mod):
+@pytest.mark.parametrize("pull", ["grid", "single", "sdma"])
+def test_ipc_stalled_neighbour_times_out(pconv_mod, pull):
     """A neighbour that never exchanges: the waiting rank's flag kernel gives
     up after its timeout (no wave spins forever) and drain() raises."""
     cfg = dict(w=40, h=64, ch="grey", filter="gaussian", reps=8, halo=8, fuse=8, slots=1, graph=True,
-               overlap=False, seed=3, images=1, stall=True, timeout=2.0)
+               overlap=False, seed=3, images=1, stall=True, timeout=2.0, pull=pull)
     res = _run(pconv_mod, 2, cfg, timeout=200)
     r0 = res[0]
     assert isinstance(r0[2], str) and "timed out" in r0[2], r0
@@ -127,3 +140,17 @@ def test_ipc_segments_unlinked():
     import glob
 
     assert not glob.glob("/dev/shm/pconv_ipc_*") and not glob.glob("/dev/shm/pconv_conv_*")
+
+
+@pytest.mark.parametrize("form,workgroups", [("grid", 0), ("grid", 8), ("grid", 13), ("grid", 64), ("single", 0),
+                                             ("sdma", 0)])
+@pytest.mark.parametrize("host_source", [False, True])
+def test_ipc_pull_probe(pconv_mod, form, workgroups, host_source):
+    """One process, self-neighbour flag protocol: each pull form moves the
+    8-way headline rank's ghost zone (2 x 40 rows x 5,760 B, ~460 KB) from
+    this GPU's HBM or from pinned host memory (the stand-in for a peer GPU
+    behind xGMI); the probe checks the exchange count, the error word and
+    every byte pulled, and returns ms per exchange."""
+    n = pconv_mod.native
+    ms = n.ipc_pull_probe(form, 40 * 5760, host_source, 20, 0, workgroups)
+    assert 0 < ms < 50, ms

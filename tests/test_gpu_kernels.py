@@ -127,10 +127,9 @@ def _run_fused(native, img, steps, r0, r1, halo, g_row0, height, variant="auto",
     return gpu, cpu.reshape(h + 2 * halo, lay["pitch"])
 
 
-@pytest.mark.parametrize("variant", ["temporal", "temporal_pk"])
 @pytest.mark.parametrize("channels", ["grey", "rgb", "rgba"])
 @pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 8, 11, 16])
-def test_temporal_matches_fused_reference(native, rng, channels, steps, variant):
+def test_temporal_matches_fused_reference(native, rng, channels, steps, variant="temporal"):
     c = CH[channels]
     for (h, w) in [(1, 3), (7, 5), (40, 33), (97, 130), (150, 700), (33, 1500)]:
         img = rng.integers(0, 256, size=(h, w, c) if c > 1 else (h, w), dtype=np.uint8)
@@ -181,7 +180,6 @@ def test_float_temporal_equals_repeated_single_steps(pconv_mod, rng):
 @pytest.mark.parametrize("steps", [2, 4, 8, 16])
 def test_temporal_band_regions(native, rng, steps):
     _band_regions(native, steps, "temporal")
-    _band_regions(native, steps, "temporal_pk")
 
 
 def _band_regions(native, steps, variant, filt="gaussian"):
@@ -233,18 +231,17 @@ def test_every_swar_shape_bit_exact(native, rng, form):
         native.set_swar_alt(-1)
 
 
-@pytest.mark.parametrize("cap", [0, 13])
+@pytest.mark.parametrize("swizzle", [True, False])
 @pytest.mark.parametrize("form", [0, 1])
-def test_prefetch_kernel_every_shape_bit_exact(native, rng, form, cap):
+def test_prefetch_kernel_every_shape_bit_exact(native, rng, form, swizzle):
     """The buffer-op tile kernel (k_swar_pf), forced in each shape and step
-    form: whole images and band regions with ghost rows and image edges,
-    guard-band canaries, untouched rows outside [r0, r1).  cap 0: one
-    workgroup per tile (the tuned form); cap 13: persistent, 13 workgroups
-    (not a multiple of the 8 XCDs) each walking many tiles — the prefetch of
-    the next tile, the rotated loop and the per-XCD tile runs."""
+    form, with and without the XCD-aware tile order: whole images and band
+    regions with ghost rows and image edges, guard-band canaries, untouched
+    rows outside [r0, r1)."""
     try:
         native.set_swar_alt(form)
-        native.set_prefetch_mode(1, cap)
+        native.set_xcd_swizzle(swizzle)
+        native.set_prefetch_mode(1)
         for (lw, m, nw) in native.swar_prefetch_shapes():
             native.set_swar_shape(lw, m, nw)
             for channels, steps in (("grey", 3), ("rgb", 4), ("rgba", 2), ("rgb", 8), ("grey", 8), ("rgb", 1)):
@@ -258,16 +255,17 @@ def test_prefetch_kernel_every_shape_bit_exact(native, rng, form, cap):
                 gpu, cpu = _run_fused(native, img[:40], steps, -5, 45, 16, 30, 200, variant="temporal")
                 assert np.array_equal(gpu[11:61], cpu[11:61]), (lw, m, nw, channels, steps, "band")
     finally:
-        native.set_prefetch_mode(-1, 0)
+        native.set_prefetch_mode(-1)
+        native.set_xcd_swizzle(True)
         native.set_swar_shape(0, 0, 0)
         native.set_swar_alt(-1)
         native.clear_swar_tuning()
 
 
 def test_prefetch_kernel_tuned_large_frame(native, rng):
-    """Tuned (default) choice on a frame with many tiles per resident
-    workgroup, with the prefetch kernel among the candidates, against the CPU
-    fused reference; and the prefetch kernel forced at its full grid."""
+    """Tuned (default) choice on a frame with many tiles (thousands of
+    workgroups), with the buffer-op kernel among the candidates, against the
+    CPU fused reference; and the buffer-op kernel forced in a tall shape."""
     import torch
 
     h, w = 1536, 4096
@@ -276,12 +274,12 @@ def test_prefetch_kernel_tuned_large_frame(native, rng):
         native.clear_swar_tuning()
         gpu, cpu = _run_fused(native, img, 8, 0, h, 8, 0, h, variant="temporal")
         assert np.array_equal(gpu, cpu)
-        native.set_prefetch_mode(1, -1)  # persistent, full resident grid
+        native.set_prefetch_mode(1)
         native.set_swar_shape(4, 16, 8)
         gpu, cpu = _run_fused(native, img, 8, 0, h, 8, 0, h, variant="temporal")
         assert np.array_equal(gpu, cpu)
     finally:
-        native.set_prefetch_mode(-1, 0)
+        native.set_prefetch_mode(-1)
         native.set_swar_shape(0, 0, 0)
         native.clear_swar_tuning()
         torch.cuda.synchronize()

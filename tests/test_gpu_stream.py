@@ -83,15 +83,14 @@ def test_streamed_preloaded_bands(pconv_mod, rng, mode, world, rank):
     _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps)
 
 
-@pytest.mark.parametrize("streams", ["cumask", "slots"])
+@pytest.mark.parametrize("on_slots", [False, True])
 @pytest.mark.parametrize("slots", [2, 3, 4])
-def test_head_stream_modes(pconv_mod, rng, monkeypatch, streams, slots):
-    """PCONV_HEAD_STREAMS: the streamed head image's copies on dedicated
-    queues, or on the next two slots' streams (falls back below 3 slots);
+def test_head_stream_modes(pconv_mod, rng, on_slots, slots):
+    """head_on_slot_streams: the streamed head image's copies on two pool
+    streams, or on the next two slots' streams (falls back below 3 slots);
     bursts and single images (blur.step) bit-exact."""
-    monkeypatch.setenv("PCONV_HEAD_STREAMS", streams)
     w, h, reps = 96, 120, 40
-    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=slots, mode="head")
+    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=slots, mode="head", head_on_slot_streams=on_slots)
     _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps, rounds=3)
     img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
     blur.load_image(img)

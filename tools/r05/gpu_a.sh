@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round 5, first GPU call after the clean-up (wave kernel, k_temporal and the
+# persistent k_swar_pf removed; env knobs -> options; external upload event;
+# IPC pull forms): the whole GPU suite, smoke, the driver's command, the
+# stagger A/B, the IPC pull probe and the 8-way ipc proxy per pull form.
+set -o pipefail
+OUT=gpurun_out/r05/a
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+  > $OUT/pytest_gpu.txt 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/pytest_gpu.txt; exit 1; }
+tail -1 $OUT/pytest_gpu.txt
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { echo "smoke failed"; cat $OUT/smoke.txt; exit 1; }
+tail -1 $OUT/smoke.txt
+timeout -k 10 200 python -u tools/r05/ipc_probe.py > $OUT/ipc_probe.jsonl 2> $OUT/ipc_probe.err || { echo "probe failed"; tail -20 $OUT/ipc_probe.err; exit 1; }
+cat $OUT/ipc_probe.jsonl
+one() {  # name, -- bench args
+  local name=$1; shift
+  timeout -k 10 300 python -u bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "bench $name failed"; tail -5 $OUT/$name.err; return 1; }
+  python - "$OUT/$name.json" "$name" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(f"{sys.argv[2]:14s} ms/step {d['ms_per_step']:.4f} latency {d['latency_ms']:.4f} pair {d['copy_floor']['pair_ms']} mism {d.get('mismatches')} vs {d.get('vs_baseline')}")
+PY
+}
+for i in a b c; do one bench_$i --gpus 1 --steps 20 --warmup 5 || exit 1; done
+for i in a b c; do one nostag_$i --gpus 1 --steps 20 --warmup 5 --no-stagger || exit 1; done
+one s200 --steps 200 --warmup 5 || exit 1
+one e8 --emulate 8:3 --steps 300 --warmup 10 || exit 1
+for p in grid single sdma; do one e8_ipc_$p --emulate 8:3 --emulate-halo ipc --ipc-pull $p --steps 300 --warmup 10 || exit 1; done
