@@ -151,6 +151,9 @@ def parse():
                         "queue, profiles/r04/slots_c/)")
     p.add_argument("--head-pool-streams", dest="head_on_slot_streams", action="store_false", default=True,
                    help="a streamed head image's copies on two pool streams (default: the next two slots' streams)")
+    p.add_argument("--stream-sync", type=int, choices=[0, 1, 2], default=0,
+                   help="streamed image's cross-stream order: 0 events, 1 downloads on the compute stream, 2 as 1 "
+                        "with signal-memory stream waits for the uploads")
     p.add_argument("--ipc-pull", choices=["grid", "single", "sdma"], default="grid",
                    help="halo mode ipc: how a rank pulls its neighbours' rows (grid: one dispatch of many "
                         "workgroups; single: one workgroup; sdma: flag kernels around SDMA peer copies)")
@@ -180,7 +183,11 @@ def oracle_rows(a, band):
     sub = np.empty((hi - lo) * a.width * c, np.uint8)
     n.synth_rows(sub, a.width, a.height, a.channels, int(a.seed), lo, hi - lo)
     ref = np.empty_like(sub)
-    n.cpu_convolve(sub, ref, a.width, hi - lo, a.channels, a.reps, get_filter(a.filter).to_native(), True, 0)
+    # the node's CPU budget split between the ranks on it (8 ranks with a team
+    # of the whole budget each would oversubscribe the host 8x)
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    threads = max(1, n.default_cpu_threads() // local)
+    n.cpu_convolve(sub, ref, a.width, hi - lo, a.channels, a.reps, get_filter(a.filter).to_native(), True, threads)
     return ref.reshape(hi - lo, -1)[band.y0 - lo:band.y0 - lo + band.rows]
 
 
@@ -246,6 +253,7 @@ def policy_kwargs(a) -> dict:
     """Pipeline policy flags -> DistributedBlur / native EngineOptions (echoed in the JSON config)."""
     return dict(stagger=getattr(a, "stagger", True), cu_mask_queues=getattr(a, "cu_mask_queues", True),
                 head_on_slot_streams=getattr(a, "head_on_slot_streams", True),
+                stream_sync=getattr(a, "stream_sync", 0),
                 ipc_pull=getattr(a, "ipc_pull", "grid"))
 
 
@@ -410,6 +418,7 @@ def run_native(a) -> int:
     cmd += [] if a.cu_mask_queues else ["--pool-queues"]
     cmd += [] if a.head_on_slot_streams else ["--head-pool-streams"]
     cmd += [] if a.numa_bind == "on" else ["--no-numa-bind"]
+    cmd += ["--stream-sync", str(a.stream_sync)]
     if a.emulate:
         cmd[cmd.index("--gpus") + 1] = "1"
         cmd += ["--emulate", a.emulate]  # one rank of a WORLD-way split, alone (per-rank proxy)
@@ -623,6 +632,7 @@ def main():
                 "halo_depth": int(blur.engine.halo),
                 "fuse": int(blur.engine.fuse),
                 "stream_chunks": int(a.stream_chunks),
+                "stream_sync": int(a.stream_sync),
                 "preload_halo": bool(blur.preload_halo),
                 "launches_per_step": int(stats.launches),
                 "exchanges_per_step": int(stats.exchanges),

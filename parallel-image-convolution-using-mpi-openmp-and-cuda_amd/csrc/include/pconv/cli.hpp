@@ -71,6 +71,7 @@ struct CliConfig {
   bool head_on_slot_streams = true;       // --bench: streamed head image's copies on the next slots' streams
   std::string ipc_pull = "grid";          // --transport ipc: pull form (grid | single | sdma)
   bool numa_bind = true;                  // N > 1: each rank on its GPU's NUMA node
+  int stream_sync = 0;                    // --bench: EngineOptions::stream_sync
 };
 
 // Parse argv.  Throws pconv::Error with the message to print on bad input.

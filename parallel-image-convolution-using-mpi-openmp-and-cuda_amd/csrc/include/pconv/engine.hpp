@@ -74,6 +74,12 @@ struct EngineOptions {
   // fork/join branches it measured 1.4-4.3x slower per image
   // (profiles/r04/stream_a/).
   int stream_chunks = 0;
+  // Cross-stream order of a streamed image: 0 events (upload -> launches ->
+  // download on three streams), 1 downloads on the compute stream right
+  // behind each chunk's launches, 2 as 1 with the upload -> launch order by
+  // stream memory operations on signal memory (hipStreamWriteValue32 /
+  // hipStreamWaitValue32) instead of events.
+  int stream_sync = 0;
   // Step graphs record an event right after their upload (upload_event()):
   // a pipeline staggers the first images of a burst on it (BandPipeline).
   bool upload_event = false;
@@ -180,8 +186,10 @@ class BandEngine {
   // Enqueue a streamed image: chunk uploads on `up`, launches on the compute
   // stream, downloads of the finished rows on `down` (cross-stream events per
   // chunk).  The caller orders `up` after any earlier use of these frames.
-  void enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
-                        const StreamPlan& sp, hipStream_t up, hipStream_t down);
+  // Returns the stream whose completion means the whole image is done
+  // (`down`, or the compute stream when the downloads ride on it).
+  hipStream_t enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
+                               const StreamPlan& sp, hipStream_t up, hipStream_t down);
   // With options().upload_event: recorded by every step graph once its
   // upload is done.
   const Event& upload_event() const { return ev_uploaded_; }
@@ -221,6 +229,8 @@ class BandEngine {
   hipStream_t cs_ = nullptr, ms_ = nullptr;
   Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_, ev_uploaded_;
   std::vector<Event> up_evs_, dn_evs_;  // streamed images: per chunk, uploaded / rows final
+  uint32_t* seq_flag_ = nullptr;        // stream_sync 2: chunk sequence word (signal memory)
+  uint32_t seq_ = 0;
   std::shared_ptr<HaloTransport> transport_;
   RunStats stats_;
   double wall_t0_ = 0;

@@ -76,6 +76,8 @@ std::string help_text(const std::string& prog) {
          "  --tune {auto,on,off}      SWAR tile-shape tuning (auto: off for a one-shot run, on in a server)\n"
          "  --ring-chunk-bytes B      one-shot staging ring chunk (default 32 MiB; 0 = one pinned image)\n"
          "  --no-numa-bind            N > 1: leave each rank's CPU affinity alone\n"
+         "  --stream-sync M           --bench: streamed image order: 0 events, 1 downloads on the compute\n"
+         "                            stream, 2 as 1 with signal-memory waits for the uploads\n"
          "\n"
          "       " + prog + " --serve SOCKET [--device D] [--idle-timeout S] [--max-engines N]\n"
          "                            resident service: initialise the GPU once, then run jobs sent by\n"
@@ -204,6 +206,8 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       char* end = nullptr;
       c.auto_gpu_min_s = std::strtod(v.c_str(), &end);
       if (v.empty() || *end != '\0' || !(c.auto_gpu_min_s >= 0)) PCONV_FAIL("invalid --auto-gpu-min '" + v + "'");
+    } else if (a == "--stream-sync") {
+      c.stream_sync = static_cast<int>(parse_int(next("--stream-sync"), "--stream-sync", 0, 2));
     } else if (a == "--no-numa-bind") {
       c.numa_bind = false;
     } else if (a == "--warmup") {

@@ -73,6 +73,7 @@ BandEngine::~BandEngine() {
   // Drain first: a cached graph may still be executing on the stream.
   if (cs_) (void)hipStreamSynchronize(cs_);
   if (ms_ && ms_ != cs_) (void)hipStreamSynchronize(ms_);
+  if (seq_flag_) (void)hipFree(seq_flag_);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : step_graphs_) (void)hipGraphExecDestroy(kv.second.exec);
 }
@@ -354,8 +355,8 @@ StreamPlan BandEngine::stream_plan(int reps, int64_t in_r0, int64_t in_r1) const
   return plan_streamed(ph, in_r0, in_r1, band_.rows, stream_cuts(in_r0, in_r1, opt_.stream_chunks));
 }
 
-void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
-                                  const StreamPlan& sp, hipStream_t up, hipStream_t down) {
+hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
+                                         const StreamPlan& sp, hipStream_t up, hipStream_t down) {
   TraceRange tr("pconv.streamed_image");
   PCONV_CHECK(!sp.chunks.empty(), "enqueue_streamed: empty stream plan");
   PCONV_CHECK(sp.chunks.front().up_lo == in_r0 && sp.chunks.back().up_hi == in_r1,
@@ -382,6 +383,66 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
                   hipStream_t s) {
     if (rows > 0) PCONV_HIP_CHECK(hipMemcpy2DAsync(dst, dpitch, src, spitch, rb, rows, kind, s));
   };
+  auto launches = [&](const StreamChunk& ch) {
+    for (size_t i = 0; i < ch.launches.size(); ++i) {
+      launch_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1, nullptr, 0),
+                     cs_, opt_.variant);
+      ++stats_.launches;
+    }
+  };
+  auto download = [&](const StreamChunk& ch, hipStream_t s) {
+    if (ch.down_hi > ch.down_lo && host_out)
+      copy(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, ch.down_hi - ch.down_lo,
+           hipMemcpyDeviceToHost, s);
+  };
+  const int sync = opt_.stream_sync;
+  if (sync == 2 && up != cs_) {
+    // Cross-stream order by stream memory operations on HSA signal memory
+    // (hipStreamWriteValue32 / hipStreamWaitValue32) instead of events: the
+    // upload stream writes chunk c's sequence number, the compute stream
+    // waits for it; downloads ride on the compute stream (mode 1's order).
+    if (!seq_flag_) {
+      void* f = nullptr;
+      PCONV_HIP_CHECK(hipExtMallocWithFlags(&f, 64, hipMallocSignalMemory));
+      seq_flag_ = static_cast<uint32_t*>(f);
+      PCONV_HIP_CHECK(hipMemset(seq_flag_, 0, 64));
+    }
+    const uint32_t base = seq_;
+    seq_ += static_cast<uint32_t>(nc);
+    for (size_t c = 0; c < nc; ++c) {
+      const StreamChunk& ch = sp.chunks[c];
+      copy(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, ch.up_hi - ch.up_lo,
+           hipMemcpyHostToDevice, up);
+      PCONV_HIP_CHECK(hipStreamWriteValue32(up, seq_flag_, base + static_cast<uint32_t>(c) + 1, 0));
+    }
+    for (size_t c = 0; c < nc; ++c) {
+      PCONV_HIP_CHECK(hipStreamWaitValue32(cs_, seq_flag_, base + static_cast<uint32_t>(c) + 1,
+                                           hipStreamWaitValueGte, 0xffffffffu));
+      launches(sp.chunks[c]);
+      download(sp.chunks[c], cs_);
+    }
+    cur_ = (c0 + sp.levels) & 1;
+    halo_valid_ = false;
+    return cs_;
+  }
+  if (sync == 1 || down == cs_) {
+    // Downloads on the compute stream right behind each chunk's launches
+    // (stream order, no launch -> D2H hop); uploads on `up` as in mode 0.
+    for (size_t c = 0; c < nc; ++c) {
+      const StreamChunk& ch = sp.chunks[c];
+      copy(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, ch.up_hi - ch.up_lo,
+           hipMemcpyHostToDevice, up);
+      if (up != cs_) up_evs_[c].record(up);
+    }
+    for (size_t c = 0; c < nc; ++c) {
+      if (up != cs_) up_evs_[c].wait_on(cs_);
+      launches(sp.chunks[c]);
+      download(sp.chunks[c], cs_);
+    }
+    cur_ = (c0 + sp.levels) & 1;
+    halo_valid_ = false;
+    return cs_;
+  }
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     copy(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, ch.up_hi - ch.up_lo,
@@ -392,30 +453,26 @@ void BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     if (up != cs_) up_evs_[c].wait_on(cs_);
-    for (size_t i = 0; i < ch.launches.size(); ++i) {
-      launch_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1, nullptr, 0),
-                     cs_, opt_.variant);
-      ++stats_.launches;
-      pending = true;
-    }
-    if (ch.down_hi > ch.down_lo && host_out && down != cs_) {
+    launches(ch);
+    if (!ch.launches.empty()) pending = true;
+    if (ch.down_hi > ch.down_lo && host_out) {
       dn_evs_[c].record(cs_);
       pending = false;
     }
   }
   // `down` finishing must mean the whole image is done (the next image of
   // these frames waits on it), also when launches follow the last download.
-  if (pending && down != cs_) dn_evs_[nc].record(cs_);
+  if (pending) dn_evs_[nc].record(cs_);
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     if (!(ch.down_hi > ch.down_lo && host_out)) continue;
-    if (down != cs_) dn_evs_[c].wait_on(down);
-    copy(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, ch.down_hi - ch.down_lo, hipMemcpyDeviceToHost,
-         down);
+    dn_evs_[c].wait_on(down);
+    download(ch, down);
   }
-  if (pending && down != cs_) dn_evs_[nc].wait_on(down);
+  if (pending) dn_evs_[nc].wait_on(down);
   cur_ = (c0 + sp.levels) & 1;
   halo_valid_ = false;
+  return down;
 }
 
 void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
@@ -676,11 +733,13 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
         hipStream_t down = head_on_slots_ ? computes_[static_cast<size_t>((k + 2) % slots())].get() : d2h_.get();
         h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
         h2d_wait_.wait_on(up);
-        e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down);
+        hipStream_t done = e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down);
         head_up_.record(up);  // every chunk upload issued first: all of them done
         last_upload_ = &head_up_;
-        ev_head_.record(down);
-        ev_head_.wait_on(e.compute_stream());
+        if (done != e.compute_stream()) {
+          ev_head_.record(done);
+          ev_head_.wait_on(e.compute_stream());
+        }
         idle_ = false;
         used_[k] = true;
         ++count_;
@@ -711,8 +770,8 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
     // stream, one event pair per chunk (exchange-free images only).
     const StreamPlan sp = e.stream_plan(reps, in_r0, in_r1);
     if (!sp.chunks.empty()) {
-      e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, h2d_.get(), d2h_.get());
-      ev_free_[k].record(d2h_.get());
+      hipStream_t done = e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, h2d_.get(), d2h_.get());
+      ev_free_[k].record(done);
       used_[k] = true;
       ++count_;
       return;

@@ -51,6 +51,22 @@ def preload_is_exchange_free(height: int, world: int, reps: int) -> bool:
     return world <= 1 or int(reps) <= height // world
 
 
+def pcie_bytes_per_image(width: int, height: int, channels: str, world: int, rank: int, halo: int,
+                         preload: bool) -> tuple:
+    """(H2D, D2H) bytes one rank moves per image: its band plus, when the
+    ghost rows are pre-loaded, `halo` rows per side clipped at the image
+    edges in; its owned rows out.  The bench JSON reports them per rank
+    (h2d_bytes_per_step / d2h_bytes_per_step): at N = 8 pre-loading 40 ghost
+    rows per side makes an interior rank's H2D 25 % larger than its band."""
+    rb = int(width) * {"grey": 1, "rgb": 3, "rgba": 4}[channels]
+    base, rem = divmod(int(height), int(world))
+    rows = base + (1 if rank < rem else 0)
+    y0 = rank * base + min(rank, rem)
+    above = min(int(halo), y0) if preload and world > 1 else 0
+    below = min(int(halo), int(height) - (y0 + rows)) if preload and world > 1 else 0
+    return (rows + above + below) * rb, rows * rb
+
+
 class DistributedBlur:
     def __init__(self, width: int, height: int, channels: str = "grey", filter="gaussian",
                  reps: Optional[int] = None, *, rank: Optional[int] = None, world: Optional[int] = None,
@@ -60,7 +76,7 @@ class DistributedBlur:
                  step_graphs: Optional[bool] = None, graph_capture: bool = True, slot_exchange: bool = False,
                  self_neighbours: bool = False, slot_comm: bool = False, stream_chunks: int = 0,
                  ipc_timeout_s: float = 30.0, ipc_pull: str = "grid", stagger: bool = True,
-                 cu_mask_queues: bool = True, head_on_slot_streams: bool = True):
+                 cu_mask_queues: bool = True, head_on_slot_streams: bool = True, stream_sync: int = 0):
         """Pipeline policy (native EngineOptions, echoed by bench.py's JSON
         config): `stagger` starts the first images of a burst one upload after
         another; `cu_mask_queues` puts every slot stream on its own hardware
@@ -84,7 +100,8 @@ class DistributedBlur:
         # and D2H of ONE image overlap; schedule.hpp plan_streamed)
         kw = dict(halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant, slots=int(slots),
                   concurrent=int(concurrent), stream_chunks=int(stream_chunks), stagger=bool(stagger),
-                  cu_mask_queues=bool(cu_mask_queues), head_on_slot_streams=bool(head_on_slot_streams))
+                  cu_mask_queues=bool(cu_mask_queues), head_on_slot_streams=bool(head_on_slot_streams),
+                  stream_sync=int(stream_sync))
         if self_neighbours:
             # One-GPU emulation of rank `rank` of a `world`-way split whose halos
             # really move: its neighbours are replaced by itself (a 1-rank

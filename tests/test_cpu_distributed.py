@@ -2,6 +2,7 @@
 schedule with real point-to-point halo messages — CPU stand-in for RCCL."""
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -235,3 +236,47 @@ def test_import_leaves_omp_wait_policy_unset():
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip() == "None"
+
+
+def test_pcie_bytes_per_rank(pconv_mod):
+    """h2d_bytes_per_step / d2h_bytes_per_step of the bench lines: band plus
+    pre-loaded ghost rows in (clipped at the image edges), owned rows out;
+    the 8-way headline's interior ranks upload 25 % more than their band."""
+    from pconv.parallel.dist_engine import pcie_bytes_per_image
+
+    n = pconv_mod.native
+    rb = 1920 * 3
+    tot_in = tot_out = 0
+    for r in range(8):
+        b = n.row_band(2520, 8, r)
+        h2d, d2h = pcie_bytes_per_image(1920, 2520, "rgb", 8, r, 40, True)
+        above, below = min(40, b.y0), min(40, 2520 - b.y0 - b.rows)
+        assert (h2d, d2h) == ((b.rows + above + below) * rb, b.rows * rb)
+        tot_in, tot_out = tot_in + h2d, tot_out + d2h
+        assert pcie_bytes_per_image(1920, 2520, "rgb", 8, r, 40, False) == (b.rows * rb, b.rows * rb)
+    assert tot_out == 2520 * rb
+    assert pcie_bytes_per_image(1920, 2520, "rgb", 8, 3, 40, True)[0] == 395 * rb  # 315 + 2 x 40
+    assert pcie_bytes_per_image(1920, 2520, "rgb", 1, 0, 40, True) == (2520 * rb, 2520 * rb)
+
+
+def test_bench_policy_flags():
+    """Pipeline policy is bench flags (echoed in the JSON config), not env vars."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_flags", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    old = sys.argv
+    try:
+        sys.argv = ["bench.py"]
+        a = bench.parse()
+        assert (a.stagger, a.cu_mask_queues, a.head_on_slot_streams, a.ipc_pull, a.numa_bind) == \
+            (True, True, True, "grid", "on")
+        sys.argv = ["bench.py", "--no-stagger", "--pool-queues", "--head-pool-streams", "--ipc-pull", "sdma",
+                    "--numa-bind", "off"]
+        a = bench.parse()
+    finally:
+        sys.argv = old
+    kw = bench.policy_kwargs(a)
+    assert kw == dict(stagger=False, cu_mask_queues=False, head_on_slot_streams=False, ipc_pull="sdma", stream_sync=0)
+    assert bench.mode_kwargs(a, "ipc", 8)["ipc_pull"] == "sdma"

@@ -70,7 +70,7 @@ def test_multiprocess_bands_one_gpu(pconv_mod, world, halo, fuse, preload, slots
     assert all(r[3] >= 1 for r in res)
 
 
-@pytest.mark.parametrize("world,extra", [(2, []), (3, ["--halo-mode", "exchange"]), (4, []),
+@pytest.mark.parametrize("world,extra", [(2, []), (3, ["--halo-mode", "exchange"]), (4, []), (8, []),
                                          (2, ["--slots", "1", "--no-overlap", "--halo-mode", "exchange"]),
                                          (2, ["--halo-select", "exchange"]), (3, ["--halo-select", "overlap"]),
                                          (2, ["--halo-select", "event"])])
@@ -95,12 +95,20 @@ def test_bench_torchrun_rehearsal(world, extra):
     assert meta["n_gpus"] == world and meta["mismatches"] == 0
     assert meta["value"] > 0 and meta["config"]["parallelism"] == f"rowband{world}"
     assert meta["runtime"]["hip_runtime_version"] > 0 and meta["runtime"]["hip_runtime_path"]
+    assert len(meta["per_rank_ms_per_step"]) == world
+    # PCIe bytes per rank: band (+ pre-loaded ghost rows) in, owned rows out; the bands tile the image
+    assert len(meta["h2d_bytes_per_step"]) == world and len(meta["d2h_bytes_per_step"]) == world
+    assert sum(meta["d2h_bytes_per_step"]) == 1920 * 2520 * 3
+    assert all(i >= o for i, o in zip(meta["h2d_bytes_per_step"], meta["d2h_bytes_per_step"]))
+    assert meta["config"]["ipc_pull"] == "grid" and meta["config"]["stagger"] is True
     modes = meta["halo_modes"]
     head = "event" if "--halo-mode" in extra else "preload"
     assert set(modes) == {head, "slot_exchange", "slot_exchange_direct", "event", "overlap", "ipc"}, modes
     for m, r in modes.items():
         assert r["status"] == "ok", (m, r)
         assert r["ms_per_step"] > 0
+        if m != head:
+            assert len(r["per_rank_ms_per_step"]) == world and len(r["h2d_bytes_per_step"]) == world, (m, r)
         assert r["mismatches"] == 0, (m, r)  # every mode against the oracle, not only the headline's bytes
         if m != head:
             assert r["mismatches_vs_headline"] == 0 and r["exchanges_per_step"] >= 1, (m, r)

@@ -26,6 +26,7 @@ PY
 }
 for i in a b c; do one bench_$i --gpus 1 --steps 20 --warmup 5 || exit 1; done
 for i in a b c; do one nostag_$i --gpus 1 --steps 20 --warmup 5 --no-stagger || exit 1; done
+for m in 1 2; do for i in a b c; do one sync${m}_$i --gpus 1 --steps 20 --warmup 5 --stream-sync $m || exit 1; done; done
 one s200 --steps 200 --warmup 5 || exit 1
 one e8 --emulate 8:3 --steps 300 --warmup 10 || exit 1
 for p in grid single sdma; do one e8_ipc_$p --emulate 8:3 --emulate-halo ipc --ipc-pull $p --steps 300 --warmup 10 || exit 1; done
