@@ -54,7 +54,42 @@
 namespace pconv {
 namespace {
 
-template <int CH, int LW, int M, int NW, bool ALT>
+// The `steps` repetitions of a tile in one of three step forms (the tuner
+// times all three per launch geometry):
+//   0: one swar_step per repetition, truncating every step;
+//   1: steps in pairs keeping 16 x the truncated value in between (one AND
+//      instead of shift + AND every other step), one barrier per step;
+//   2: as 1 with ONE barrier per pair (swar_step2: two boundary rows per
+//      side exchanged, one ghost row per side recomputed).
+// Forms 1 and 2 cost registers (up to +40 VGPRs on grey tiles).  g_row /
+// height: global row of the wave's register row 0 and the image height
+// (form 2's ghost rows outside the image read as zero).
+template <int CH, int NP, int M, int NW, int FORM, int R>
+__device__ __forceinline__ void run_steps(u32 (&D)[M][NP], uint4 (&lds)[2][NW][R][NP / 4][64], int steps, int w,
+                                          int lane, bool needs_mask, const u32 (&cm)[NP], int out_top, int out_bot,
+                                          int g_row, int height) {
+  if constexpr (FORM == 2) {
+    static_assert(R == 4, "form 2 exchanges two boundary rows per side");
+    const bool ga_out = g_row - 1 < 0 || g_row - 1 >= height;
+    const bool gb_out = g_row + M < 0 || g_row + M >= height;
+    int s = 0;
+    for (; s + 2 <= steps; s += 2)
+      swar_step2<CH, NP, M, NW>(D, lds, (s >> 1) & 1, w, lane, needs_mask, cm, out_top, out_bot, ga_out, gb_out);
+    if (s < steps) swar_step<CH, NP, M, NW, 0, R>(D, lds, (s >> 1) & 1, w, lane, needs_mask, cm, out_top, out_bot);
+  } else if constexpr (FORM == 1) {
+    int s = 0;
+    for (; s + 2 <= steps; s += 2) {
+      swar_step<CH, NP, M, NW, 1, R>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+      swar_step<CH, NP, M, NW, 2, R>(D, lds, 1, w, lane, needs_mask, cm, out_top, out_bot);
+    }
+    if (s < steps) swar_step<CH, NP, M, NW, 0, R>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+  } else {
+    for (int s = 0; s < steps; ++s)
+      swar_step<CH, NP, M, NW, 0, R>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
+  }
+}
+
+template <int CH, int LW, int M, int NW, int FORM>
 __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                   int64_t pitch, int64_t dst_pitch, int row_bytes, int r0, int r1,
                                                   int steps, int g_row0, int height, int nstrips, int pair_stride,
@@ -62,7 +97,8 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
   constexpr int NP = LW;       // pairs per row per lane
   constexpr int NQ = NP / 4;   // uint4 per row per lane
   using CT = typename Chunk<NP>::T;
-  __shared__ uint4 lds[2][NW][2][NQ][64];  // [parity][wave][top/bottom][quad][lane]
+  // [parity][wave][boundary rows: top, bottom (FORM 2: two each)][quad][lane]
+  __shared__ uint4 lds[2][NW][FORM == 2 ? 4 : 2][NQ][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hl = (steps * CH + LW - 1) / LW;  // halo lanes per side
@@ -109,20 +145,7 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
   const int out_top = min(max(-g_row0 - row_base, 0), M);
   const int out_bot = min(max(height - g_row0 - row_base, 0), M);
 
-  // ALT: steps in pairs keeping 16 x the truncated value in between (one AND
-  // instead of shift + AND every other step).  Two step bodies per iteration
-  // cost registers (up to +40 VGPRs on grey tiles), so both forms exist and
-  // the tuner picks per launch geometry.
-  if constexpr (ALT) {  // pairs of steps: scale-16 intermediate, one AND saved per pair
-    int s = 0;
-    for (; s + 2 <= steps; s += 2) {
-      swar_step<CH, NP, M, NW, 1>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
-      swar_step<CH, NP, M, NW, 2>(D, lds, 1, w, lane, needs_mask, cm, out_top, out_bot);
-    }
-    if (s < steps) swar_step<CH, NP, M, NW, 0>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
-  } else {
-    for (int s = 0; s < steps; ++s) swar_step<CH, NP, M, NW, 0>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
-  }
+  run_steps<CH, NP, M, NW, FORM>(D, lds, steps, w, lane, needs_mask, cm, out_top, out_bot, row_base + g_row0, height);
 
   const bool lane_in = lane >= hl && lane < 64 - hl;
   const bool stA = lane_in && validA > 0, stB = lane_in && validB > 0;
@@ -165,14 +188,14 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
 // in docs/PERFORMANCE.md).
 //   Contract (checked at launch): row_bytes % 4 == 0, source and destination
 // ranges under 2 GiB.
-template <int CH, int M, int NW, bool ALT>
+template <int CH, int M, int NW, int FORM>
 __global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                      int pitch, int dst_pitch, int row_bytes, int r0, int r1,
                                                      int steps, int g_row0, int height, int nstrips, int pair_stride,
                                                      int row_tiles, int xcd_swizzle) {
   constexpr int LW = 4, NP = 4, NQ = 1;
   constexpr u32 kOut = 0x80000000u;  // offset past every descriptor's range
-  __shared__ uint4 lds[2][NW][2][NQ][64];
+  __shared__ uint4 lds[2][NW][FORM == 2 ? 4 : 2][NQ][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hl = (steps * CH + LW - 1) / LW;
@@ -218,16 +241,7 @@ __global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__
     cm[k] = (xA >= 0 && xA + k < row_bytes ? 0xffffu : 0u) | (xB >= 0 && xB + k < row_bytes ? 0xffff0000u : 0u);
   const int out_top = min(max(-g_row0 - row_base, 0), M);
   const int out_bot = min(max(height - g_row0 - row_base, 0), M);
-  if constexpr (ALT) {
-    int s = 0;
-    for (; s + 2 <= steps; s += 2) {
-      swar_step<CH, NP, M, NW, 1>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
-      swar_step<CH, NP, M, NW, 2>(D, lds, 1, w, lane, needs_mask, cm, out_top, out_bot);
-    }
-    if (s < steps) swar_step<CH, NP, M, NW, 0>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
-  } else {
-    for (int s = 0; s < steps; ++s) swar_step<CH, NP, M, NW, 0>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
-  }
+  run_steps<CH, NP, M, NW, FORM>(D, lds, steps, w, lane, needs_mask, cm, out_top, out_bot, row_base + g_row0, height);
   const bool lane_in = lane >= hl && lane < 64 - hl;
   const int tile_r0 = row_base + steps - w * M;
   const int st_lo = max(tile_r0, r0), st_hi = min(tile_r0 + vrows, st_end);
@@ -259,16 +273,39 @@ std::atomic<int> g_xcd_swizzle{1};  // XCD-aware tile order (neutral +-2 %, kept
 
 bool xcd_swizzle_enabled() { return g_xcd_swizzle.load(std::memory_order_relaxed) != 0; }
 
-std::atomic<int> g_alt_mode{-1};  // -1 tune, 0 off, 1 on
+std::atomic<int> g_alt_mode{-1};  // step form: -1 tuned, else forced 0 / 1 / 2 (run_steps)
 
 int alt_mode() { return g_alt_mode.load(std::memory_order_relaxed); }
 
 // Step form when nothing was tuned (graph capture, autotune off): the paired
 // form is faster in most measured geometries.
-bool default_alt() { return alt_mode() != 0; }
+int default_form() { return alt_mode() >= 0 ? alt_mode() : 1; }
+
+// Form 2 needs three register rows per wave and four boundary rows per wave
+// in LDS (64 KB at most: NW x LW/4 <= 8); other shapes run form 1 instead.
+constexpr bool form2_ok(int lw, int m, int nw) { return m >= 3 && nw * (lw / 4) <= 8; }
+
+// Kernel of one step form.
+template <int CH, int LW, int M, int NW>
+auto swar_kernel(int form) {
+  using F = decltype(&k_swar<CH, LW, M, NW, 0>);
+  if constexpr (form2_ok(LW, M, NW)) {
+    if (form == 2) return static_cast<F>(&k_swar<CH, LW, M, NW, 2>);
+  }
+  return form >= 1 ? static_cast<F>(&k_swar<CH, LW, M, NW, 1>) : static_cast<F>(&k_swar<CH, LW, M, NW, 0>);
+}
+
+template <int CH, int M, int NW>
+auto swar_pf_kernel(int form) {
+  using F = decltype(&k_swar_pf<CH, M, NW, 0>);
+  if constexpr (form2_ok(4, M, NW)) {
+    if (form == 2) return static_cast<F>(&k_swar_pf<CH, M, NW, 2>);
+  }
+  return form >= 1 ? static_cast<F>(&k_swar_pf<CH, M, NW, 1>) : static_cast<F>(&k_swar_pf<CH, M, NW, 0>);
+}
 
 template <int CH, int LW, int M, int NW>
-void launch_one(const StencilLaunch& a, hipStream_t s, bool alt) {
+void launch_one(const StencilLaunch& a, hipStream_t s, int form) {
   const int steps = a.steps;
   const int hl = (steps * CH + LW - 1) / LW;
   const int vbytes = (64 - 2 * hl) * LW;
@@ -279,25 +316,17 @@ void launch_one(const StencilLaunch& a, hipStream_t s, bool alt) {
   const int row_tiles = ceil_div(static_cast<int>(a.r1 - a.r0), vrows);
   const dim3 grid(pair_stride * row_tiles);
   const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
-  if (alt)
-    k_swar<CH, LW, M, NW, true><<<grid, dim3(64 * NW), 0, s>>>(a.src, a.dst, a.pitch, a.dst_pitch ? a.dst_pitch : a.pitch,
-                                                       static_cast<int>(a.row_bytes),
-                                                       static_cast<int>(a.r0), static_cast<int>(a.r1), steps,
-                                                       static_cast<int>(a.g_row0), static_cast<int>(hmax), nstrips,
-                                                       pair_stride, row_tiles, xcd_swizzle_enabled() ? 1 : 0);
-  else
-    k_swar<CH, LW, M, NW, false><<<grid, dim3(64 * NW), 0, s>>>(a.src, a.dst, a.pitch, a.dst_pitch ? a.dst_pitch : a.pitch,
-                                                       static_cast<int>(a.row_bytes),
-                                                       static_cast<int>(a.r0), static_cast<int>(a.r1), steps,
-                                                       static_cast<int>(a.g_row0), static_cast<int>(hmax), nstrips,
-                                                       pair_stride, row_tiles, xcd_swizzle_enabled() ? 1 : 0);
+  swar_kernel<CH, LW, M, NW>(form)<<<grid, dim3(64 * NW), 0, s>>>(
+      a.src, a.dst, a.pitch, a.dst_pitch ? a.dst_pitch : a.pitch, static_cast<int>(a.row_bytes),
+      static_cast<int>(a.r0), static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), static_cast<int>(hmax), nstrips,
+      pair_stride, row_tiles, xcd_swizzle_enabled() ? 1 : 0);
 }
 
 template <int CH>
-void launch_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh, bool alt) {
+void launch_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh, int form) {
 #define PCONV_SWAR(LW_, M_, NW_)                            \
   if (sh.lw == LW_ && sh.m == M_ && sh.nw == NW_) {         \
-    launch_one<CH, LW_, M_, NW_>(a, s, alt);                \
+    launch_one<CH, LW_, M_, NW_>(a, s, form);               \
     return;                                                 \
   }
   PCONV_SWAR(8, 8, 8)
@@ -346,7 +375,7 @@ bool pf_launch_ok(const StencilLaunch& a, int steps) {
 }
 
 template <int CH, int M, int NW>
-void launch_pf_one(const StencilLaunch& a, hipStream_t s, bool alt) {
+void launch_pf_one(const StencilLaunch& a, hipStream_t s, int form) {
   const int steps = a.steps;
   const int hl = (steps * CH + 3) / 4;
   const int vbytes = (64 - 2 * hl) * 4;
@@ -362,14 +391,9 @@ void launch_pf_one(const StencilLaunch& a, hipStream_t s, bool alt) {
   const int xs = xcd_swizzle_enabled() ? 1 : 0;
   const int hmax = static_cast<int>(std::min<int64_t>(a.height, int64_t(1) << 30));
   const int dp = static_cast<int>(a.dst_pitch ? a.dst_pitch : a.pitch);
-  if (alt)
-    k_swar_pf<CH, M, NW, true><<<dim3(grid), dim3(64 * NW), 0, s>>>(
-        a.src, a.dst, static_cast<int>(a.pitch), dp, static_cast<int>(a.row_bytes), static_cast<int>(a.r0),
-        static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), hmax, nstrips, pair_stride, row_tiles, xs);
-  else
-    k_swar_pf<CH, M, NW, false><<<dim3(grid), dim3(64 * NW), 0, s>>>(
-        a.src, a.dst, static_cast<int>(a.pitch), dp, static_cast<int>(a.row_bytes), static_cast<int>(a.r0),
-        static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), hmax, nstrips, pair_stride, row_tiles, xs);
+  swar_pf_kernel<CH, M, NW>(form)<<<dim3(grid), dim3(64 * NW), 0, s>>>(
+      a.src, a.dst, static_cast<int>(a.pitch), dp, static_cast<int>(a.row_bytes), static_cast<int>(a.r0),
+      static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), hmax, nstrips, pair_stride, row_tiles, xs);
 }
 
 // Tiles of a launch and the workgroups the prefetch kernel keeps resident.
@@ -382,10 +406,10 @@ int64_t pf_tiles(SwarShape sh, int ch, int steps, int64_t rows, int64_t row_byte
 }
 
 template <int CH>
-void launch_pf_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh, bool alt) {
+void launch_pf_ch(const StencilLaunch& a, hipStream_t s, SwarShape sh, int form) {
 #define PCONV_PF(LW_, M_, NW_)                       \
   if (sh.lw == LW_ && sh.m == M_ && sh.nw == NW_) {  \
-    launch_pf_one<CH, M_, NW_>(a, s, alt);           \
+    launch_pf_one<CH, M_, NW_>(a, s, form);          \
     return;                                          \
   }
   PCONV_PF(4, 8, 8) PCONV_PF(4, 12, 4) PCONV_PF(4, 16, 4) PCONV_PF(4, 12, 8) PCONV_PF(4, 16, 8) PCONV_PF(4, 20, 8)
@@ -437,13 +461,12 @@ struct KernelRes {
 };
 
 template <int CH>
-KernelRes query_res(SwarShape sh, bool alt) {
+KernelRes query_res(SwarShape sh, int form) {
   hipFuncAttributes at{};
   hipError_t e = hipErrorInvalidValue;
 #define PCONV_SWAR(LW_, M_, NW_)                                                                     \
   if (sh.lw == LW_ && sh.m == M_ && sh.nw == NW_)                                                   \
-    e = hipFuncGetAttributes(&at, alt ? reinterpret_cast<const void*>(&k_swar<CH, LW_, M_, NW_, true>)   \
-                                      : reinterpret_cast<const void*>(&k_swar<CH, LW_, M_, NW_, false>));
+    e = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(swar_kernel<CH, LW_, M_, NW_>(form)));
   PCONV_SWAR(8, 8, 8)
   PCONV_SWAR(8, 8, 4)
   PCONV_SWAR(8, 16, 4)
@@ -477,14 +500,14 @@ KernelRes query_res(SwarShape sh, bool alt) {
   return r;
 }
 
-KernelRes kernel_res(SwarShape sh, int ch, bool alt) {
+KernelRes kernel_res(SwarShape sh, int ch, int form) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, int, int, bool>, KernelRes> cache;
+  static std::map<std::tuple<int, int, int, int, int>, KernelRes> cache;
   std::lock_guard<std::mutex> lk(mu);
-  const auto key = std::make_tuple(ch, sh.lw, sh.m, sh.nw, alt);
+  const auto key = std::make_tuple(ch, sh.lw, sh.m, sh.nw, form);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  const KernelRes r = ch == 1 ? query_res<1>(sh, alt) : ch == 3 ? query_res<3>(sh, alt) : query_res<4>(sh, alt);
+  const KernelRes r = ch == 1 ? query_res<1>(sh, form) : ch == 3 ? query_res<3>(sh, form) : query_res<4>(sh, form);
   if (r.measured) cache.emplace(key, r);  // estimates (no device) are not cached
   return r;
 }
@@ -507,12 +530,12 @@ KernelRes kernel_res(SwarShape sh, int ch, bool alt) {
 // tools/fit_swar_data.py + tools/fit_swar_model.py); they pick the measured
 // best shape in 6 of 6 configurations of the current kernel.
 void set_xcd_swizzle(bool on) { g_xcd_swizzle.store(on ? 1 : 0, std::memory_order_relaxed); }
-void set_swar_alt(int mode) { g_alt_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
+void set_swar_alt(int mode) { g_alt_mode.store(mode < 0 ? -1 : std::min(mode, 2), std::memory_order_relaxed); }
 void set_prefetch_mode(int mode) { g_pf_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
 std::vector<SwarShape> swar_prefetch_shapes() { return std::vector<SwarShape>(std::begin(kPfShapes), std::end(kPfShapes)); }
 
 SwarResources swar_resources(SwarShape s, int ch) {
-  const KernelRes r = kernel_res(s, ch, default_alt());
+  const KernelRes r = kernel_res(s, ch, default_form());
   return SwarResources{r.vgpr, r.lds, r.measured};
 }
 
@@ -526,7 +549,7 @@ double swar_launch_cycles(SwarShape s, int steps, int ch, int64_t rows, int64_t 
   const int vrows = s.m * s.nw - 2 * steps;
   if (vrows <= 0 || np < ch) return 1e300;
   const double g = static_cast<double>(pairs * ceil_div<int64_t>(rows, vrows));
-  const KernelRes res = kernel_res(s, ch, default_alt());
+  const KernelRes res = kernel_res(s, ch, default_form());
   const int vgpr_waves = std::max(1, std::min(8, 512 / round_up(std::max(res.vgpr, 1), 8)));
   const int lds_wgs = res.lds > 0 ? (160 * 1024) / res.lds : 8;
   const int L = std::max(1, std::min({lds_wgs, vgpr_waves * 4 / s.nw, 32 / s.nw}));
@@ -564,23 +587,23 @@ namespace {
 
 struct SwarChoice {
   SwarShape shape;
-  bool alt = true;
+  int form = 1;  // step form of run_steps
   bool pf = false;  // buffer-op tile kernel (k_swar_pf)
 };
 
 void launch_choice(const StencilLaunch& a, Channels ch, hipStream_t stream, SwarChoice c) {
   if (c.pf) {
     switch (ch) {
-      case Channels::Grey: launch_pf_ch<1>(a, stream, c.shape, c.alt); break;
-      case Channels::Rgb: launch_pf_ch<3>(a, stream, c.shape, c.alt); break;
-      case Channels::Rgba: launch_pf_ch<4>(a, stream, c.shape, c.alt); break;
+      case Channels::Grey: launch_pf_ch<1>(a, stream, c.shape, c.form); break;
+      case Channels::Rgb: launch_pf_ch<3>(a, stream, c.shape, c.form); break;
+      case Channels::Rgba: launch_pf_ch<4>(a, stream, c.shape, c.form); break;
     }
     return;
   }
   switch (ch) {
-    case Channels::Grey: launch_ch<1>(a, stream, c.shape, c.alt); break;
-    case Channels::Rgb: launch_ch<3>(a, stream, c.shape, c.alt); break;
-    case Channels::Rgba: launch_ch<4>(a, stream, c.shape, c.alt); break;
+    case Channels::Grey: launch_ch<1>(a, stream, c.shape, c.form); break;
+    case Channels::Rgb: launch_ch<3>(a, stream, c.shape, c.form); break;
+    case Channels::Rgba: launch_ch<4>(a, stream, c.shape, c.form); break;
   }
 }
 
@@ -616,7 +639,7 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   const int64_t rows = a.r1 - a.r0;
   const int mode = alt_mode();
   SwarChoice fallback;
-  fallback.alt = default_alt();
+  fallback.form = default_form();
   if (pf_mode() == 1 && pf_launch_ok(a, a.steps) && (override_shape(fallback.shape) || !autotune_enabled())) {
     // forced prefetch kernel, untuned: the overridden shape if it has a
     // prefetch instantiation, else the first prefetch shape that runs
@@ -646,7 +669,7 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
     auto it = g_tuned.find(key);
     if (it != g_tuned.end()) {
       SwarChoice r = it->second;
-      if (mode >= 0) r.alt = mode == 1;  // forced form (the shape stays tuned)
+      if (mode >= 0) r.form = mode;  // forced form (the shape stays tuned)
       return r;
     }
   }
@@ -664,8 +687,9 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   if (ranked.size() > keep) ranked.resize(keep);
   std::vector<SwarChoice> cands;
   for (const auto& r : ranked)
-    for (int alt = 0; alt <= 1; ++alt)
-      if (mode < 0 || mode == alt) cands.push_back(SwarChoice{r.second, alt == 1, false});
+    for (int form = 0; form <= 2; ++form)
+      if ((mode < 0 || mode == form) && (form < 2 || form2_ok(r.second.lw, r.second.m, r.second.nw)))
+        cands.push_back(SwarChoice{r.second, form, false});
   // Buffer-op tile kernel (k_swar_pf, one workgroup per tile) for the
   // model's candidate shapes it instantiates: hardware zero-fill of rows and
   // lanes outside the frame instead of branches (measured 2-6 % faster on RGB
@@ -674,8 +698,9 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
     std::vector<SwarChoice> pfs;
     for (const auto& r : ranked)
       if (known_pf_shape(r.second))
-        for (int alt = 0; alt <= 1; ++alt)
-          if (mode < 0 || mode == alt) pfs.push_back(SwarChoice{r.second, alt == 1, true});
+        for (int form = 0; form <= 2; ++form)
+          if ((mode < 0 || mode == form) && (form < 2 || form2_ok(4, r.second.m, r.second.nw)))
+            pfs.push_back(SwarChoice{r.second, form, true});
     if (pf_mode() == 1 && !pfs.empty()) cands.clear();  // forced: only these candidates
     cands.insert(cands.end(), pfs.begin(), pfs.end());
   }
@@ -728,7 +753,7 @@ std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned() {
   std::lock_guard<std::mutex> lk(g_tune_mu);
   std::vector<std::pair<std::vector<int64_t>, SwarShape>> out;
   for (const auto& kv : g_tuned)
-    out.push_back({{kv.first.ch, kv.first.steps, kv.first.rows, kv.first.row_bytes, kv.second.alt ? 1 : 0,
+    out.push_back({{kv.first.ch, kv.first.steps, kv.first.rows, kv.first.row_bytes, kv.second.form,
                     kv.second.pf ? 1 : 0},
                    kv.second.shape});
   return out;

@@ -31,7 +31,7 @@ void set_autotune(bool on);
 // How many of the model's best shapes the tuner times (default 6).
 void set_tune_candidates(int n);
 void clear_swar_tuning();
-// Tuned entries: ({channels, steps, rows, row_bytes, paired_form, prefetch}, shape); prefetch = 1: the
+// Tuned entries: ({channels, steps, rows, row_bytes, step_form, prefetch}, shape); prefetch = 1: the
 // buffer-op tile kernel k_swar_pf won.
 std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned();
 
@@ -49,7 +49,8 @@ SwarResources swar_resources(SwarShape s, int ch);
 // XCD-aware tile order of the SWAR kernels (default on).
 void set_xcd_swizzle(bool on);
 // Step form: -1 tuned per launch geometry (default), 0 truncate every step,
-// 1 steps in pairs with a scale-16 intermediate.
+// 1 steps in pairs with a scale-16 intermediate, 2 as 1 with one barrier per
+// pair (two boundary rows exchanged per side, swar_step2).
 void set_swar_alt(int mode);
 // Buffer-op tile kernel (k_swar_pf): -1 among the tuned candidates
 // (default), 0 never, 1 forced; with the mode forced, a shape set by

@@ -208,11 +208,14 @@ def test_temporal_equals_repeated_single_steps(pconv_mod, rng):
         assert np.array_equal(got, pconv_mod.numpy_convolve(img, t)), t
 
 
-@pytest.mark.parametrize("form", [0, 1])
+@pytest.mark.parametrize("form", [0, 1, 2])
 def test_every_swar_shape_bit_exact(native, rng, form):
     """Force each instantiated SWAR tile shape (lane width, rows/wave, waves)
     in each step form (0: truncate every step, 1: pairs of steps with a x16
-    intermediate) and compare a fused launch with the CPU fused reference."""
+    intermediate, 2: as 1 with one barrier per pair — two boundary rows per
+    side, ghost rows recomputed; shapes without form 2 run form 1) and
+    compare a fused launch with the CPU fused reference: odd and even step
+    counts, a band whose ghost rows reach the image top."""
     try:
         native.set_swar_alt(form)
         for (lw, m, nw) in native.swar_shapes():
@@ -232,7 +235,7 @@ def test_every_swar_shape_bit_exact(native, rng, form):
 
 
 @pytest.mark.parametrize("swizzle", [True, False])
-@pytest.mark.parametrize("form", [0, 1])
+@pytest.mark.parametrize("form", [0, 1, 2])
 def test_prefetch_kernel_every_shape_bit_exact(native, rng, form, swizzle):
     """The buffer-op tile kernel (k_swar_pf), forced in each shape and step
     form, with and without the XCD-aware tile order: whole images and band

@@ -30,3 +30,15 @@ for m in 1 2; do for i in a b c; do one sync${m}_$i --gpus 1 --steps 20 --warmup
 one s200 --steps 200 --warmup 5 || exit 1
 one e8 --emulate 8:3 --steps 300 --warmup 10 || exit 1
 for p in grid single sdma; do one e8_ipc_$p --emulate 8:3 --emulate-halo ipc --ipc-pull $p --steps 300 --warmup 10 || exit 1; done
+OUT0=$OUT
+bash tools/r05/teardown.sh > $OUT0/teardown.txt 2>&1 || { echo "teardown probe failed"; tail -5 $OUT0/teardown.txt; exit 1; }
+python3 - <<'PY'
+import json, collections
+rows = [json.loads(l) for l in open("gpurun_out/r05/teardown/next.jsonl")]
+by = collections.defaultdict(list)
+for r in rows:
+    by[r["prev"]].append(r["next"]["hip_init_ms"])
+for k, v in by.items():
+    v.sort()
+    print(f"prev={k:9s} next hip_init ms median {v[len(v)//2]:7.1f} all {v}")
+PY
