@@ -118,6 +118,13 @@ class BandEngine {
   static constexpr size_t kMaxCachedGraphs = 64;
   size_t cached_graphs() const { return graphs_.size() + step_graphs_.size(); }
   size_t cached_step_graphs() const { return step_graphs_.size(); }
+  // Event-record nodes over the cached step graphs (tests: the upload event
+  // of the burst stagger is a real node, recorded by every replay).
+  int step_graph_event_nodes() const {
+    int n = 0;
+    for (const auto& kv : step_graphs_) n += kv.second.event_nodes;
+    return n;
+  }
   hipStream_t compute_stream() const { return cs_; }
   hipStream_t comm_stream() const { return ms_; }
 
@@ -242,6 +249,7 @@ class BandEngine {
     int end_cur = 0;
     int launches = 0;
     int exchanges = 0;
+    int event_nodes = 0;  // event-record nodes of the captured graph (the stagger's upload event)
   };
   // (reps, start buffer, in, in_r0, in_r1, out) -> whole-step graph.  Keyed
   // on host pointers, so both caches are bounded: past kMaxCachedGraphs

@@ -512,10 +512,23 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     prepare(ph);  // tile-shape tuning cannot run inside the capture
     PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
     upload_rows(host_in, rb, in_r0, in_r1, cs_);
-    // The upload-done event as an EXTERNAL event-record node: a plain
-    // hipEventRecord inside a capture only orders nodes of this graph, and
-    // replays of the instantiated graph would never record the event.
-    if (opt_.upload_event) PCONV_HIP_CHECK(hipEventRecordWithFlags(ev_uploaded_.get(), cs_, hipEventRecordExternal));
+    // The upload-done event as a real event-record NODE hanging off the
+    // upload: a plain hipEventRecord inside a capture only orders nodes of
+    // this graph, so replays of the instantiated graph would never record
+    // the event (hipEventRecordWithFlags(..., hipEventRecordExternal) is
+    // refused by torch's HIP 7.0 runtime).  The node is added to the graph
+    // being captured with the upload as its only dependency and is left out
+    // of the stream's capture dependencies: nothing waits on it.
+    if (opt_.upload_event) {
+      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+      hipGraph_t cg = nullptr;
+      const hipGraphNode_t* deps = nullptr;
+      size_t ndeps = 0;
+      PCONV_HIP_CHECK(hipStreamGetCaptureInfo_v2(cs_, &st, nullptr, &cg, &deps, &ndeps));
+      PCONV_CHECK(st == hipStreamCaptureStatusActive && cg != nullptr, "step graph: capture not active");
+      hipGraphNode_t ev_node = nullptr;
+      PCONV_HIP_CHECK(hipGraphAddEventRecordNode(&ev_node, cg, deps, ndeps, ev_uploaded_.get()));
+    }
     if (zone_first) {
       transport_->exchange(*this, lay_.halo, cs_);  // stream order: after the upload, before the launches
       ++stats_.exchanges;
@@ -524,6 +537,17 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     if (host_out) download_rows(host_out, rb, 0, band_.rows, cs_);  // nullptr: the caller downloads itself
     PCONV_HIP_CHECK(hipStreamEndCapture(cs_, &g));
     StepGraph sg;
+    {
+      size_t nn = 0;
+      PCONV_HIP_CHECK(hipGraphGetNodes(g, nullptr, &nn));
+      std::vector<hipGraphNode_t> nodes(nn);
+      if (nn) PCONV_HIP_CHECK(hipGraphGetNodes(g, nodes.data(), &nn));
+      for (size_t i = 0; i < nn; ++i) {
+        hipGraphNodeType t{};
+        PCONV_HIP_CHECK(hipGraphNodeGetType(nodes[i], &t));
+        sg.event_nodes += t == hipGraphNodeTypeEventRecord ? 1 : 0;
+      }
+    }
     PCONV_HIP_CHECK(hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0));
     PCONV_HIP_CHECK(hipGraphDestroy(g));
     sg.end_cur = cur_;

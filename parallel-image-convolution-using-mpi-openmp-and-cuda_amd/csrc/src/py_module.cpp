@@ -456,6 +456,7 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_property_readonly("fuse", [](const BandEngine& e) { return e.options().fuse; })
       .def_property_readonly("cached_graphs", &BandEngine::cached_graphs)
       .def_property_readonly("cached_step_graphs", &BandEngine::cached_step_graphs)
+      .def_property_readonly("step_graph_event_nodes", &BandEngine::step_graph_event_nodes)
       .def_property_readonly_static("max_cached_graphs", [](py::object) { return BandEngine::kMaxCachedGraphs; })
       .def_property_readonly("pitch", [](const BandEngine& e) { return e.layout().pitch; })
       .def_property_readonly("row_bytes", [](const BandEngine& e) { return e.layout().row_bytes; })
