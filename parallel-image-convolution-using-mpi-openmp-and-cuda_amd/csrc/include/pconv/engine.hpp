@@ -218,8 +218,8 @@ class BandEngine {
  private:
   friend class LocalCluster;
   void enqueue_phase(const Phase& p);
-  void launch(const LaunchSpec& l, hipStream_t s, uint8_t* dst = nullptr, int64_t dst_pitch = 0);
-  StencilLaunch make_launch(const LaunchSpec& l, int cur, uint8_t* dst, int64_t dst_pitch) const;
+  void launch(const LaunchSpec& l, hipStream_t s);
+  StencilLaunch make_launch(const LaunchSpec& l, int cur) const;
   // Settle per-launch choices (tile-shape tuning) of a plan before capturing it.
   void prepare(const std::vector<Phase>& ph);
 

@@ -38,10 +38,6 @@ struct StencilLaunch {
   int steps = 1;                 // fused repetitions (temporal blocking) in this launch
   int64_t g_row0 = 0;            // global image row of frame row 0
   int64_t height = 0;            // global image height (rows outside are zero each step)
-  // Row pitch of `dst` (0 = `pitch`).  A different pitch lets the final
-  // launch of an image store straight into pinned host memory (zero-copy
-  // D2H fused into the producing kernel); SWAR temporal kernel only.
-  int64_t dst_pitch = 0;
 };
 
 enum class KernelVariant : int {

@@ -292,8 +292,7 @@ void prepare_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hi
   a.r0 = std::max(a.r0, -a.g_row0);
   a.r1 = std::min(a.r1, a.height - a.g_row0);
   if (a.r1 <= a.r0) return;
-  const bool own_dst_pitch = a.dst_pitch != 0 && a.dst_pitch != a.pitch;
-  if (v == KernelVariant::Auto && f.binomial121 && (a.steps > 1 || own_dst_pitch)) v = KernelVariant::Temporal;
+  if (v == KernelVariant::Auto && f.binomial121 && a.steps > 1) v = KernelVariant::Temporal;
   if (v == KernelVariant::Auto && !f.binomial121 && a.steps > 1) v = KernelVariant::FloatTemporal;
   if (v == KernelVariant::Temporal && f.binomial121 && a.steps <= kMaxFusedSteps) prepare_swar(a, ch, stream);
   if (v == KernelVariant::FloatTemporal && a.steps <= kMaxFusedSteps) prepare_float_temporal(f, ch, a, stream);
@@ -316,9 +315,8 @@ void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hip
               "launch_stencil: pitch too small for 16-byte vector access");
   PCONV_CHECK(a.row_bytes < (int64_t(1) << 31) && a.r1 - a.frame_lo < (int64_t(1) << 31),
               "launch_stencil: geometry exceeds 32-bit kernel indices");
-  const bool own_dst_pitch = a.dst_pitch != 0 && a.dst_pitch != a.pitch;
   if (v == KernelVariant::Auto)
-    v = f.binomial121 ? (a.steps > 1 || own_dst_pitch ? KernelVariant::Temporal : KernelVariant::Binomial)
+    v = f.binomial121 ? (a.steps > 1 ? KernelVariant::Temporal : KernelVariant::Binomial)
                       : (a.steps > 1 ? KernelVariant::FloatTemporal
                                      : (f.int_exact ? KernelVariant::Int9 : KernelVariant::Float9));
   if (v == KernelVariant::FloatTemporal) {
@@ -326,8 +324,6 @@ void launch_stencil(const Filter& f, Channels ch, const StencilLaunch& a_in, hip
     PCONV_HIP_CHECK(hipGetLastError());
     return;
   }
-  PCONV_CHECK(!own_dst_pitch || (v == KernelVariant::Temporal && a.dst_pitch >= a.row_bytes && a.dst_pitch % 4 == 0),
-              "launch_stencil: a separate destination pitch needs the SWAR temporal kernel");
   PCONV_CHECK(a.steps == 1 || v == KernelVariant::Temporal,
               "launch_stencil: fused steps not supported by kernel '" + std::string(kernel_variant_name(v)) + "'");
   if (v == KernelVariant::Temporal) {

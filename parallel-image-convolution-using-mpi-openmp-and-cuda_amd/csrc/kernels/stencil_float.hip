@@ -392,7 +392,6 @@ namespace {
 
 void float_temporal(const Filter& f, Channels ch, const StencilLaunch& a, hipStream_t stream, bool launch) {
   PCONV_CHECK(a.steps >= 1 && a.steps <= kMaxFusedSteps, "float temporal kernel: steps out of range");
-  PCONV_CHECK(a.dst_pitch == 0 || a.dst_pitch == a.pitch, "float temporal kernel: no separate destination pitch");
   PCONV_CHECK(a.height < (int64_t(1) << 30) && a.g_row0 < (int64_t(1) << 30), "float temporal kernel: rows exceed 2^30");
   PCONV_CHECK(a.row_bytes > 0 && a.row_bytes < (int64_t(1) << 30), "float temporal kernel: row bytes out of range");
   switch (ch) {

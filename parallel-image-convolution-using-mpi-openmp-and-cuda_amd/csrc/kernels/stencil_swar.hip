@@ -317,7 +317,7 @@ void launch_one(const StencilLaunch& a, hipStream_t s, int form) {
   const dim3 grid(pair_stride * row_tiles);
   const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
   swar_kernel<CH, LW, M, NW>(form)<<<grid, dim3(64 * NW), 0, s>>>(
-      a.src, a.dst, a.pitch, a.dst_pitch ? a.dst_pitch : a.pitch, static_cast<int>(a.row_bytes),
+      a.src, a.dst, a.pitch, a.pitch, static_cast<int>(a.row_bytes),
       static_cast<int>(a.r0), static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), static_cast<int>(hmax), nstrips,
       pair_stride, row_tiles, xcd_swizzle_enabled() ? 1 : 0);
 }
@@ -370,7 +370,7 @@ int pf_mode() { return g_pf_mode.load(std::memory_order_relaxed); }
 // Launches the prefetch kernel can take: 4-byte lanes, whole dwords per row,
 // source and destination ranges under 2 GiB (32-bit buffer offsets).
 bool pf_launch_ok(const StencilLaunch& a, int steps) {
-  const int64_t src_rows = (a.r1 + steps) - (a.r0 - steps), dp = a.dst_pitch ? a.dst_pitch : a.pitch;
+  const int64_t src_rows = (a.r1 + steps) - (a.r0 - steps), dp = a.pitch;
   return a.row_bytes % 4 == 0 && src_rows * a.pitch < (int64_t(1) << 31) && (a.r1 - a.r0) * dp < (int64_t(1) << 31);
 }
 
@@ -390,7 +390,7 @@ void launch_pf_one(const StencilLaunch& a, hipStream_t s, int form) {
   const int grid = static_cast<int>(ntiles);
   const int xs = xcd_swizzle_enabled() ? 1 : 0;
   const int hmax = static_cast<int>(std::min<int64_t>(a.height, int64_t(1) << 30));
-  const int dp = static_cast<int>(a.dst_pitch ? a.dst_pitch : a.pitch);
+  const int dp = static_cast<int>(a.pitch);
   swar_pf_kernel<CH, M, NW>(form)<<<dim3(grid), dim3(64 * NW), 0, s>>>(
       a.src, a.dst, static_cast<int>(a.pitch), dp, static_cast<int>(a.row_bytes), static_cast<int>(a.r0),
       static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), hmax, nstrips, pair_stride, row_tiles, xs);

@@ -172,11 +172,10 @@ std::vector<Phase> BandEngine::plan(int reps) const {
   return plan_band(band_, reps, c);
 }
 
-StencilLaunch BandEngine::make_launch(const LaunchSpec& l, int cur, uint8_t* dst, int64_t dst_pitch) const {
+StencilLaunch BandEngine::make_launch(const LaunchSpec& l, int cur) const {
   StencilLaunch a;
   a.src = frame_[cur].data() + lay_.offset(0);
-  a.dst = dst ? dst : frame_[cur ^ 1].data() + lay_.offset(0);
-  a.dst_pitch = dst ? dst_pitch : 0;
+  a.dst = frame_[cur ^ 1].data() + lay_.offset(0);
   a.pitch = lay_.pitch;
   a.row_bytes = lay_.row_bytes;
   a.r0 = l.lo;
@@ -197,7 +196,7 @@ void BandEngine::prepare(const std::vector<Phase>& ph) {
   // depends only on (channels, steps, rows, row bytes), not on the frames.
   for (const auto& p : ph)
     for (const auto& l : p.launches)
-      prepare_stencil(filter_, geom_.channels, make_launch(l, cur_, nullptr, 0), cs_, opt_.variant);
+      prepare_stencil(filter_, geom_.channels, make_launch(l, cur_), cs_, opt_.variant);
 }
 
 bool BandEngine::input_preloaded(int64_t in_r0, int64_t in_r1) const {
@@ -215,20 +214,8 @@ bool BandEngine::input_preloaded(int64_t in_r0, int64_t in_r1) const {
   return true;
 }
 
-void BandEngine::launch(const LaunchSpec& l, hipStream_t s, uint8_t* dst, int64_t dst_pitch) {
-  StencilLaunch a;
-  a.src = src_frame();
-  a.dst = dst ? dst : dst_frame();
-  a.dst_pitch = dst ? dst_pitch : 0;
-  a.pitch = lay_.pitch;
-  a.row_bytes = lay_.row_bytes;
-  a.r0 = l.lo;
-  a.r1 = l.hi;
-  a.frame_lo = -lay_.halo;
-  a.frame_hi = lay_.rows + lay_.halo;
-  a.steps = l.steps;
-  a.g_row0 = band_.y0;
-  a.height = geom_.height;
+void BandEngine::launch(const LaunchSpec& l, hipStream_t s) {
+  const StencilLaunch a = make_launch(l, cur_);
   launch_stencil(filter_, geom_.channels, a, s, opt_.variant);
   ++stats_.launches;
 }
@@ -385,7 +372,7 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
   };
   auto launches = [&](const StreamChunk& ch) {
     for (size_t i = 0; i < ch.launches.size(); ++i) {
-      launch_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1, nullptr, 0),
+      launch_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1),
                      cs_, opt_.variant);
       ++stats_.launches;
     }
