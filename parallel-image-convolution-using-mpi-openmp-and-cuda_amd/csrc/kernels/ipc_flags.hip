@@ -203,7 +203,7 @@ void launch_ipc_exchange(IpcPull form, IpcFlags* f, uint32_t* arrive, int me, in
   for (const void* p : {static_cast<const void*>(dst_up), static_cast<const void*>(src_up),
                         static_cast<const void*>(dst_down), static_cast<const void*>(src_down)})
     PCONV_CHECK(reinterpret_cast<uintptr_t>(p) % 16 == 0, "ipc exchange: unaligned row pointer");
-  PCONV_CHECK(!src_up == !dst_up && !src_down == !dst_down, "ipc exchange: source without destination");
+  PCONV_CHECK((!src_up || dst_up) && (!src_down || dst_down), "ipc exchange: source without destination");
   auto* du = reinterpret_cast<uint4*>(dst_up);
   auto* dd = reinterpret_cast<uint4*>(dst_down);
   const auto* su = reinterpret_cast<const uint4*>(src_up);

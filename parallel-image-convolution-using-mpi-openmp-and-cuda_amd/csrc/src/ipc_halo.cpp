@@ -156,8 +156,8 @@ void IpcHaloTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream
   // pitch-aligned rows (pads included: zero in every frame).
   const uint8_t* src_up = up >= 0 ? peer_up_[par] + lay_up_.offset(lay_up_.rows - depth) - kPadLeft : nullptr;
   const uint8_t* src_down = down >= 0 ? peer_down_[par] + lay_down_.offset(0) - kPadLeft : nullptr;
-  uint8_t* dst_up = mine + L.offset(-depth) - kPadLeft;
-  uint8_t* dst_down = mine + L.offset(b.rows) - kPadLeft;
+  uint8_t* dst_up = up >= 0 ? mine + L.offset(-depth) - kPadLeft : nullptr;
+  uint8_t* dst_down = down >= 0 ? mine + L.offset(b.rows) - kPadLeft : nullptr;
   launch_ipc_exchange(pull_, dflags_, reinterpret_cast<uint32_t*>(arrive_.data()), me, up, down, timeout_ticks_,
                       dst_up, src_up, dst_down, src_down, static_cast<int64_t>(n), stream);
   ++enqueued_;

@@ -145,8 +145,8 @@ def test_cli_multi_rank_shm(pconv_mod, tmp_path, rng, transport, extra):
     exchanges at every phase with --exchange-halo / shallow halos."""
     img = rng.integers(0, 256, size=(77, 61, 3), dtype=np.uint8)
     pconv_mod.write_raw(str(tmp_path / "img.raw"), img)
-    r = subprocess.run([CONV_BIN, "img.raw", "61", "77", "13", "rgb", "--transport", transport, "--check", "--json"]
-                       + extra, cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    r = subprocess.run([CONV_BIN, "img.raw", "61", "77", "13", "rgb", "--transport", transport, "--check", "--json",
+                        "--timeout", "30"] + extra, cwd=tmp_path, capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, r.stderr
     meta = json.loads(r.stdout.strip().splitlines()[-1])
     assert meta["mismatches"] == 0
