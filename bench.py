@@ -144,16 +144,11 @@ def parse():
                    help="after timing (outside the timed region), compare every rank's newest image, and every halo "
                         "mode's at N>1, with the CPU oracle; 'mismatches' in the JSON line (default on)")
     p.add_argument("--no-check", dest="check", action="store_false", help="skip the oracle check (sweeps)")
-    p.add_argument("--no-stagger", dest="stagger", action="store_false", default=True,
-                   help="the first images of a burst upload all at once (default: one after another)")
     p.add_argument("--pool-queues", dest="cu_mask_queues", action="store_false", default=True,
                    help="slot streams from the runtime's queue pool (default: each on its own CU-masked hardware "
                         "queue, profiles/r04/slots_c/)")
     p.add_argument("--head-pool-streams", dest="head_on_slot_streams", action="store_false", default=True,
                    help="a streamed head image's copies on two pool streams (default: the next two slots' streams)")
-    p.add_argument("--stream-sync", type=int, choices=[0, 1, 2], default=0,
-                   help="streamed image's cross-stream order: 0 events, 1 downloads on the compute stream, 2 as 1 "
-                        "with signal-memory stream waits for the uploads")
     p.add_argument("--ipc-pull", choices=["grid", "single", "sdma"], default="grid",
                    help="halo mode ipc: how a rank pulls its neighbours' rows (grid: one dispatch of many "
                         "workgroups; single: one workgroup; sdma: flag kernels around SDMA peer copies)")
@@ -251,9 +246,8 @@ def mode_transport(mode: str, transport: str) -> str:
 
 def policy_kwargs(a) -> dict:
     """Pipeline policy flags -> DistributedBlur / native EngineOptions (echoed in the JSON config)."""
-    return dict(stagger=getattr(a, "stagger", True), cu_mask_queues=getattr(a, "cu_mask_queues", True),
+    return dict(cu_mask_queues=getattr(a, "cu_mask_queues", True),
                 head_on_slot_streams=getattr(a, "head_on_slot_streams", True),
-                stream_sync=getattr(a, "stream_sync", 0),
                 ipc_pull=getattr(a, "ipc_pull", "grid"))
 
 
@@ -414,11 +408,9 @@ def run_native(a) -> int:
         cmd.append("--check")
     if a.transport == "gloo-host":
         cmd += ["--transport", "shm"]  # rehearsal: ranks may share one GPU
-    cmd += [] if a.stagger else ["--no-stagger"]
     cmd += [] if a.cu_mask_queues else ["--pool-queues"]
     cmd += [] if a.head_on_slot_streams else ["--head-pool-streams"]
     cmd += [] if a.numa_bind == "on" else ["--no-numa-bind"]
-    cmd += ["--stream-sync", str(a.stream_sync)]
     if a.emulate:
         cmd[cmd.index("--gpus") + 1] = "1"
         cmd += ["--emulate", a.emulate]  # one rank of a WORLD-way split, alone (per-rank proxy)
@@ -632,11 +624,9 @@ def main():
                 "halo_depth": int(blur.engine.halo),
                 "fuse": int(blur.engine.fuse),
                 "stream_chunks": int(a.stream_chunks),
-                "stream_sync": int(a.stream_sync),
                 "preload_halo": bool(blur.preload_halo),
                 "launches_per_step": int(stats.launches),
                 "exchanges_per_step": int(stats.exchanges),
-                "stagger": bool(a.stagger),
                 "cu_mask_queues": bool(a.cu_mask_queues),
                 "head_on_slot_streams": bool(a.head_on_slot_streams),
                 "ipc_pull": a.ipc_pull,

@@ -66,12 +66,10 @@ struct CliConfig {
   int tune = -1;                          // SWAR tile tuning: -1 auto (one-shot off, server on), 0 off, 1 on
   int64_t ring_chunk_bytes = int64_t(32) << 20;  // one-shot ring staging chunk (0: one pinned image)
   double auto_gpu_min_s = 0.1;            // --backend auto: CPU seconds above which the GPU runs the job
-  bool stagger = true;                    // --bench: burst stagger of the first uploads
   bool cu_mask_queues = true;             // --bench: slot streams on dedicated (CU-masked) queues
   bool head_on_slot_streams = true;       // --bench: streamed head image's copies on the next slots' streams
   std::string ipc_pull = "grid";          // --transport ipc: pull form (grid | single | sdma)
   bool numa_bind = true;                  // N > 1: each rank on its GPU's NUMA node
-  int stream_sync = 0;                    // --bench: EngineOptions::stream_sync
 };
 
 // Parse argv.  Throws pconv::Error with the message to print on bad input.

@@ -74,20 +74,7 @@ struct EngineOptions {
   // fork/join branches it measured 1.4-4.3x slower per image
   // (profiles/r04/stream_a/).
   int stream_chunks = 0;
-  // Cross-stream order of a streamed image: 0 events (upload -> launches ->
-  // download on three streams), 1 downloads on the compute stream right
-  // behind each chunk's launches, 2 as 1 with the upload -> launch order by
-  // stream memory operations on signal memory (hipStreamWriteValue32 /
-  // hipStreamWaitValue32) instead of events.
-  int stream_sync = 0;
-  // Step graphs record an event right after their upload (upload_event()):
-  // a pipeline staggers the first images of a burst on it (BandPipeline).
-  bool upload_event = false;
   // ---- serving-pipeline policy (BandPipeline, slot-stream mode) ----
-  // Burst stagger: the first `slots` images of a burst start their uploads
-  // one after another (on the previous image's upload event) instead of all
-  // at once.
-  bool stagger = true;
   // Slot streams on dedicated hardware queues (created with an all-CU mask):
   // from the runtime's shared pool, 4 slot streams landed on queues of which
   // two ran every launch ~5x longer (profiles/r04/slots_c/).
@@ -118,13 +105,6 @@ class BandEngine {
   static constexpr size_t kMaxCachedGraphs = 64;
   size_t cached_graphs() const { return graphs_.size() + step_graphs_.size(); }
   size_t cached_step_graphs() const { return step_graphs_.size(); }
-  // Event-record nodes over the cached step graphs (tests: the upload event
-  // of the burst stagger is a real node, recorded by every replay).
-  int step_graph_event_nodes() const {
-    int n = 0;
-    for (const auto& kv : step_graphs_) n += kv.second.event_nodes;
-    return n;
-  }
   hipStream_t compute_stream() const { return cs_; }
   hipStream_t comm_stream() const { return ms_; }
 
@@ -193,13 +173,9 @@ class BandEngine {
   // Enqueue a streamed image: chunk uploads on `up`, launches on the compute
   // stream, downloads of the finished rows on `down` (cross-stream events per
   // chunk).  The caller orders `up` after any earlier use of these frames.
-  // Returns the stream whose completion means the whole image is done
-  // (`down`, or the compute stream when the downloads ride on it).
+  // Returns the stream whose completion means the whole image is done.
   hipStream_t enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
                                const StreamPlan& sp, hipStream_t up, hipStream_t down);
-  // With options().upload_event: recorded by every step graph once its
-  // upload is done.
-  const Event& upload_event() const { return ev_uploaded_; }
   // Phase-by-phase execution for multi-band emulation on one device.
   std::vector<Phase> plan(int reps) const;
   void exec_exchange(const Phase& p);
@@ -234,10 +210,8 @@ class BandEngine {
   int pre_exchanges_ = 0;  // exchange_now() calls since the last run()
   Stream own_cs_, own_ms_;
   hipStream_t cs_ = nullptr, ms_ = nullptr;
-  Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_, ev_uploaded_;
+  Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_;
   std::vector<Event> up_evs_, dn_evs_;  // streamed images: per chunk, uploaded / rows final
-  uint32_t* seq_flag_ = nullptr;        // stream_sync 2: chunk sequence word (signal memory)
-  uint32_t seq_ = 0;
   std::shared_ptr<HaloTransport> transport_;
   RunStats stats_;
   double wall_t0_ = 0;
@@ -249,7 +223,6 @@ class BandEngine {
     int end_cur = 0;
     int launches = 0;
     int exchanges = 0;
-    int event_nodes = 0;  // event-record nodes of the captured graph (the stagger's upload event)
   };
   // (reps, start buffer, in, in_r0, in_r1, out) -> whole-step graph.  Keyed
   // on host pointers, so both caches are bounded: past kMaxCachedGraphs
@@ -321,15 +294,8 @@ class BandPipeline {
   // step-graph mode with stream_chunks > 1: images submitted while nothing is
   // in flight (after construction / drain) are row-streamed (head streaming)
   bool idle_ = true;
-  // Burst stagger (step-graph mode): image i < slots of a burst (counted from
-  // the last drain) starts its upload only when image i-1's upload is done,
-  // instead of all slots uploading at once and moving in lockstep.
-  bool stagger_ = true;
   bool head_streaming_ = false;  // stream_chunks > 1 with step graphs
   bool head_on_slots_ = false;   // the head's copies on the next two slots' streams
-  int burst_ = 0;
-  const Event* last_upload_ = nullptr;  // upload-done event of the burst's previous image
-  Event head_up_;                       // a streamed head image's uploads done
   Event ev_head_, h2d_wait_;
   std::vector<bool> used_;
   int64_t count_ = 0;

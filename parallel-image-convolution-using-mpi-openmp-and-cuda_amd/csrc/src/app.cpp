@@ -848,10 +848,8 @@ void bench_rank(const CliConfig& c, BenchShared* sh, uint8_t* image, int rank) {
   const Filter f = Filter::by_name(c.filter);
   const Band b = row_band(g.height, world, rank);
   EngineOptions o = engine_options(c, g, world, device);
-  o.stagger = c.stagger;
   o.cu_mask_queues = c.cu_mask_queues;
   o.head_on_slot_streams = c.head_on_slot_streams;
-  o.stream_sync = c.stream_sync;
   // Pre-loaded ghost zone deep enough for every repetition (exchange-free
   // images, like bench.py's headline): rows of the band's dependency cone.
   if (world > 1 && c.halo == 0 && c.reps <= g.height / world) o.halo_depth = std::max(c.reps, o.fuse);
@@ -1026,7 +1024,7 @@ std::string run_bench_impl(const CliConfig& c) {
      << c.reps << " reps\", \"global_batch\": 1, \"seq_len\": " << c.height << ", \"parallelism\": \"rowband"
      << c.gpus << "\", \"step\": \"H2D + reps + D2H per image (reference GPU_convolution scope)\", \"halo_mode\": \""
      << (c.gpus > 1 || c.emulate_world > 1 ? "preload" : "none") << "\", \"images_in_flight\": " << c.slots
-     << ", \"stream_chunks\": " << c.stream_chunks << ", \"stream_sync\": " << c.stream_sync << ", \"stagger\": " << (c.stagger ? "true" : "false")
+     << ", \"stream_chunks\": " << c.stream_chunks
      << ", \"cu_mask_queues\": " << (c.cu_mask_queues ? "true" : "false")
      << ", \"head_on_slot_streams\": " << (c.head_on_slot_streams ? "true" : "false")
      << ", \"numa_bind\": " << (c.numa_bind ? "true" : "false") << ", \"halo_depth\": " << sh->halo << ", \"fuse\": " << sh->fuse

@@ -67,7 +67,6 @@ std::string help_text(const std::string& prog) {
          "  --slots S                 --bench: images in flight (default 4)\n"
          "  --stream-chunks C         --bench: rows of each image streamed in C chunks (0 = off)\n"
          "  --emulate W:R             --bench: time rank R of a W-way split alone (per-rank proxy)\n"
-         "  --no-stagger              --bench: the first images of a burst upload all at once\n"
          "  --pool-queues             --bench: slot streams from the runtime's queue pool (default: each on\n"
          "                            its own CU-masked hardware queue)\n"
          "  --head-pool-streams       --bench: a streamed head image's copies on two pool streams (default:\n"
@@ -76,8 +75,7 @@ std::string help_text(const std::string& prog) {
          "  --tune {auto,on,off}      SWAR tile-shape tuning (auto: off for a one-shot run, on in a server)\n"
          "  --ring-chunk-bytes B      one-shot staging ring chunk (default 32 MiB; 0 = one pinned image)\n"
          "  --no-numa-bind            N > 1: leave each rank's CPU affinity alone\n"
-         "  --stream-sync M           --bench: streamed image order: 0 events, 1 downloads on the compute\n"
-         "                            stream, 2 as 1 with signal-memory waits for the uploads\n"
+
          "\n"
          "       " + prog + " --serve SOCKET [--device D] [--idle-timeout S] [--max-engines N]\n"
          "                            resident service: initialise the GPU once, then run jobs sent by\n"
@@ -183,8 +181,6 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       c.emulate_rank = static_cast<int>(parse_int(v.substr(colon + 1), "--emulate rank", 0, c.emulate_world - 1));
     } else if (a == "--stream-chunks") {
       c.stream_chunks = static_cast<int>(parse_int(next("--stream-chunks"), "--stream-chunks", 0, 4096));
-    } else if (a == "--no-stagger") {
-      c.stagger = false;
     } else if (a == "--pool-queues") {
       c.cu_mask_queues = false;
     } else if (a == "--head-pool-streams") {
@@ -206,8 +202,6 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       char* end = nullptr;
       c.auto_gpu_min_s = std::strtod(v.c_str(), &end);
       if (v.empty() || *end != '\0' || !(c.auto_gpu_min_s >= 0)) PCONV_FAIL("invalid --auto-gpu-min '" + v + "'");
-    } else if (a == "--stream-sync") {
-      c.stream_sync = static_cast<int>(parse_int(next("--stream-sync"), "--stream-sync", 0, 2));
     } else if (a == "--no-numa-bind") {
       c.numa_bind = false;
     } else if (a == "--warmup") {

@@ -65,7 +65,6 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
   ev_sync_ = Event::create();
   ev_t0_ = Event::create(true);
   ev_t1_ = Event::create(true);
-  if (opt_.upload_event) ev_uploaded_ = Event::create();
   PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
 }
 
@@ -73,7 +72,6 @@ BandEngine::~BandEngine() {
   // Drain first: a cached graph may still be executing on the stream.
   if (cs_) (void)hipStreamSynchronize(cs_);
   if (ms_ && ms_ != cs_) (void)hipStreamSynchronize(ms_);
-  if (seq_flag_) (void)hipFree(seq_flag_);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : step_graphs_) (void)hipGraphExecDestroy(kv.second.exec);
 }
@@ -382,54 +380,6 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
       copy(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, ch.down_hi - ch.down_lo,
            hipMemcpyDeviceToHost, s);
   };
-  const int sync = opt_.stream_sync;
-  if (sync == 2 && up != cs_) {
-    // Cross-stream order by stream memory operations on HSA signal memory
-    // (hipStreamWriteValue32 / hipStreamWaitValue32) instead of events: the
-    // upload stream writes chunk c's sequence number, the compute stream
-    // waits for it; downloads ride on the compute stream (mode 1's order).
-    if (!seq_flag_) {
-      void* f = nullptr;
-      PCONV_HIP_CHECK(hipExtMallocWithFlags(&f, 64, hipMallocSignalMemory));
-      seq_flag_ = static_cast<uint32_t*>(f);
-      PCONV_HIP_CHECK(hipMemset(seq_flag_, 0, 64));
-    }
-    const uint32_t base = seq_;
-    seq_ += static_cast<uint32_t>(nc);
-    for (size_t c = 0; c < nc; ++c) {
-      const StreamChunk& ch = sp.chunks[c];
-      copy(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, ch.up_hi - ch.up_lo,
-           hipMemcpyHostToDevice, up);
-      PCONV_HIP_CHECK(hipStreamWriteValue32(up, seq_flag_, base + static_cast<uint32_t>(c) + 1, 0));
-    }
-    for (size_t c = 0; c < nc; ++c) {
-      PCONV_HIP_CHECK(hipStreamWaitValue32(cs_, seq_flag_, base + static_cast<uint32_t>(c) + 1,
-                                           hipStreamWaitValueGte, 0xffffffffu));
-      launches(sp.chunks[c]);
-      download(sp.chunks[c], cs_);
-    }
-    cur_ = (c0 + sp.levels) & 1;
-    halo_valid_ = false;
-    return cs_;
-  }
-  if (sync == 1 || down == cs_) {
-    // Downloads on the compute stream right behind each chunk's launches
-    // (stream order, no launch -> D2H hop); uploads on `up` as in mode 0.
-    for (size_t c = 0; c < nc; ++c) {
-      const StreamChunk& ch = sp.chunks[c];
-      copy(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, ch.up_hi - ch.up_lo,
-           hipMemcpyHostToDevice, up);
-      if (up != cs_) up_evs_[c].record(up);
-    }
-    for (size_t c = 0; c < nc; ++c) {
-      if (up != cs_) up_evs_[c].wait_on(cs_);
-      launches(sp.chunks[c]);
-      download(sp.chunks[c], cs_);
-    }
-    cur_ = (c0 + sp.levels) & 1;
-    halo_valid_ = false;
-    return cs_;
-  }
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     copy(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, ch.up_hi - ch.up_lo,
@@ -499,23 +449,6 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     prepare(ph);  // tile-shape tuning cannot run inside the capture
     PCONV_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
     upload_rows(host_in, rb, in_r0, in_r1, cs_);
-    // The upload-done event as a real event-record NODE hanging off the
-    // upload: a plain hipEventRecord inside a capture only orders nodes of
-    // this graph, so replays of the instantiated graph would never record
-    // the event (hipEventRecordWithFlags(..., hipEventRecordExternal) is
-    // refused by torch's HIP 7.0 runtime).  The node is added to the graph
-    // being captured with the upload as its only dependency and is left out
-    // of the stream's capture dependencies: nothing waits on it.
-    if (opt_.upload_event) {
-      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-      hipGraph_t cg = nullptr;
-      const hipGraphNode_t* deps = nullptr;
-      size_t ndeps = 0;
-      PCONV_HIP_CHECK(hipStreamGetCaptureInfo_v2(cs_, &st, nullptr, &cg, &deps, &ndeps));
-      PCONV_CHECK(st == hipStreamCaptureStatusActive && cg != nullptr, "step graph: capture not active");
-      hipGraphNode_t ev_node = nullptr;
-      PCONV_HIP_CHECK(hipGraphAddEventRecordNode(&ev_node, cg, deps, ndeps, ev_uploaded_.get()));
-    }
     if (zone_first) {
       transport_->exchange(*this, lay_.halo, cs_);  // stream order: after the upload, before the launches
       ++stats_.exchanges;
@@ -524,17 +457,6 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     if (host_out) download_rows(host_out, rb, 0, band_.rows, cs_);  // nullptr: the caller downloads itself
     PCONV_HIP_CHECK(hipStreamEndCapture(cs_, &g));
     StepGraph sg;
-    {
-      size_t nn = 0;
-      PCONV_HIP_CHECK(hipGraphGetNodes(g, nullptr, &nn));
-      std::vector<hipGraphNode_t> nodes(nn);
-      if (nn) PCONV_HIP_CHECK(hipGraphGetNodes(g, nodes.data(), &nn));
-      for (size_t i = 0; i < nn; ++i) {
-        hipGraphNodeType t{};
-        PCONV_HIP_CHECK(hipGraphNodeGetType(nodes[i], &t));
-        sg.event_nodes += t == hipGraphNodeTypeEventRecord ? 1 : 0;
-      }
-    }
     PCONV_HIP_CHECK(hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0));
     PCONV_HIP_CHECK(hipGraphDestroy(g));
     sg.end_cur = cur_;
@@ -593,8 +515,6 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
     // no split launches.  With it, each slot's exchanges run on the slot's
     // own communication stream beside the interior launch.
     o.overlap = slot_comm && opt.overlap;
-    stagger_ = step_graphs && opt.stagger;
-    o.upload_event = stagger_;
     // Slot streams on dedicated hardware queues (opt.cu_mask_queues): a
     // stream created with a CU mask (all CUs) gets its own HSA queue instead
     // of one from the runtime's round-robin pool.  From the pool, 4 slot
@@ -636,7 +556,6 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
       }
       ev_head_ = Event::create();
       h2d_wait_ = Event::create();
-      head_up_ = Event::create();
       head_streaming_ = true;
     }
     used_.assign(slots, false);
@@ -724,11 +643,6 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   }
   if (graphs_) {
     PCONV_CHECK(trace_ev_.empty(), "pipeline trace needs directly issued images (graph capture off)");
-    if (idle_) {
-      burst_ = 0;
-      last_upload_ = nullptr;
-    }
-    const int pos = burst_++;
     if (idle_ && head_streaming_) {
       // Head streaming: nothing is in flight, so this image's rows stream
       // (chunked H2D ‖ launches ‖ D2H of finished rows, schedule.hpp
@@ -745,8 +659,6 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
         h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
         h2d_wait_.wait_on(up);
         hipStream_t done = e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down);
-        head_up_.record(up);  // every chunk upload issued first: all of them done
-        last_upload_ = &head_up_;
         if (done != e.compute_stream()) {
           ev_head_.record(done);
           ev_head_.wait_on(e.compute_stream());
@@ -757,16 +669,7 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
         return;
       }
     }
-    if (stagger_ && pos > 0 && pos < slots() && last_upload_) {
-      // Head of a burst: start this upload when the previous image's is done
-      // (one cross-stream wait per image, first `slots` images only).  All
-      // slots uploading at once would split the link three ways and move the
-      // slots in lockstep — no download beside an upload until the whole
-      // first group is in (the driver's 20-image window pays that).
-      last_upload_->wait_on(e.compute_stream());
-    }
     e.process_graph(host_in, in_r0, in_r1, host_out, reps);
-    last_upload_ = stagger_ ? &e.upload_event() : nullptr;
     idle_ = false;
     used_[k] = true;
     ++count_;

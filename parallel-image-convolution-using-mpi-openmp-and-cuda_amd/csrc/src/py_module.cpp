@@ -456,7 +456,6 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_property_readonly("fuse", [](const BandEngine& e) { return e.options().fuse; })
       .def_property_readonly("cached_graphs", &BandEngine::cached_graphs)
       .def_property_readonly("cached_step_graphs", &BandEngine::cached_step_graphs)
-      .def_property_readonly("step_graph_event_nodes", &BandEngine::step_graph_event_nodes)
       .def_property_readonly_static("max_cached_graphs", [](py::object) { return BandEngine::kMaxCachedGraphs; })
       .def_property_readonly("pitch", [](const BandEngine& e) { return e.layout().pitch; })
       .def_property_readonly("row_bytes", [](const BandEngine& e) { return e.layout().row_bytes; })
@@ -575,12 +574,9 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
                        int concurrent, bool graphs, bool step_graphs, py::object band, bool slot_comm,
-                       int stream_chunks, bool stagger, bool cu_mask_queues, bool head_on_slot_streams,
-                       int stream_sync) {
+                       int stream_chunks, bool cu_mask_queues, bool head_on_slot_streams) {
              EngineOptions o;
              o.stream_chunks = stream_chunks;
-             o.stream_sync = stream_sync;
-             o.stagger = stagger;
              o.cu_mask_queues = cu_mask_queues;
              o.head_on_slot_streams = head_on_slot_streams;
              o.device = device;
@@ -599,8 +595,7 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1,
            py::arg("graphs") = false, py::arg("step_graphs") = true,
            py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0,
-           py::arg("stagger") = true, py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true,
-           py::arg("stream_sync") = 0)
+           py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -633,8 +628,6 @@ PYBIND11_MODULE(_pconv_native, m) {
                                const EngineOptions& o = p.slot(0).options();
                                py::dict d;
                                d["stream_chunks"] = o.stream_chunks;
-                               d["stream_sync"] = o.stream_sync;
-                               d["stagger"] = o.stagger;
                                d["cu_mask_queues"] = o.cu_mask_queues;
                                d["head_on_slot_streams"] = o.head_on_slot_streams;
                                return d;

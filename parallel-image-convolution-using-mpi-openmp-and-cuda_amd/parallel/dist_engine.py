@@ -75,11 +75,10 @@ class DistributedBlur:
                  variant: str = "auto", graph: bool = False, transport: str = "rccl", concurrent: int = -1,
                  step_graphs: Optional[bool] = None, graph_capture: bool = True, slot_exchange: bool = False,
                  self_neighbours: bool = False, slot_comm: bool = False, stream_chunks: int = 0,
-                 ipc_timeout_s: float = 30.0, ipc_pull: str = "grid", stagger: bool = True,
-                 cu_mask_queues: bool = True, head_on_slot_streams: bool = True, stream_sync: int = 0):
+                 ipc_timeout_s: float = 30.0, ipc_pull: str = "grid", cu_mask_queues: bool = True,
+                 head_on_slot_streams: bool = True):
         """Pipeline policy (native EngineOptions, echoed by bench.py's JSON
-        config): `stagger` starts the first images of a burst one upload after
-        another; `cu_mask_queues` puts every slot stream on its own hardware
+        config): `cu_mask_queues` puts every slot stream on its own hardware
         queue; `head_on_slot_streams` runs a streamed head image's copies on
         the next slots' streams; `ipc_pull` is the IPC transport's pull form
         (grid | single | sdma, ipc_halo.hpp)."""
@@ -99,9 +98,8 @@ class DistributedBlur:
         # that many chunks and its levels advance behind them (H2D, launches
         # and D2H of ONE image overlap; schedule.hpp plan_streamed)
         kw = dict(halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant, slots=int(slots),
-                  concurrent=int(concurrent), stream_chunks=int(stream_chunks), stagger=bool(stagger),
-                  cu_mask_queues=bool(cu_mask_queues), head_on_slot_streams=bool(head_on_slot_streams),
-                  stream_sync=int(stream_sync))
+                  concurrent=int(concurrent), stream_chunks=int(stream_chunks),
+                  cu_mask_queues=bool(cu_mask_queues), head_on_slot_streams=bool(head_on_slot_streams))
         if self_neighbours:
             # One-GPU emulation of rank `rank` of a `world`-way split whose halos
             # really move: its neighbours are replaced by itself (a 1-rank

@@ -270,13 +270,12 @@ def test_bench_policy_flags():
     try:
         sys.argv = ["bench.py"]
         a = bench.parse()
-        assert (a.stagger, a.cu_mask_queues, a.head_on_slot_streams, a.ipc_pull, a.numa_bind) == \
-            (True, True, True, "grid", "on")
-        sys.argv = ["bench.py", "--no-stagger", "--pool-queues", "--head-pool-streams", "--ipc-pull", "sdma",
+        assert (a.cu_mask_queues, a.head_on_slot_streams, a.ipc_pull, a.numa_bind) == (True, True, "grid", "on")
+        sys.argv = ["bench.py", "--pool-queues", "--head-pool-streams", "--ipc-pull", "sdma",
                     "--numa-bind", "off"]
         a = bench.parse()
     finally:
         sys.argv = old
     kw = bench.policy_kwargs(a)
-    assert kw == dict(stagger=False, cu_mask_queues=False, head_on_slot_streams=False, ipc_pull="sdma", stream_sync=0)
+    assert kw == dict(cu_mask_queues=False, head_on_slot_streams=False, ipc_pull="sdma")
     assert bench.mode_kwargs(a, "ipc", 8)["ipc_pull"] == "sdma"

@@ -180,34 +180,6 @@ def test_pipeline_step_graphs(pconv_mod, rng, slots, reps, fuse):
             assert np.array_equal(blur.outputs[k].reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps)), (rnd, k)
 
 
-@pytest.mark.parametrize("stagger", [True, False])
-def test_stagger_event_is_a_graph_node(pconv_mod, rng, stagger):
-    """Burst stagger: every step graph carries the upload-done event as a
-    real event-record node (a plain record inside a capture would only order
-    nodes of that graph and replays would never record it, ADVICE r04);
-    bursts with and without it are bit-exact."""
-    from pconv.parallel.dist_engine import DistributedBlur
-
-    w, h, reps, slots = 67, 45, 13, 4
-    blur = DistributedBlur(w, h, "rgb", "gaussian", reps, rank=0, world=1, device=0, slots=slots, step_graphs=True,
-                           stagger=stagger)
-    assert blur.pipe.options["stagger"] is stagger
-    for rnd in range(3):
-        imgs = [rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for _ in range(slots)]
-        ks = []
-        for img in imgs:
-            k = blur._next
-            blur.load_image(img, slot=k)
-            ks.append(blur.submit(reps))
-        blur.drain()
-        for img, k in zip(imgs, ks):
-            assert np.array_equal(blur.outputs[k].reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps)), (rnd, k)
-    for k in range(slots):
-        e = blur.pipe.slot(k)
-        assert e.cached_step_graphs >= 1
-        assert e.step_graph_event_nodes == (e.cached_step_graphs if stagger else 0), (k, e.step_graph_event_nodes)
-
-
 def test_pipeline_step_graphs_preloaded_band(pconv_mod, rng):
     """A middle band of a 3-way split with pre-loaded ghost rows >= reps runs
     as step graphs and matches the oracle rows (no transport involved)."""

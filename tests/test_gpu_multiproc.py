@@ -100,7 +100,7 @@ def test_bench_torchrun_rehearsal(world, extra):
     assert len(meta["h2d_bytes_per_step"]) == world and len(meta["d2h_bytes_per_step"]) == world
     assert sum(meta["d2h_bytes_per_step"]) == 1920 * 2520 * 3
     assert all(i >= o for i, o in zip(meta["h2d_bytes_per_step"], meta["d2h_bytes_per_step"]))
-    assert meta["config"]["ipc_pull"] == "grid" and meta["config"]["stagger"] is True
+    assert meta["config"]["ipc_pull"] == "grid" and meta["config"]["cu_mask_queues"] is True
     modes = meta["halo_modes"]
     head = "event" if "--halo-mode" in extra else "preload"
     assert set(modes) == {head, "slot_exchange", "slot_exchange_direct", "event", "overlap", "ipc"}, modes

@@ -59,25 +59,6 @@ def test_streamed_pipeline_bit_exact(pconv_mod, rng, mode, slots, chunks, w, h, 
 
 
 @pytest.mark.parametrize("mode", ["direct", "head"])
-@pytest.mark.parametrize("sync", [1, 2])
-@pytest.mark.parametrize("slots", [1, 4])
-@pytest.mark.parametrize("chunks", [3, 4, 8])
-@pytest.mark.parametrize("w,h,ch,reps", [(67, 45, "rgb", 9), (64, 133, "grey", 40), (1920, 252, "rgb", 40)])
-def test_streamed_sync_modes_bit_exact(pconv_mod, rng, mode, sync, slots, chunks, w, h, ch, reps):
-    """stream_sync 1 (downloads on the compute stream behind each chunk's
-    launches) and 2 (as 1, the uploads ordered by signal-memory stream waits):
-    bursts and single images bit-exact."""
-    blur = _blur(w, h, ch, "gaussian", reps, chunks, slots=slots, mode=mode, stream_sync=sync)
-    assert blur.pipe.options["stream_sync"] == sync
-    _run_images(pconv_mod, rng, blur, w, h, ch, "gaussian", reps, rounds=3)
-    img = rng.integers(0, 256, size=(h, w, CH[ch]), dtype=np.uint8)
-    blur.load_image(img)
-    ref = pconv_mod.numpy_convolve(img if CH[ch] > 1 else img[..., 0], reps).reshape(h, -1)
-    for _ in range(3):
-        assert np.array_equal(blur.step(reps).reshape(h, -1), ref)
-
-
-@pytest.mark.parametrize("mode", ["direct", "head"])
 @pytest.mark.parametrize("filt", ["box", "edge"])
 def test_streamed_float_filters(pconv_mod, rng, mode, filt):
     _run_images(pconv_mod, rng, _blur(59, 83, "rgb", filt, 11, 4, mode=mode), 59, 83, "rgb", filt, 11)
