@@ -2,50 +2,47 @@
 //
 // Replaces the reference's MPI_Isend/Irecv of boundary rows and the
 // MPI_Wait pairs around them (mpi/mpi_convolution.c:157-234) for ranks that
-// are processes on ONE node: every rank exports its two frames with
-// hipIpcGetMemHandle once, opens its neighbours' frames with
-// hipIpcOpenMemHandle (same GPU, or a peer GPU mapped over xGMI), and an
-// exchange PULLS the neighbours' boundary rows straight into its own ghost
-// rows with device copies — no communication library kernel, no host
-// staging, nothing on the host path after set-up.
+// are processes on ONE node: every rank exports its two frames and a small
+// device-memory MAILBOX with hipIpcGetMemHandle once, opens its neighbours'
+// (same GPU, or a peer GPU mapped over xGMI), and an exchange PULLS the
+// neighbours' boundary rows straight into its own ghost rows — no
+// communication library kernel, no host staging, nothing on the host path
+// after set-up.
 //
-// Three pull forms (IpcPull, chosen per transport; docs/PERFORMANCE.md has
-// the measurements that pick the default):
-//   * Grid (default): ONE dispatch of G workgroups.  Every workgroup's
-//     thread 0 waits for the neighbours' level flags with its own
-//     system-scope acquire (so each CU's and each XCD's caches are
-//     invalidated for the rows it reads), the workgroup copies its slice,
-//     and the workgroups meet on a device-memory arrival counter; the last
-//     one to arrive publishes `count` / `ack` and waits for the neighbours'
-//     acks.  G workgroups keep G times the single form's bytes in flight —
-//     what a pull over xGMI (microseconds per round trip) needs.
-//   * Single: the same in ONE workgroup (round 4's form: one acquire
-//     covers it; latency-bound on a remote source).
-//   * Sdma: a one-thread signal / wait kernel, the rows moved by SDMA
-//     (hipMemcpyAsync peer copies, no CU involved), a one-thread ack / wait
-//     kernel.  The copies cannot be skipped after a timed-out wait: a
-//     neighbour that stalls (but keeps its frames mapped) yields stale
-//     rows and the raised error, as in the other forms.
-// The rows a neighbour reads always come from an earlier kernel of its
-// stream, whose end-of-kernel release wrote them back on every XCD.
-// Ordering across processes is device-side, through flag words in a shared
-// host-memory segment (POSIX shm, registered with hipHostRegister so every
-// rank's GPU reads and writes it with system-scope atomics).  Per (rank,
-// slot): `count` (exchanges done by this transport), `level` (its rows for
-// exchange #count are final) and `ack` (it has copied its neighbours' rows of
-// exchange #count).  One exchange, all in stream order on the caller's
-// stream:
-//   1. signal kernel: count += 1; level = count; wait until every
-//      neighbour's level >= count (their rows are final);
-//   2. pull kernel: the neighbours' rows (same frame parity: bands advance
-//      in lockstep) copied into this rank's ghost rows by the CUs, reading
-//      the neighbours' memory directly (skipped after a timeout);
-//   3. ack kernel: ack = count; wait until every neighbour's ack >= count
-//      (they have copied this rank's rows, so later launches may overwrite
-//      them — the reference's wait on its sends before the swap).
-// The exchange number lives in device-visible memory, so a captured graph
-// replays correctly.  Every wait has a timeout: an expired wait sets the
-// rank's error word and returns (no wave spins forever); check() raises.
+// Signalling is push-to-the-poller: a rank WRITES its exchange number into
+// its neighbours' mailboxes (one remote store each) and POLLS only its own
+// mailbox (local HBM), so no poll ever crosses PCIe or xGMI.  Per rank and
+// slot the mailbox holds `count` (exchanges done, written by the rank
+// itself), `level_up` / `level_down` (the upper / lower neighbour's rows of
+// exchange #n are final) and `ack_up` / `ack_down` (that neighbour has copied
+// this rank's rows), each on its own cache line.  One exchange, n = count+1,
+// in stream order on the caller's stream:
+//   1. signal: level_down of the upper neighbour's mailbox = n, level_up of
+//      the lower one's = n; wait until this mailbox's level_up / level_down
+//      >= n (the neighbours' rows are final: they came from earlier kernels
+//      of their streams, whose end-of-kernel release wrote them back);
+//   2. pull: the neighbours' rows (same frame parity: bands advance in
+//      lockstep) into this rank's ghost rows (skipped after a timeout);
+//   3. ack: count = n; ack_down / ack_up of the neighbours' mailboxes = n;
+//      wait until this mailbox's acks >= n (they have copied this rank's
+//      rows, so later launches may overwrite them — the reference's wait on
+//      its sends before the swap).
+// Three forms (IpcPull; docs/PERFORMANCE.md has the measurements):
+//   * Grid (default): ONE dispatch of G workgroups; every workgroup's thread
+//     0 waits with its own system-scope acquire (each CU's and XCD's caches
+//     invalidated for the rows it reads), copies its slice, and arrives on a
+//     counter in the mailbox; the last one performs step 3.  G workgroups
+//     keep G times the single form's bytes in flight — what a pull over
+//     xGMI (microseconds per round trip) needs.
+//   * Single: the same in ONE workgroup (round 4's form).
+//   * Sdma: one-thread signal and ack kernels around SDMA peer copies.  The
+//     copies cannot be skipped after a timed-out wait: a neighbour that
+//     stalls (but keeps its frames mapped) yields stale rows and the raised
+//     error, as in the other forms.
+// The exchange number lives in device memory, so a captured graph replays
+// correctly.  Every wait has a wall-clock timeout: an expired wait sets the
+// rank's error word (a host shared-memory segment the host checks) and
+// returns (no wave spins forever); check() raises.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -58,15 +55,27 @@
 
 namespace pconv {
 
-// Flag words of one (rank, slot), padded to a cache line.
+// Host-visible words of one (rank, slot), padded to a cache line: the
+// error word (1: a level wait timed out, 2: an ack wait timed out).
 struct IpcFlags {
-  uint32_t count;
-  uint32_t level;
-  uint32_t ack;
   uint32_t err;
-  uint32_t pad[12];
+  uint32_t pad[15];
 };
 static_assert(sizeof(IpcFlags) == 64, "one cache line per flag block");
+
+// Device-memory mailbox of one (rank, slot); one cache line per word.
+struct IpcMailbox {
+  uint32_t count, pad0[15];
+  uint32_t level_up, pad1[15];    // written by the upper neighbour
+  uint32_t level_down, pad2[15];  // written by the lower neighbour
+  uint32_t ack_up, pad3[15];
+  uint32_t ack_down, pad4[15];
+  uint32_t arrive, pad5[15];      // grid form: workgroups done with this exchange
+};
+static_assert(sizeof(IpcMailbox) == 384, "six cache lines");
+
+// hipIpcMemHandle_t of frame 0, frame 1 and the mailbox, back to back.
+constexpr size_t kIpcHandleBytes = 3 * sizeof(hipIpcMemHandle_t);
 
 // Create (rank 0) / map (every rank) the shared flag segment of a job:
 // world x slots flag blocks, zeroed at creation.
@@ -77,20 +86,21 @@ enum class IpcPull { Grid, Single, Sdma };
 IpcPull parse_ipc_pull(const std::string& s);  // "grid" | "single" | "sdma"
 const char* ipc_pull_name(IpcPull p);
 
-// One exchange in stream order on `s` (kernels/ipc_flags.hip).  `flags` is
-// the device pointer of the segment's block array; dst_* are this rank's
-// ghost rows, src_* the neighbours' boundary rows (null: no neighbour on that
-// side), `bytes` per side, a multiple of 16.  Grid needs `arrive` (one zeroed
-// device word per transport, left zeroed by every exchange) and uses
-// `workgroups` (0: chosen from the size).
-void launch_ipc_exchange(IpcPull form, IpcFlags* flags, uint32_t* arrive, int me, int up, int down,
+// One exchange in stream order on `s` (kernels/ipc_flags.hip).  `mine` is
+// this rank's mailbox, `up_mb` / `down_mb` the neighbours' (null: no
+// neighbour on that side; this rank's own for a self-neighbour), `err` the
+// device address of this rank's host-visible error word; dst_* are this
+// rank's ghost rows, src_* the neighbours' boundary rows, `bytes` per side, a
+// multiple of 16.  Grid uses `workgroups` (0: chosen from the size).
+void launch_ipc_exchange(IpcPull form, IpcMailbox* mine, IpcMailbox* up_mb, IpcMailbox* down_mb, uint32_t* err,
                          uint64_t timeout_ticks, uint8_t* dst_up, const uint8_t* src_up, uint8_t* dst_down,
                          const uint8_t* src_down, int64_t bytes, hipStream_t s, int workgroups = 0);
 // Workgroups the Grid form uses for `bytes` per side.
 int ipc_grid_workgroups(int64_t bytes);
 
-// Cost of one exchange of each pull form without a neighbour process: a flag
-// block in pinned host memory (self-neighbour protocol, up = down = me),
+// Cost of one exchange of each pull form without a neighbour process: a
+// mailbox in device memory and an error word in pinned host memory
+// (self-neighbour protocol: this rank is its own upper and lower neighbour),
 // `bytes` per side pulled from a pinned HOST buffer (host_source: the
 // stand-in for a peer GPU's HBM behind xGMI — PCIe round trips of
 // microseconds) or from this GPU's HBM; ms per exchange over `iters`
@@ -108,7 +118,7 @@ class IpcHaloTransport : public HaloTransport {
   IpcHaloTransport(const IpcHaloTransport&) = delete;
   IpcHaloTransport& operator=(const IpcHaloTransport&) = delete;
 
-  // hipIpcMemHandle_t of frame 0 and frame 1, back to back.
+  // kIpcHandleBytes: frame 0, frame 1 and the mailbox.
   std::vector<uint8_t> local_handles() const { return handles_; }
   // Open the neighbours' frames (empty vector: no neighbour on that side).
   void connect(const std::vector<uint8_t>& up_handles, const std::vector<uint8_t>& down_handles);
@@ -131,7 +141,7 @@ class IpcHaloTransport : public HaloTransport {
   std::string segment_;
   size_t seg_bytes_ = 0;
   void* host_ = nullptr;       // mapped segment
-  IpcFlags* dflags_ = nullptr;  // its device address
+  IpcFlags* dflags_ = nullptr;  // its device address (error words)
   uint64_t timeout_ticks_ = 0;
   std::vector<uint8_t> handles_;
   uint8_t* peer_up_[2] = {nullptr, nullptr};    // neighbour frames (base of the allocation)
@@ -140,7 +150,9 @@ class IpcHaloTransport : public HaloTransport {
   bool connected_ = false;
   bool own_ = false;  // a neighbour is this engine itself (one-process emulation)
   IpcPull pull_ = IpcPull::Grid;
-  DeviceBuffer arrive_;  // Grid form: the workgroups' arrival counter
+  DeviceBuffer mail_;                       // this rank's mailbox (exported)
+  IpcMailbox* peer_mail_up_ = nullptr;      // the neighbours' mailboxes (opened)
+  IpcMailbox* peer_mail_down_ = nullptr;
   uint8_t* own_base_[2] = {nullptr, nullptr};  // this engine's frames (the destructor never touches the engine)
   int64_t enqueued_ = 0;
 };

@@ -1,12 +1,11 @@
-// Flag kernels of the HIP-IPC halo protocol (include/pconv/ipc_halo.hpp).
+// Kernels of the HIP-IPC halo protocol (include/pconv/ipc_halo.hpp).
 //
-// One thread each.  The flag words live in host shared memory that every
-// rank's GPU maps; they are read and written with system-scope atomics
-// through ordinary vector memory instructions (global loads / stores with
-// the system-coherence bits), so a rank's GPU sees a neighbour's store
-// without any cache maintenance.  Every wait is bounded by a wall-clock
-// timeout (wall_clock64, constant rate): on expiry the rank's error word is
-// set and the kernel returns, so no wave ever spins without end.
+// Signalling words live in device-memory mailboxes: a rank stores into its
+// neighbours' mailboxes (release, system scope: the store may cross xGMI)
+// and polls only its own (acquire, system scope, local HBM).  Every wait is
+// bounded by a wall-clock timeout (wall_clock64, constant rate): on expiry
+// the rank's host-visible error word is set and the kernel returns, so no
+// wave ever spins without end.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,34 +28,41 @@ __device__ __forceinline__ void store_sys(uint32_t* p, uint32_t v) {
 __device__ bool wait_ge(const uint32_t* p, uint32_t target, uint64_t t0, uint64_t timeout) {
   while (static_cast<int32_t>(load_sys(p) - target) < 0) {
     if (static_cast<uint64_t>(wall_clock64()) - t0 > timeout) return false;
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(1);
   }
   return true;
 }
 
-__global__ __launch_bounds__(64) void k_ipc_signal_wait(IpcFlags* f, int me, int up, int down, uint64_t timeout) {
-  if (threadIdx.x != 0) return;
+// Step 1 (thread 0): publish "my rows of exchange n are final" into the
+// neighbours' mailboxes (publish = false: another workgroup of this
+// dispatch does it) and wait for theirs; false on timeout.
+__device__ bool signal_wait(IpcMailbox* mine, IpcMailbox* up_mb, IpcMailbox* down_mb, uint32_t n, bool publish,
+                            uint64_t timeout) {
   const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
-  // Everything earlier on this stream (the launches that produced this
-  // rank's boundary rows) is complete when the kernel starts: publish them.
-  const uint32_t n = load_sys(&f[me].count) + 1;
-  store_sys(&f[me].count, n);
-  store_sys(&f[me].level, n);
+  if (publish) {
+    if (up_mb) store_sys(&up_mb->level_down, n);  // I am my upper neighbour's lower neighbour
+    if (down_mb) store_sys(&down_mb->level_up, n);
+  }
   bool ok = true;
-  if (up >= 0) ok = wait_ge(&f[up].level, n, t0, timeout);
-  if (ok && down >= 0) ok = wait_ge(&f[down].level, n, t0, timeout);
-  if (!ok) store_sys(&f[me].err, 1u);
+  if (up_mb) ok = wait_ge(&mine->level_up, n, t0, timeout);
+  if (ok && down_mb) ok = wait_ge(&mine->level_down, n, t0, timeout);
+  return ok;
 }
 
-__global__ __launch_bounds__(64) void k_ipc_ack_wait(IpcFlags* f, int me, int up, int down, uint64_t timeout) {
-  if (threadIdx.x != 0) return;
+// Step 3 (thread 0): count = n, publish "copied" into the neighbours'
+// mailboxes, wait for theirs.  Skipped after a timed-out level wait (the
+// neighbours' ack waits time out too).
+__device__ void ack_wait(IpcMailbox* mine, IpcMailbox* up_mb, IpcMailbox* down_mb, uint32_t* err, uint32_t n,
+                         uint64_t timeout) {
+  store_sys(&mine->count, n);
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
   const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
-  const uint32_t n = load_sys(&f[me].count);
-  store_sys(&f[me].ack, n);  // this rank's copies of exchange #n are complete
+  if (up_mb) store_sys(&up_mb->ack_down, n);
+  if (down_mb) store_sys(&down_mb->ack_up, n);
   bool ok = true;
-  if (up >= 0) ok = wait_ge(&f[up].ack, n, t0, timeout);
-  if (ok && down >= 0) ok = wait_ge(&f[down].ack, n, t0, timeout);
-  if (!ok) store_sys(&f[me].err, 2u);
+  if (up_mb) ok = wait_ge(&mine->ack_up, n, t0, timeout);
+  if (ok && down_mb) ok = wait_ge(&mine->ack_down, n, t0, timeout);
+  if (!ok) store_sys(err, 2u);
 }
 
 // Copy of `n16` 16-byte granules per side by `nthreads` threads starting
@@ -88,105 +94,80 @@ __device__ __forceinline__ void pull_rows(uint4* __restrict__ dst_up, const uint
 }
 
 // Grid form: G workgroups, ONE dispatch.  `count` changes only at the very
-// end of an exchange (by its last workgroup), so every workgroup of this
-// dispatch reads the same exchange number n = count + 1 at its start (the
-// previous exchange's dispatch completed before this one started: stream
-// order).  Workgroup 0 publishes level = n (this rank's rows came from
-// earlier kernels, released at their end).  Every workgroup's thread 0 waits
-// for the neighbours' level >= n with its OWN system-scope acquire, which
+// end of an exchange (by its last workgroup), so every workgroup reads the
+// same exchange number n = count + 1 (the previous exchange's dispatch
+// completed before this one started: stream order).  Workgroup 0 publishes;
+// every workgroup's thread 0 waits with its OWN system-scope acquire, which
 // invalidates the caches of its CU and XCD before the workgroup loads the
-// neighbours' rows (one acquire per workgroup: a workgroup on another XCD
-// is not covered by anyone else's).  After its slice the workgroup arrives
-// on a device-memory counter; the last one resets it, publishes count = n
-// and ack = n (system-scope release) and waits for the neighbours' acks, so
-// the dispatch ends only once they have copied this rank's rows.
-__global__ __launch_bounds__(256) void k_ipc_exchange_grid(IpcFlags* f, uint32_t* arrive, int me, int up, int down,
-                                                           uint64_t timeout, uint4* __restrict__ dst_up,
-                                                           const uint4* __restrict__ src_up,
+// neighbours' rows (a workgroup on another XCD is covered by no one else's
+// acquire); after its slice the workgroup arrives on the mailbox's counter
+// and the last one resets it and performs the ack.
+__global__ __launch_bounds__(256) void k_ipc_exchange_grid(IpcMailbox* mine, IpcMailbox* up_mb, IpcMailbox* down_mb,
+                                                           uint32_t* err, uint64_t timeout,
+                                                           uint4* __restrict__ dst_up, const uint4* __restrict__ src_up,
                                                            uint4* __restrict__ dst_down,
                                                            const uint4* __restrict__ src_down, int64_t n16) {
   __shared__ int ok_s;
+  __shared__ uint32_t n_s;
   if (threadIdx.x == 0) {
-    const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
-    const uint32_t n = load_sys(&f[me].count) + 1;
-    if (blockIdx.x == 0) store_sys(&f[me].level, n);
-    bool ok = true;
-    if (up >= 0) ok = wait_ge(&f[up].level, n, t0, timeout);
-    if (ok && down >= 0) ok = wait_ge(&f[down].level, n, t0, timeout);
-    if (!ok) store_sys(&f[me].err, 1u);
+    const uint32_t n = __hip_atomic_load(&mine->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    const bool ok = signal_wait(mine, up_mb, down_mb, n, blockIdx.x == 0, timeout);
+    if (!ok) store_sys(err, 1u);
     ok_s = ok;
+    n_s = n;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the acquire's invalidate, before the barrier
   }
   __syncthreads();
   if (ok_s)
-    pull_rows(dst_up, src_up, dst_down, src_down, n16,
-              static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
+    pull_rows(dst_up, src_up, dst_down, src_down, n16, static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
               static_cast<int64_t>(gridDim.x) * blockDim.x);
   __syncthreads();  // every load of this workgroup has returned
   if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t prev = __hip_atomic_fetch_add(&mine->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (prev + 1 == gridDim.x) {
-      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
-      const uint32_t n = load_sys(&f[me].count) + 1;
-      store_sys(&f[me].count, n);
-      // a timed-out level wait: no ack (the neighbours' ack waits time out too)
-      if (__hip_atomic_load(&f[me].err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
-        store_sys(&f[me].ack, n);
-        bool ok = true;
-        if (up >= 0) ok = wait_ge(&f[up].ack, n, t0, timeout);
-        if (ok && down >= 0) ok = wait_ge(&f[down].ack, n, t0, timeout);
-        if (!ok) store_sys(&f[me].err, 2u);
-      }
+      __hip_atomic_store(&mine->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ack_wait(mine, up_mb, down_mb, err, n_s, timeout);
     }
   }
 }
 
-// Single form: the whole exchange as ONE dispatch (one workgroup): thread 0 publishes and
-// waits for the neighbours' rows, the workgroup pulls them, thread 0
-// publishes "copied" and waits for the neighbours' copies.  The rows a
-// neighbour pulls were produced by an EARLIER kernel of its stream (the
-// command processor's end-of-kernel release wrote them back on every XCD);
-// this kernel's system-scope acquire (thread 0, before the barrier)
-// invalidates this CU's caches before any thread loads them.  Three
-// dispatches (signal / pull / ack) cost ~14 us more per exchange on the
-// 8-way proxy (profiles/r04/slots_b/).
-__global__ __launch_bounds__(1024) void k_ipc_exchange(IpcFlags* f, int me, int up, int down, uint64_t timeout,
-                                                       uint4* __restrict__ dst_up, const uint4* __restrict__ src_up,
-                                                       uint4* __restrict__ dst_down,
+// Single form: the whole exchange in ONE workgroup.
+__global__ __launch_bounds__(1024) void k_ipc_exchange(IpcMailbox* mine, IpcMailbox* up_mb, IpcMailbox* down_mb,
+                                                       uint32_t* err, uint64_t timeout, uint4* __restrict__ dst_up,
+                                                       const uint4* __restrict__ src_up, uint4* __restrict__ dst_down,
                                                        const uint4* __restrict__ src_down, int64_t n16) {
   __shared__ int ok_s;
+  __shared__ uint32_t n_s;
   if (threadIdx.x == 0) {
-    const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
-    const uint32_t n = load_sys(&f[me].count) + 1;
-    store_sys(&f[me].count, n);
-    store_sys(&f[me].level, n);
-    bool ok = true;
-    if (up >= 0) ok = wait_ge(&f[up].level, n, t0, timeout);
-    if (ok && down >= 0) ok = wait_ge(&f[down].level, n, t0, timeout);
-    if (!ok) store_sys(&f[me].err, 1u);
+    const uint32_t n = __hip_atomic_load(&mine->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    const bool ok = signal_wait(mine, up_mb, down_mb, n, true, timeout);
+    if (!ok) store_sys(err, 1u);
     ok_s = ok;
+    n_s = n;
     // the acquire's cache invalidate completes asynchronously: wait for it
     // before the barrier releases the other waves' loads of the neighbours'
     // rows (CDNA4 guide, Guideline 16)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  if (!ok_s) return;  // a neighbour may be gone: do not touch its frames
-  for (int64_t i = threadIdx.x; i < n16; i += blockDim.x) {
-    if (src_up) dst_up[i] = src_up[i];
-    if (src_down) dst_down[i] = src_down[i];
-  }
+  if (ok_s) pull_rows(dst_up, src_up, dst_down, src_down, n16, threadIdx.x, blockDim.x);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
-    const uint32_t n = load_sys(&f[me].count);
-    store_sys(&f[me].ack, n);
-    bool ok = true;
-    if (up >= 0) ok = wait_ge(&f[up].ack, n, t0, timeout);
-    if (ok && down >= 0) ok = wait_ge(&f[down].ack, n, t0, timeout);
-    if (!ok) store_sys(&f[me].err, 2u);
-  }
+  if (threadIdx.x == 0) ack_wait(mine, up_mb, down_mb, err, n_s, timeout);
+}
+
+// Sdma form: one thread before and one after the SDMA copies.
+__global__ __launch_bounds__(64) void k_ipc_signal_wait(IpcMailbox* mine, IpcMailbox* up_mb, IpcMailbox* down_mb,
+                                                        uint32_t* err, uint64_t timeout) {
+  if (threadIdx.x != 0) return;
+  const uint32_t n = __hip_atomic_load(&mine->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  if (!signal_wait(mine, up_mb, down_mb, n, true, timeout)) store_sys(err, 1u);
+}
+
+__global__ __launch_bounds__(64) void k_ipc_ack_wait(IpcMailbox* mine, IpcMailbox* up_mb, IpcMailbox* down_mb,
+                                                     uint32_t* err, uint64_t timeout) {
+  if (threadIdx.x != 0) return;
+  const uint32_t n = __hip_atomic_load(&mine->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  ack_wait(mine, up_mb, down_mb, err, n, timeout);
 }
 
 }  // namespace
@@ -196,13 +177,15 @@ int ipc_grid_workgroups(int64_t bytes) {
   return static_cast<int>(std::min<int64_t>(64, std::max<int64_t>(8, (bytes / 16 + 511) / 512)));
 }
 
-void launch_ipc_exchange(IpcPull form, IpcFlags* f, uint32_t* arrive, int me, int up, int down, uint64_t timeout,
-                         uint8_t* dst_up, const uint8_t* src_up, uint8_t* dst_down, const uint8_t* src_down,
-                         int64_t bytes, hipStream_t s, int workgroups) {
+void launch_ipc_exchange(IpcPull form, IpcMailbox* mine, IpcMailbox* up_mb, IpcMailbox* down_mb, uint32_t* err,
+                         uint64_t timeout, uint8_t* dst_up, const uint8_t* src_up, uint8_t* dst_down,
+                         const uint8_t* src_down, int64_t bytes, hipStream_t s, int workgroups) {
+  PCONV_CHECK(mine != nullptr && err != nullptr, "ipc exchange: no mailbox / error word");
   PCONV_CHECK(bytes % 16 == 0, "ipc exchange: rows must span whole 16-byte granules");
   for (const void* p : {static_cast<const void*>(dst_up), static_cast<const void*>(src_up),
                         static_cast<const void*>(dst_down), static_cast<const void*>(src_down)})
     PCONV_CHECK(reinterpret_cast<uintptr_t>(p) % 16 == 0, "ipc exchange: unaligned row pointer");
+  PCONV_CHECK(!src_up == !up_mb && !src_down == !down_mb, "ipc exchange: rows without a mailbox (or the reverse)");
   PCONV_CHECK((!src_up || dst_up) && (!src_down || dst_down), "ipc exchange: source without destination");
   auto* du = reinterpret_cast<uint4*>(dst_up);
   auto* dd = reinterpret_cast<uint4*>(dst_down);
@@ -210,21 +193,21 @@ void launch_ipc_exchange(IpcPull form, IpcFlags* f, uint32_t* arrive, int me, in
   const auto* sd = reinterpret_cast<const uint4*>(src_down);
   switch (form) {
     case IpcPull::Grid: {
-      PCONV_CHECK(arrive != nullptr, "ipc exchange: the grid form needs its arrival counter");
       const int g = workgroups > 0 ? std::min(workgroups, 256) : ipc_grid_workgroups(bytes);
-      k_ipc_exchange_grid<<<dim3(g), dim3(256), 0, s>>>(f, arrive, me, up, down, timeout, du, su, dd, sd, bytes / 16);
+      k_ipc_exchange_grid<<<dim3(g), dim3(256), 0, s>>>(mine, up_mb, down_mb, err, timeout, du, su, dd, sd,
+                                                         bytes / 16);
       break;
     }
     case IpcPull::Single:
-      k_ipc_exchange<<<dim3(1), dim3(1024), 0, s>>>(f, me, up, down, timeout, du, su, dd, sd, bytes / 16);
+      k_ipc_exchange<<<dim3(1), dim3(1024), 0, s>>>(mine, up_mb, down_mb, err, timeout, du, su, dd, sd, bytes / 16);
       break;
     case IpcPull::Sdma:
-      k_ipc_signal_wait<<<dim3(1), dim3(64), 0, s>>>(f, me, up, down, timeout);
+      k_ipc_signal_wait<<<dim3(1), dim3(64), 0, s>>>(mine, up_mb, down_mb, err, timeout);
       PCONV_HIP_CHECK(hipGetLastError());
       if (src_up) PCONV_HIP_CHECK(hipMemcpyAsync(dst_up, src_up, static_cast<size_t>(bytes), hipMemcpyDefault, s));
       if (src_down)
         PCONV_HIP_CHECK(hipMemcpyAsync(dst_down, src_down, static_cast<size_t>(bytes), hipMemcpyDefault, s));
-      k_ipc_ack_wait<<<dim3(1), dim3(64), 0, s>>>(f, me, up, down, timeout);
+      k_ipc_ack_wait<<<dim3(1), dim3(64), 0, s>>>(mine, up_mb, down_mb, err, timeout);
       break;
   }
   PCONV_HIP_CHECK(hipGetLastError());

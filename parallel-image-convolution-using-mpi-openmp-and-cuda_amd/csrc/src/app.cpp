@@ -547,7 +547,7 @@ struct SharedState {
   char error[512];
   // --transport ipc: every rank's frame handles (hipIpcMemHandle_t x 2) and
   // the flag segment's name
-  uint8_t ipc_handles[kMaxRanks][2 * sizeof(hipIpcMemHandle_t)];
+  uint8_t ipc_handles[kMaxRanks][kIpcHandleBytes];
   char ipc_segment[64];
 };
 

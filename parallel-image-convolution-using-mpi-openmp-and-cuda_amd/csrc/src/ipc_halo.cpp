@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstddef>
 #include <cstring>
 
 #include "pconv/trace.hpp"
@@ -79,15 +80,17 @@ IpcHaloTransport::IpcHaloTransport(BandEngine& e, const std::string& segment, in
   int khz = 0;
   PCONV_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e.options().device));
   timeout_ticks_ = static_cast<uint64_t>(timeout_s * static_cast<double>(khz > 0 ? khz : 100000) * 1000.0);
-  if (pull_ == IpcPull::Grid) {
-    arrive_ = DeviceBuffer(64);
-    PCONV_HIP_CHECK(hipMemset(arrive_.data(), 0, arrive_.size()));
-  }
-  handles_.resize(2 * sizeof(hipIpcMemHandle_t));
-  for (int i = 0; i < 2; ++i) {
+  // A whole 2 MiB allocation (never sub-allocated by the runtime) so that
+  // its IPC handle names exactly this buffer.
+  mail_ = DeviceBuffer(size_t(2) << 20);
+  PCONV_HIP_CHECK(hipMemset(mail_.data(), 0, sizeof(IpcMailbox)));
+  PCONV_HIP_CHECK(hipDeviceSynchronize());  // zeroed before any neighbour can store into it
+  handles_.resize(kIpcHandleBytes);
+  for (int i = 0; i < 3; ++i) {
     hipIpcMemHandle_t h;
-    own_base_[i] = e.frame_base(i);
-    PCONV_HIP_CHECK(hipIpcGetMemHandle(&h, own_base_[i]));
+    void* base = i < 2 ? static_cast<void*>(e.frame_base(i)) : static_cast<void*>(mail_.data());
+    if (i < 2) own_base_[i] = e.frame_base(i);
+    PCONV_HIP_CHECK(hipIpcGetMemHandle(&h, base));
     std::memcpy(handles_.data() + i * sizeof(h), &h, sizeof(h));
   }
 }
@@ -96,6 +99,8 @@ IpcHaloTransport::~IpcHaloTransport() {
   for (uint8_t** side : {peer_up_, peer_down_})
     for (int i = 0; i < 2; ++i)
       if (side[i] && side[i] != own_base_[i]) (void)hipIpcCloseMemHandle(side[i]);
+  for (IpcMailbox* m : {peer_mail_up_, peer_mail_down_})
+    if (m && m != static_cast<void*>(mail_.data())) (void)hipIpcCloseMemHandle(m);
   if (host_ && host_ != MAP_FAILED) {
     (void)hipHostUnregister(host_);
     ::munmap(host_, seg_bytes_);
@@ -106,33 +111,37 @@ void IpcHaloTransport::connect(const std::vector<uint8_t>& up_handles, const std
   PCONV_CHECK(!connected_, "ipc transport: already connected");
   const Band& b = eng_->band();
   const FrameLayout& L = eng_->layout();
-  auto open = [&](const std::vector<uint8_t>& hs, uint8_t** out) {
-    PCONV_CHECK(hs.size() == 2 * sizeof(hipIpcMemHandle_t), "ipc transport: bad handle blob");
+  auto open = [&](const std::vector<uint8_t>& hs, uint8_t** out, IpcMailbox** mail) {
+    PCONV_CHECK(hs.size() == kIpcHandleBytes, "ipc transport: bad handle blob");
     if (hs == handles_) {
       // This engine is its own neighbour (one-process emulation of a rank
       // whose halos move: the band's own rows come back as its ghost rows,
       // like RCCL send/recv to self).  A process cannot open its own handle.
       for (int i = 0; i < 2; ++i) out[i] = own_base_[i];
+      *mail = reinterpret_cast<IpcMailbox*>(mail_.data());
       own_ = true;
       return;
     }
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
       hipIpcMemHandle_t h;
       std::memcpy(&h, hs.data() + i * sizeof(h), sizeof(h));
       void* p = nullptr;
       PCONV_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-      out[i] = static_cast<uint8_t*>(p);
+      if (i < 2)
+        out[i] = static_cast<uint8_t*>(p);
+      else
+        *mail = static_cast<IpcMailbox*>(p);
     }
   };
   if (b.up >= 0) {
     PCONV_CHECK(!up_handles.empty(), "ipc transport: band has an upper neighbour but no handles");
-    open(up_handles, peer_up_);
+    open(up_handles, peer_up_, &peer_mail_up_);
     lay_up_ = FrameLayout::make(L.row_bytes, row_band(eng_->geom().height, world_, b.up).rows, L.halo);
     PCONV_CHECK(lay_up_.pitch == L.pitch, "ipc transport: neighbour pitch differs");
   }
   if (b.down >= 0) {
     PCONV_CHECK(!down_handles.empty(), "ipc transport: band has a lower neighbour but no handles");
-    open(down_handles, peer_down_);
+    open(down_handles, peer_down_, &peer_mail_down_);
     lay_down_ = FrameLayout::make(L.row_bytes, row_band(eng_->geom().height, world_, b.down).rows, L.halo);
     PCONV_CHECK(lay_down_.pitch == L.pitch, "ipc transport: neighbour pitch differs");
   }
@@ -158,14 +167,18 @@ void IpcHaloTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream
   const uint8_t* src_down = down >= 0 ? peer_down_[par] + lay_down_.offset(0) - kPadLeft : nullptr;
   uint8_t* dst_up = up >= 0 ? mine + L.offset(-depth) - kPadLeft : nullptr;
   uint8_t* dst_down = down >= 0 ? mine + L.offset(b.rows) - kPadLeft : nullptr;
-  launch_ipc_exchange(pull_, dflags_, reinterpret_cast<uint32_t*>(arrive_.data()), me, up, down, timeout_ticks_,
-                      dst_up, src_up, dst_down, src_down, static_cast<int64_t>(n), stream);
+  (void)up;
+  (void)down;
+  launch_ipc_exchange(pull_, reinterpret_cast<IpcMailbox*>(mail_.data()), up >= 0 ? peer_mail_up_ : nullptr,
+                      down >= 0 ? peer_mail_down_ : nullptr, &dflags_[me].err, timeout_ticks_, dst_up, src_up,
+                      dst_down, src_down, static_cast<int64_t>(n), stream);
   ++enqueued_;
 }
 
 uint32_t IpcHaloTransport::device_count() const {
-  const auto* f = static_cast<const volatile IpcFlags*>(host_);
-  return f[rank_ * slots_ + slot_].count;
+  uint32_t v = 0;
+  PCONV_HIP_CHECK(hipMemcpy(&v, mail_.data() + offsetof(IpcMailbox, count), sizeof(v), hipMemcpyDeviceToHost));
+  return v;
 }
 
 void IpcHaloTransport::check() const {
@@ -185,8 +198,8 @@ double ipc_pull_probe(const std::string& form, int64_t bytes, bool host_source, 
   PCONV_CHECK(bytes > 0 && bytes % 16 == 0 && iters >= 1, "ipc_pull_probe: bytes must be a positive multiple of 16");
   const IpcPull p = parse_ipc_pull(form);
   set_device(device);
-  // the flag block in coherent (fine-grained) mapped host memory, like the
-  // shared segment the transport registers
+  // the error word in coherent (fine-grained) mapped host memory, like the
+  // shared segment the transport registers; the mailbox in device memory
   void* fh = nullptr;
   PCONV_HIP_CHECK(hipHostMalloc(&fh, sizeof(IpcFlags), hipHostMallocCoherent | hipHostMallocMapped));
   struct FreeHost {
@@ -196,8 +209,8 @@ double ipc_pull_probe(const std::string& form, int64_t bytes, bool host_source, 
   std::memset(fh, 0, sizeof(IpcFlags));
   void* fd = nullptr;
   PCONV_HIP_CHECK(hipHostGetDevicePointer(&fd, fh, 0));
-  DeviceBuffer arrive(64), dst(static_cast<size_t>(2 * bytes));
-  PCONV_HIP_CHECK(hipMemset(arrive.data(), 0, arrive.size()));
+  DeviceBuffer mail(sizeof(IpcMailbox)), dst(static_cast<size_t>(2 * bytes));
+  PCONV_HIP_CHECK(hipMemset(mail.data(), 0, mail.size()));
   PinnedBuffer hsrc;
   DeviceBuffer dsrc;
   uint8_t* src = nullptr;
@@ -216,10 +229,10 @@ double ipc_pull_probe(const std::string& form, int64_t bytes, bool host_source, 
   PCONV_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
   const uint64_t timeout = static_cast<uint64_t>(5.0 * static_cast<double>(khz > 0 ? khz : 100000) * 1000.0);
   Stream st = Stream::create(0);
-  auto* f = static_cast<IpcFlags*>(fd);
-  auto* arr = reinterpret_cast<uint32_t*>(arrive.data());
+  auto* err = &static_cast<IpcFlags*>(fd)->err;
+  auto* mb = reinterpret_cast<IpcMailbox*>(mail.data());
   auto one = [&] {
-    launch_ipc_exchange(p, f, arr, 0, 0, 0, timeout, dst.data(), src + bytes, dst.data() + bytes, src, bytes,
+    launch_ipc_exchange(p, mb, mb, mb, err, timeout, dst.data(), src + bytes, dst.data() + bytes, src, bytes,
                         st.get(), workgroups);
   };
   for (int i = 0; i < 3; ++i) one();
@@ -231,7 +244,9 @@ double ipc_pull_probe(const std::string& form, int64_t bytes, bool host_source, 
   PCONV_HIP_CHECK(hipStreamSynchronize(st.get()));
   const auto* fl = reinterpret_cast<const volatile IpcFlags*>(fh);
   PCONV_CHECK(fl->err == 0, "ipc_pull_probe: a self-neighbour wait timed out");
-  PCONV_CHECK(fl->count == static_cast<uint32_t>(iters + 3), "ipc_pull_probe: exchange count mismatch");
+  uint32_t count = 0;
+  PCONV_HIP_CHECK(hipMemcpy(&count, mail.data() + offsetof(IpcMailbox, count), sizeof(count), hipMemcpyDeviceToHost));
+  PCONV_CHECK(count == static_cast<uint32_t>(iters + 3), "ipc_pull_probe: exchange count mismatch");
   std::vector<uint8_t> back(static_cast<size_t>(2 * bytes));
   PCONV_HIP_CHECK(hipMemcpy(back.data(), dst.data(), back.size(), hipMemcpyDeviceToHost));
   for (uint8_t v : back) PCONV_CHECK(v == 0x5a, "ipc_pull_probe: pulled bytes differ from the source");
