@@ -169,7 +169,11 @@ void IpcHaloTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream
   uint8_t* dst_down = down >= 0 ? mine + L.offset(b.rows) - kPadLeft : nullptr;
   (void)up;
   (void)down;
-  launch_ipc_exchange(pull_, reinterpret_cast<IpcMailbox*>(mail_.data()), up >= 0 ? peer_mail_up_ : nullptr,
+  // A self-neighbour (one-process emulation) copies within its own frame
+  // allocations, which the runtime refuses as a captured SDMA copy: the grid
+  // form pulls instead.
+  const IpcPull form = pull_ == IpcPull::Sdma && own_ ? IpcPull::Grid : pull_;
+  launch_ipc_exchange(form, reinterpret_cast<IpcMailbox*>(mail_.data()), up >= 0 ? peer_mail_up_ : nullptr,
                       down >= 0 ? peer_mail_down_ : nullptr, &dflags_[me].err, timeout_ticks_, dst_up, src_up,
                       dst_down, src_down, static_cast<int64_t>(n), stream);
   ++enqueued_;
