@@ -135,7 +135,8 @@ def parse():
                         "every rank exits with the line as it stands printed (default modes x (timeout + 10) + 30)")
     p.add_argument("--stall-exchange", action="store_true", help=argparse.SUPPRESS)  # tests: a hung peer
     p.add_argument("--hw-queues", type=int, default=0,
-                   help="GPU_MAX_HW_QUEUES for this process (default: max(8, slots + 3))")
+                   help="GPU_MAX_HW_QUEUES for this process (default: 4 with CU-masked slot queues, else "
+                        "max(8, slots + 3))")
     p.add_argument("--trace", type=int, default=0, metavar="IMAGES",
                    help="after the timed region, time the stages of IMAGES more images (needs a directly issued "
                         "pipeline: --graph-capture off or --step-graphs off) and write them to --trace-out")
@@ -389,6 +390,22 @@ def copy_floor_ms(in_bytes: int, out_bytes: int, device: int, iters: int = 8):
     return h2d, d2h
 
 
+def hw_queue_budget(a) -> int:
+    """GPU_MAX_HW_QUEUES for this process.  With CU-masked slot streams (the
+    default) every image slot has its own dedicated hardware queue outside
+    the runtime's pool, and the pool keeps the runtime's default of 4:
+    measured on one box, 6 interleaved pairs of the driver's 20-image
+    command, 4 pool queues 0.335-0.349 ms per step (mean 0.342) against
+    0.346-0.355 (0.350) with 8 (profiles/r05/c/).  Pool slot streams
+    (--pool-queues) get one queue per stream of the pipeline (H2D, D2H, comm
+    and one per slot) so independent streams never alias a queue.
+    N > 1 (and the per-rank proxy) keeps the larger pool: its halo modes
+    run event-ordered pipelines on pool streams (H2D, D2H, comm, compute)."""
+    if a.hw_queues:
+        return a.hw_queues
+    return 4 if a.cu_mask_queues and a.gpus == 1 and not a.emulate else max(8, a.slots + 3)
+
+
 def run_native(a) -> int:
     """`bench.py --native`: the serving step of the `conv` binary (C++ fork
     launcher + BandPipeline on the HIP runtime it links) instead of this
@@ -415,7 +432,7 @@ def run_native(a) -> int:
         cmd[cmd.index("--gpus") + 1] = "1"
         cmd += ["--emulate", a.emulate]  # one rank of a WORLD-way split, alone (per-rank proxy)
     env = dict(os.environ)
-    want = a.hw_queues if a.hw_queues else max(8, a.slots + 3)  # as for the torch pipeline below
+    want = hw_queue_budget(a)  # as for the torch pipeline below
     if a.hw_queues or int(env.get("GPU_MAX_HW_QUEUES", "4")) < want:
         env["GPU_MAX_HW_QUEUES"] = str(min(want, 32))
     r = subprocess.run(cmd, capture_output=True, text=True, env=env)
@@ -436,10 +453,9 @@ def main():
         sys.exit(run_native(a))
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not a.emulate:
         sys.exit(spawn_ranks(a))
-    # One hardware queue per stream of the serving pipeline (H2D, D2H, comm and
-    # one compute stream per image in flight) so independent streams never
-    # alias a queue; must be set before the HIP runtime initialises.
-    want = a.hw_queues if a.hw_queues else max(8, a.slots + 3)
+    # The runtime's hardware-queue pool (must be set before the HIP runtime
+    # initialises): see hw_queue_budget.
+    want = hw_queue_budget(a)
     if a.hw_queues or int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < want:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(want, 32))
     import torch
