@@ -108,6 +108,9 @@ def parse():
                         "them, download finished rows meanwhile (H2D, reps and D2H of ONE image overlap; 0 = off). "
                         "With step graphs only an image submitted to an idle pipeline is streamed (the head of a "
                         "burst, every single image: latency_ms 0.56 vs 0.69 ms whole-image, profiles/r04/head/)")
+    p.add_argument("--stream-min-mb", type=float, default=0.0,
+                   help="head-stream only images of at least this many MB of input (small bands: the hand-offs "
+                        "of a streamed image cost more than they hide)")
     p.add_argument("--emulate", default=None, metavar="WORLD:RANK",
                    help="time ONE rank of a WORLD-way split on this GPU (pre-loaded halos, no peers): a "
                         "single-GPU proxy of the per-rank step; reported as emulated, never as the headline")
@@ -507,7 +510,7 @@ def main():
                                transport=head_transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
                                step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
                                graph_capture=a.graph_capture == "on", stream_chunks=a.stream_chunks,
-                               **policy_kwargs(a))
+                               stream_min_bytes=int(a.stream_min_mb * 2 ** 20), **policy_kwargs(a))
     blur.load_synthetic(a.seed)
     # --emulate-rccl: hold a (1-rank) RCCL communicator through the timed
     # region, as every real N>1 rank of the exchange path does.
@@ -640,6 +643,7 @@ def main():
                 "halo_depth": int(blur.engine.halo),
                 "fuse": int(blur.engine.fuse),
                 "stream_chunks": int(a.stream_chunks),
+                "stream_min_mb": a.stream_min_mb,
                 "preload_halo": bool(blur.preload_halo),
                 "launches_per_step": int(stats.launches),
                 "exchanges_per_step": int(stats.exchanges),

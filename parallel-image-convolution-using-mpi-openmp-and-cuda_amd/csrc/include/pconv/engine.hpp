@@ -74,6 +74,11 @@ struct EngineOptions {
   // fork/join branches it measured 1.4-4.3x slower per image
   // (profiles/r04/stream_a/).
   int stream_chunks = 0;
+  // Head streaming only for images of at least this many input bytes: the
+  // cross-stream hand-offs of a streamed image cost more than they hide on
+  // small bands (the 8-way band of the headline: 0.27 ms streamed vs 0.15
+  // ms as one graph, profiles/r05/b/e8*.json).
+  int64_t stream_min_bytes = 0;
   // ---- serving-pipeline policy (BandPipeline, slot-stream mode) ----
   // Slot streams on dedicated hardware queues (created with an all-CU mask):
   // from the runtime's shared pool, 4 slot streams landed on queues of which

@@ -643,7 +643,8 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   }
   if (graphs_) {
     PCONV_CHECK(trace_ev_.empty(), "pipeline trace needs directly issued images (graph capture off)");
-    if (idle_ && head_streaming_) {
+    const int64_t in_bytes = (in_r1 - in_r0) * e.layout().row_bytes;
+    if (idle_ && head_streaming_ && in_bytes >= e.options().stream_min_bytes) {
       // Head streaming: nothing is in flight, so this image's rows stream
       // (chunked H2D ‖ launches ‖ D2H of finished rows, schedule.hpp
       // plan_streamed) instead of waiting for its whole upload and its

@@ -574,9 +574,11 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def(py::init([](int64_t w, int64_t h, const std::string& ch, py::object filter, int rank, int world,
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
                        int concurrent, bool graphs, bool step_graphs, py::object band, bool slot_comm,
-                       int stream_chunks, bool cu_mask_queues, bool head_on_slot_streams) {
+                       int stream_chunks, bool cu_mask_queues, bool head_on_slot_streams,
+                       int64_t stream_min_bytes) {
              EngineOptions o;
              o.stream_chunks = stream_chunks;
+             o.stream_min_bytes = stream_min_bytes;
              o.cu_mask_queues = cu_mask_queues;
              o.head_on_slot_streams = head_on_slot_streams;
              o.device = device;
@@ -595,7 +597,8 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("overlap") = true, py::arg("variant") = "auto", py::arg("slots") = 2, py::arg("concurrent") = -1,
            py::arg("graphs") = false, py::arg("step_graphs") = true,
            py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0,
-           py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true)
+           py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true,
+           py::arg("stream_min_bytes") = 0)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -628,6 +631,7 @@ PYBIND11_MODULE(_pconv_native, m) {
                                const EngineOptions& o = p.slot(0).options();
                                py::dict d;
                                d["stream_chunks"] = o.stream_chunks;
+                               d["stream_min_bytes"] = o.stream_min_bytes;
                                d["cu_mask_queues"] = o.cu_mask_queues;
                                d["head_on_slot_streams"] = o.head_on_slot_streams;
                                return d;
