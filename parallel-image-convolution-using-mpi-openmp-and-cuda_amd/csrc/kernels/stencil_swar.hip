@@ -21,7 +21,7 @@
 // lane's register, read as the DPP source (wave_shr/wave_shl) of the add that
 // consumes it.  Per pair per step (swar_device.hpp): 2 v_add_u32 horizontal
 // (pair sums X_j + X_{j+CH}, then P_{k-CH} + P_k), 2 vertical (rolling pair
-// sums), 2 truncation (v_lshrrev, v_and; 1.5 on average in the paired form) —
+// sums), 2 truncation (v_lshrrev, v_and; 1.5 on average in form 1) —
 // no VOP3 in the step, 2*CH of the horizontal adds per row with a DPP
 // operand; the byte shuffles (v_perm) happen only when a tile is loaded and
 // stored (profiles/r03/valu/).
@@ -54,51 +54,42 @@
 namespace pconv {
 namespace {
 
-// The `steps` repetitions of a tile in one of three step forms (the tuner
-// times all three per launch geometry):
+// The `steps` repetitions of a tile in one of two step forms (the tuner
+// times both per launch geometry):
 //   0: one swar_step per repetition, truncating every step;
 //   1: steps in pairs keeping 16 x the truncated value in between (one AND
-//      instead of shift + AND every other step), one barrier per step;
-//   2: as 1 with ONE barrier per pair (swar_step2: two boundary rows per
-//      side exchanged, one ghost row per side recomputed).
-// Forms 1 and 2 cost registers (up to +40 VGPRs on grey tiles).  g_row /
-// height: global row of the wave's register row 0 and the image height
-// (form 2's ghost rows outside the image read as zero).
-template <int CH, int NP, int M, int NW, int FORM, int R>
-__device__ __forceinline__ void run_steps(u32 (&D)[M][NP], uint4 (&lds)[2][NW][R][NP / 4][64], int steps, int w,
-                                          int lane, bool needs_mask, const u32 (&cm)[NP], int out_top, int out_bot,
-                                          int g_row, int height) {
-  if constexpr (FORM == 2) {
-    static_assert(R == 4, "form 2 exchanges two boundary rows per side");
-    const bool ga_out = g_row - 1 < 0 || g_row - 1 >= height;
-    const bool gb_out = g_row + M < 0 || g_row + M >= height;
-    int s = 0;
-    for (; s + 2 <= steps; s += 2)
-      swar_step2<CH, NP, M, NW>(D, lds, (s >> 1) & 1, w, lane, needs_mask, cm, out_top, out_bot, ga_out, gb_out);
-    if (s < steps) swar_step<CH, NP, M, NW, 0, R>(D, lds, (s >> 1) & 1, w, lane, needs_mask, cm, out_top, out_bot);
-  } else if constexpr (FORM == 1) {
+//      instead of shift + AND every other step), one barrier per step.
+// Form 1 costs registers (up to +40 VGPRs on grey tiles).  A third form with
+// ONE barrier per pair of steps (two boundary rows per side exchanged, one
+// ghost row per side recomputed) never won a tuning and forced it measured
+// 0-8 % slower than form 1 (round 5: headline 3.645 vs 3.377 us/rep,
+// 32768^2 grey 113.8 vs 109.2; profiles/r05/d/form_ab.jsonl): removed.
+template <int CH, int NP, int M, int NW, int FORM>
+__device__ __forceinline__ void run_steps(u32 (&D)[M][NP], uint4 (&lds)[2][NW][2][NP / 4][64], int steps, int w,
+                                          int lane, bool needs_mask, const u32 (&cm)[NP], int out_top, int out_bot) {
+  if constexpr (FORM == 1) {
     int s = 0;
     for (; s + 2 <= steps; s += 2) {
-      swar_step<CH, NP, M, NW, 1, R>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
-      swar_step<CH, NP, M, NW, 2, R>(D, lds, 1, w, lane, needs_mask, cm, out_top, out_bot);
+      swar_step<CH, NP, M, NW, 1>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+      swar_step<CH, NP, M, NW, 2>(D, lds, 1, w, lane, needs_mask, cm, out_top, out_bot);
     }
-    if (s < steps) swar_step<CH, NP, M, NW, 0, R>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
+    if (s < steps) swar_step<CH, NP, M, NW, 0>(D, lds, 0, w, lane, needs_mask, cm, out_top, out_bot);
   } else {
     for (int s = 0; s < steps; ++s)
-      swar_step<CH, NP, M, NW, 0, R>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
+      swar_step<CH, NP, M, NW, 0>(D, lds, s & 1, w, lane, needs_mask, cm, out_top, out_bot);
   }
 }
 
 template <int CH, int LW, int M, int NW, int FORM>
 __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                  int64_t pitch, int64_t dst_pitch, int row_bytes, int r0, int r1,
+                                                  int64_t pitch, int row_bytes, int r0, int r1,
                                                   int steps, int g_row0, int height, int nstrips, int pair_stride,
                                                   int row_tiles, int xcd_swizzle) {
   constexpr int NP = LW;       // pairs per row per lane
   constexpr int NQ = NP / 4;   // uint4 per row per lane
   using CT = typename Chunk<NP>::T;
-  // [parity][wave][boundary rows: top, bottom (FORM 2: two each)][quad][lane]
-  __shared__ uint4 lds[2][NW][FORM == 2 ? 4 : 2][NQ][64];
+  // [parity][wave][boundary rows: top, bottom][quad][lane]
+  __shared__ uint4 lds[2][NW][2][NQ][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hl = (steps * CH + LW - 1) / LW;  // halo lanes per side
@@ -145,7 +136,7 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
   const int out_top = min(max(-g_row0 - row_base, 0), M);
   const int out_bot = min(max(height - g_row0 - row_base, 0), M);
 
-  run_steps<CH, NP, M, NW, FORM>(D, lds, steps, w, lane, needs_mask, cm, out_top, out_bot, row_base + g_row0, height);
+  run_steps<CH, NP, M, NW, FORM>(D, lds, steps, w, lane, needs_mask, cm, out_top, out_bot);
 
   const bool lane_in = lane >= hl && lane < 64 - hl;
   const bool stA = lane_in && validA > 0, stB = lane_in && validB > 0;
@@ -156,7 +147,7 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
     if (fr >= st_lo && fr < st_hi) {
       CT a, b;
       pack<NP>(D[i], a, b);
-      uint8_t* rowq = dst + static_cast<int64_t>(fr) * dst_pitch;
+      uint8_t* rowq = dst + static_cast<int64_t>(fr) * pitch;
       // Whole chunks as one store; the row's last partial chunk byte by byte
       // (dst may be a packed host buffer with no pad after the row).
       if (stA) {
@@ -190,12 +181,12 @@ __global__ __launch_bounds__(64 * NW) void k_swar(const uint8_t* __restrict__ sr
 // ranges under 2 GiB.
 template <int CH, int M, int NW, int FORM>
 __global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                     int pitch, int dst_pitch, int row_bytes, int r0, int r1,
+                                                     int pitch, int row_bytes, int r0, int r1,
                                                      int steps, int g_row0, int height, int nstrips, int pair_stride,
                                                      int row_tiles, int xcd_swizzle) {
   constexpr int LW = 4, NP = 4, NQ = 1;
   constexpr u32 kOut = 0x80000000u;  // offset past every descriptor's range
-  __shared__ uint4 lds[2][NW][FORM == 2 ? 4 : 2][NQ][64];
+  __shared__ uint4 lds[2][NW][2][NQ][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hl = (steps * CH + LW - 1) / LW;
@@ -206,8 +197,8 @@ __global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__
   const int st_end = min(r1, height - g_row0);
   const auto srsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(src) + static_cast<int64_t>(lo_ok) * pitch, 0, max(hi_ok - lo_ok, 0) * pitch, 0x00020000);
-  const auto drsrc = __builtin_amdgcn_make_buffer_rsrc(dst + static_cast<int64_t>(r0) * dst_pitch, 0,
-                                                       max(st_end - r0, 0) * dst_pitch, 0x00020000);
+  const auto drsrc = __builtin_amdgcn_make_buffer_rsrc(dst + static_cast<int64_t>(r0) * pitch, 0,
+                                                       max(st_end - r0, 0) * pitch, 0x00020000);
   // XCD-aware tile order (as k_swar): each XCD gets one contiguous run of
   // tiles walked down a column strip, so vertically adjacent tiles (which
   // read each other's halo rows) share an L2.
@@ -241,7 +232,7 @@ __global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__
     cm[k] = (xA >= 0 && xA + k < row_bytes ? 0xffffu : 0u) | (xB >= 0 && xB + k < row_bytes ? 0xffff0000u : 0u);
   const int out_top = min(max(-g_row0 - row_base, 0), M);
   const int out_bot = min(max(height - g_row0 - row_base, 0), M);
-  run_steps<CH, NP, M, NW, FORM>(D, lds, steps, w, lane, needs_mask, cm, out_top, out_bot, row_base + g_row0, height);
+  run_steps<CH, NP, M, NW, FORM>(D, lds, steps, w, lane, needs_mask, cm, out_top, out_bot);
   const bool lane_in = lane >= hl && lane < 64 - hl;
   const int tile_r0 = row_base + steps - w * M;
   const int st_lo = max(tile_r0, r0), st_hi = min(tile_r0 + vrows, st_end);
@@ -249,7 +240,7 @@ __global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__
   for (int i = 0; i < M; ++i) {
     const int fr = row_base + i;
     const bool rst = fr >= st_lo && fr < st_hi;
-    const u32 ro = static_cast<u32>(fr - r0) * static_cast<u32>(dst_pitch);
+    const u32 ro = static_cast<u32>(fr - r0) * static_cast<u32>(pitch);
     u32 a, bb;
     pack<NP>(D[i], a, bb);
     __builtin_amdgcn_raw_buffer_store_b32(a, drsrc, (rst && lane_in && xA >= 0) ? ro + xA : kOut, 0, 0);
@@ -273,7 +264,7 @@ std::atomic<int> g_xcd_swizzle{1};  // XCD-aware tile order (neutral +-2 %, kept
 
 bool xcd_swizzle_enabled() { return g_xcd_swizzle.load(std::memory_order_relaxed) != 0; }
 
-std::atomic<int> g_alt_mode{-1};  // step form: -1 tuned, else forced 0 / 1 / 2 (run_steps)
+std::atomic<int> g_alt_mode{-1};  // step form: -1 tuned, else forced 0 / 1 (run_steps)
 
 int alt_mode() { return g_alt_mode.load(std::memory_order_relaxed); }
 
@@ -281,26 +272,16 @@ int alt_mode() { return g_alt_mode.load(std::memory_order_relaxed); }
 // form is faster in most measured geometries.
 int default_form() { return alt_mode() >= 0 ? alt_mode() : 1; }
 
-// Form 2 needs three register rows per wave and four boundary rows per wave
-// in LDS (64 KB at most: NW x LW/4 <= 8); other shapes run form 1 instead.
-constexpr bool form2_ok(int lw, int m, int nw) { return m >= 3 && nw * (lw / 4) <= 8; }
-
 // Kernel of one step form.
 template <int CH, int LW, int M, int NW>
 auto swar_kernel(int form) {
   using F = decltype(&k_swar<CH, LW, M, NW, 0>);
-  if constexpr (form2_ok(LW, M, NW)) {
-    if (form == 2) return static_cast<F>(&k_swar<CH, LW, M, NW, 2>);
-  }
   return form >= 1 ? static_cast<F>(&k_swar<CH, LW, M, NW, 1>) : static_cast<F>(&k_swar<CH, LW, M, NW, 0>);
 }
 
 template <int CH, int M, int NW>
 auto swar_pf_kernel(int form) {
   using F = decltype(&k_swar_pf<CH, M, NW, 0>);
-  if constexpr (form2_ok(4, M, NW)) {
-    if (form == 2) return static_cast<F>(&k_swar_pf<CH, M, NW, 2>);
-  }
   return form >= 1 ? static_cast<F>(&k_swar_pf<CH, M, NW, 1>) : static_cast<F>(&k_swar_pf<CH, M, NW, 0>);
 }
 
@@ -317,7 +298,7 @@ void launch_one(const StencilLaunch& a, hipStream_t s, int form) {
   const dim3 grid(pair_stride * row_tiles);
   const int64_t hmax = std::min<int64_t>(a.height, int64_t(1) << 30);
   swar_kernel<CH, LW, M, NW>(form)<<<grid, dim3(64 * NW), 0, s>>>(
-      a.src, a.dst, a.pitch, a.pitch, static_cast<int>(a.row_bytes),
+      a.src, a.dst, a.pitch, static_cast<int>(a.row_bytes),
       static_cast<int>(a.r0), static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), static_cast<int>(hmax), nstrips,
       pair_stride, row_tiles, xcd_swizzle_enabled() ? 1 : 0);
 }
@@ -364,6 +345,9 @@ bool known_pf_shape(const SwarShape& s) {
 }
 
 std::atomic<int> g_pf_mode{-1};  // -1 tune, 0 off, 1 forced
+std::atomic<int> g_stream_mode{-1};  // -1 tune, 0 off, 1 forced chained, 2 forced skewed
+
+int stream_mode() { return g_stream_mode.load(std::memory_order_relaxed); }
 
 int pf_mode() { return g_pf_mode.load(std::memory_order_relaxed); }
 
@@ -390,9 +374,8 @@ void launch_pf_one(const StencilLaunch& a, hipStream_t s, int form) {
   const int grid = static_cast<int>(ntiles);
   const int xs = xcd_swizzle_enabled() ? 1 : 0;
   const int hmax = static_cast<int>(std::min<int64_t>(a.height, int64_t(1) << 30));
-  const int dp = static_cast<int>(a.pitch);
   swar_pf_kernel<CH, M, NW>(form)<<<dim3(grid), dim3(64 * NW), 0, s>>>(
-      a.src, a.dst, static_cast<int>(a.pitch), dp, static_cast<int>(a.row_bytes), static_cast<int>(a.r0),
+      a.src, a.dst, static_cast<int>(a.pitch), static_cast<int>(a.row_bytes), static_cast<int>(a.r0),
       static_cast<int>(a.r1), steps, static_cast<int>(a.g_row0), hmax, nstrips, pair_stride, row_tiles, xs);
 }
 
@@ -530,7 +513,8 @@ KernelRes kernel_res(SwarShape sh, int ch, int form) {
 // tools/fit_swar_data.py + tools/fit_swar_model.py); they pick the measured
 // best shape in 6 of 6 configurations of the current kernel.
 void set_xcd_swizzle(bool on) { g_xcd_swizzle.store(on ? 1 : 0, std::memory_order_relaxed); }
-void set_swar_alt(int mode) { g_alt_mode.store(mode < 0 ? -1 : std::min(mode, 2), std::memory_order_relaxed); }
+void set_swar_alt(int mode) { g_alt_mode.store(mode < 0 ? -1 : std::min(mode, 1), std::memory_order_relaxed); }
+void set_stream_mode(int mode) { g_stream_mode.store(mode < 0 ? -1 : std::min(mode, 2), std::memory_order_relaxed); }
 void set_prefetch_mode(int mode) { g_pf_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
 std::vector<SwarShape> swar_prefetch_shapes() { return std::vector<SwarShape>(std::begin(kPfShapes), std::end(kPfShapes)); }
 
@@ -588,11 +572,15 @@ namespace {
 struct SwarChoice {
   SwarShape shape;
   int form = 1;  // step form of run_steps
-  bool pf = false;  // buffer-op tile kernel (k_swar_pf)
+  int kern = 0;  // 0 tile kernel k_swar, 1 buffer-op k_swar_pf, 2 / 3 row-streaming chained / skewed
 };
 
 void launch_choice(const StencilLaunch& a, Channels ch, hipStream_t stream, SwarChoice c) {
-  if (c.pf) {
+  if (c.kern >= 2) {
+    launch_swar_stream(a, channel_count(ch), c.kern == 3, xcd_swizzle_enabled(), stream);
+    return;
+  }
+  if (c.kern == 1) {
     switch (ch) {
       case Channels::Grey: launch_pf_ch<1>(a, stream, c.shape, c.form); break;
       case Channels::Rgb: launch_pf_ch<3>(a, stream, c.shape, c.form); break;
@@ -640,6 +628,10 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   const int mode = alt_mode();
   SwarChoice fallback;
   fallback.form = default_form();
+  if (stream_mode() > 0 && swar_stream_ok(a, c)) {  // forced row-streaming kernel (tests, A/B)
+    fallback.kern = stream_mode() + 1;
+    return fallback;
+  }
   if (pf_mode() == 1 && pf_launch_ok(a, a.steps) && (override_shape(fallback.shape) || !autotune_enabled())) {
     // forced prefetch kernel, untuned: the overridden shape if it has a
     // prefetch instantiation, else the first prefetch shape that runs
@@ -653,7 +645,7 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
         }
     }
     if (fallback.shape.m > 0) {
-      fallback.pf = true;
+      fallback.kern = 1;
       return fallback;
     }
     fallback.shape = pick_swar_shape(a.steps, c, rows, a.row_bytes);
@@ -687,9 +679,9 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   if (ranked.size() > keep) ranked.resize(keep);
   std::vector<SwarChoice> cands;
   for (const auto& r : ranked)
-    for (int form = 0; form <= 2; ++form)
-      if ((mode < 0 || mode == form) && (form < 2 || form2_ok(r.second.lw, r.second.m, r.second.nw)))
-        cands.push_back(SwarChoice{r.second, form, false});
+    for (int form = 0; form <= 1; ++form)
+      if (mode < 0 || mode == form)
+        cands.push_back(SwarChoice{r.second, form, 0});
   // Buffer-op tile kernel (k_swar_pf, one workgroup per tile) for the
   // model's candidate shapes it instantiates: hardware zero-fill of rows and
   // lanes outside the frame instead of branches (measured 2-6 % faster on RGB
@@ -698,11 +690,20 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
     std::vector<SwarChoice> pfs;
     for (const auto& r : ranked)
       if (known_pf_shape(r.second))
-        for (int form = 0; form <= 2; ++form)
-          if ((mode < 0 || mode == form) && (form < 2 || form2_ok(4, r.second.m, r.second.nw)))
-            pfs.push_back(SwarChoice{r.second, form, true});
+        for (int form = 0; form <= 1; ++form)
+          if (mode < 0 || mode == form)
+            pfs.push_back(SwarChoice{r.second, form, 1});
     if (pf_mode() == 1 && !pfs.empty()) cands.clear();  // forced: only these candidates
     cands.insert(cands.end(), pfs.begin(), pfs.end());
+  }
+  // Row-streaming kernel, both level orders (kernels/stencil_stream.hip): no
+  // vertical halo and no barriers, fewer waves per SIMD (its level states).
+  if (stream_mode() != 0 && pf_mode() != 1 && swar_stream_ok(a, c)) {
+    SwarChoice sc = fallback;
+    sc.kern = 2;
+    cands.push_back(sc);
+    sc.kern = 3;
+    cands.push_back(sc);
   }
   SwarChoice best = cands.front();
   if (cands.size() > 1) {
@@ -754,7 +755,7 @@ std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned() {
   std::vector<std::pair<std::vector<int64_t>, SwarShape>> out;
   for (const auto& kv : g_tuned)
     out.push_back({{kv.first.ch, kv.first.steps, kv.first.rows, kv.first.row_bytes, kv.second.form,
-                    kv.second.pf ? 1 : 0},
+                    kv.second.kern},
                    kv.second.shape});
   return out;
 }

@@ -141,10 +141,10 @@ __device__ __forceinline__ u32 trunc_sum(u32 S) {
   else return (S >> 8) & 0x00ff00ffu;
 }
 
-// lds[parity][wave][R][quad][lane]: slot 0 = the wave's top row, slot R-1
-// its bottom row (R = 2; the two-repetition step below uses R = 4).
-template <int CH, int NP, int M, int NW, int MODE = 0, int R = 2>
-__device__ __forceinline__ void swar_step(u32 (&D)[M][NP], uint4 (&lds)[2][NW][R][NP / 4][64], int par, int w,
+// lds[parity][wave][2][quad][lane]: slot 0 = the wave's top row, slot 1 its
+// bottom row.
+template <int CH, int NP, int M, int NW, int MODE = 0>
+__device__ __forceinline__ void swar_step(u32 (&D)[M][NP], uint4 (&lds)[2][NW][2][NP / 4][64], int par, int w,
                                              int lane, bool needs_mask, const u32 (&cm)[NP], int out_top,
                                              int out_bot) {
   static_assert(M >= 2, "interior-first step needs two register rows per wave");
@@ -152,7 +152,7 @@ __device__ __forceinline__ void swar_step(u32 (&D)[M][NP], uint4 (&lds)[2][NW][R
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     lds[par][w][0][q][lane] = make_uint4(D[0][4 * q], D[0][4 * q + 1], D[0][4 * q + 2], D[0][4 * q + 3]);
-    lds[par][w][R - 1][q][lane] =
+    lds[par][w][1][q][lane] =
         make_uint4(D[M - 1][4 * q], D[M - 1][4 * q + 1], D[M - 1][4 * q + 2], D[M - 1][4 * q + 3]);
   }
   // Vertical [1,2,1] as rolling pair sums S_i = H_i + H_{i+1}; row i is
@@ -186,7 +186,7 @@ __device__ __forceinline__ void swar_step(u32 (&D)[M][NP], uint4 (&lds)[2][NW][R
     u32 A[NP], B[NP];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const uint4 av = lds[par][wa][R - 1][q][lane], bv = lds[par][wb][0][q][lane];
+      const uint4 av = lds[par][wa][1][q][lane], bv = lds[par][wb][0][q][lane];
       A[4 * q] = av.x; A[4 * q + 1] = av.y; A[4 * q + 2] = av.z; A[4 * q + 3] = av.w;
       B[4 * q] = bv.x; B[4 * q + 1] = bv.y; B[4 * q + 2] = bv.z; B[4 * q + 3] = bv.w;
     }
@@ -197,155 +197,6 @@ __device__ __forceinline__ void swar_step(u32 (&D)[M][NP], uint4 (&lds)[2][NW][R
     for (int k = 0; k < NP; ++k) {
       D[0][k] = trunc_sum<MODE>(keep(Ha[k] + H0[k]) + S01[k]);
       D[M - 1][k] = trunc_sum<MODE>(Sc[k] + keep(Hc[k] + Hb[k]));
-    }
-  }
-  if (needs_mask) {
-#pragma unroll
-    for (int i = 0; i < M; ++i)
-#pragma unroll
-      for (int k = 0; k < NP; ++k) D[i][k] &= cm[k];
-  }
-  if (out_top > 0 || out_bot < M) {
-#pragma unroll
-    for (int i = 0; i < M; ++i)
-      if (i < out_top || i >= out_bot)
-#pragma unroll
-        for (int k = 0; k < NP; ++k) D[i][k] = 0;
-  }
-}
-
-template <int NP>
-__device__ __forceinline__ void lds_row(const uint4 (&src)[NP / 4][64], int lane, u32 (&X)[NP]) {
-#pragma unroll
-  for (int q = 0; q < NP / 4; ++q) {
-    const uint4 v = src[q][lane];
-    X[4 * q] = v.x;
-    X[4 * q + 1] = v.y;
-    X[4 * q + 2] = v.z;
-    X[4 * q + 3] = v.w;
-  }
-}
-
-template <int NP>
-__device__ __forceinline__ void lds_put(uint4 (&dst)[NP / 4][64], int lane, const u32 (&X)[NP]) {
-#pragma unroll
-  for (int q = 0; q < NP / 4; ++q) dst[q][lane] = make_uint4(X[4 * q], X[4 * q + 1], X[4 * q + 2], X[4 * q + 3]);
-}
-
-// TWO repetitions with ONE barrier (the paired form's truncations: MODE 1
-// then MODE 2).  Each wave publishes its two top and two bottom rows,
-// computes the first repetition of its interior rows 1..M-2 from its own
-// registers, meets the other waves once, and from the neighbours' two rows
-// per side finishes the first repetition of rows 0 and M-1 AND of one ghost
-// row per side (the neighbour's row next to it, which the second repetition
-// of rows 0 / M-1 reads); the second repetition then runs over all M rows
-// with no exchange.  Two more row computations per wave per pair of steps
-// (~5 % for M = 20) against half the barriers and LDS round trips.
-// ga_out / gb_out: the ghost row above / below lies outside the image (it
-// must read as zero, like every out-of-image row after every step).
-template <int CH, int NP, int M, int NW>
-__device__ __forceinline__ void swar_step2(u32 (&D)[M][NP], uint4 (&lds)[2][NW][4][NP / 4][64], int par, int w,
-                                           int lane, bool needs_mask, const u32 (&cm)[NP], int out_top, int out_bot,
-                                           bool ga_out, bool gb_out) {
-  static_assert(M >= 3, "two-repetition step needs three register rows per wave");
-  lds_put<NP>(lds[par][w][0], lane, D[0]);
-  lds_put<NP>(lds[par][w][1], lane, D[1]);
-  lds_put<NP>(lds[par][w][2], lane, D[M - 2]);
-  lds_put<NP>(lds[par][w][3], lane, D[M - 1]);
-  // first repetition of the interior rows (as swar_step, MODE 1)
-  u32 H0[NP], Hc[NP], S01[NP], Sc[NP];
-  horiz<CH, NP>(D[0], H0);
-  horiz<CH, NP>(D[1], Hc);
-#pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    S01[k] = keep(H0[k] + Hc[k]);
-    Sc[k] = S01[k];
-  }
-#pragma unroll
-  for (int i = 1; i + 1 < M; ++i) {
-    u32 Hn[NP];
-    horiz<CH, NP>(D[i + 1], Hn);
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const u32 Sn = keep(Hc[k] + Hn[k]);
-      D[i][k] = trunc_sum<1>(Sc[k] + Sn);
-      Sc[k] = Sn;
-      Hc[k] = Hn[k];
-    }
-  }
-  // Sc = S_{M-2} (old rows), Hc = H_{M-1}, S01 = S_0, H0 = H_0.
-  __syncthreads();
-  u32 ga[NP], gb[NP];
-  {
-    const int wa = w > 0 ? w - 1 : 0;       // wave 0: tile top halo, value irrelevant
-    const int wb = w < NW - 1 ? w + 1 : w;  // last wave: tile bottom halo
-    u32 X[NP], Ha0[NP], Ha1[NP], Hb0[NP], Hb1[NP];
-    lds_row<NP>(lds[par][wa][2], lane, X);
-    horiz<CH, NP>(X, Ha0);
-    lds_row<NP>(lds[par][wa][3], lane, X);
-    horiz<CH, NP>(X, Ha1);
-    lds_row<NP>(lds[par][wb][0], lane, X);
-    horiz<CH, NP>(X, Hb0);
-    lds_row<NP>(lds[par][wb][1], lane, X);
-    horiz<CH, NP>(X, Hb1);
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const u32 Sm1 = keep(Ha1[k] + H0[k]);       // S_{-1}
-      ga[k] = trunc_sum<1>(keep(Ha0[k] + Ha1[k]) + Sm1);
-      D[0][k] = trunc_sum<1>(Sm1 + S01[k]);
-      const u32 Sl = keep(Hc[k] + Hb0[k]);        // S_{M-1}
-      D[M - 1][k] = trunc_sum<1>(Sc[k] + Sl);
-      gb[k] = trunc_sum<1>(Sl + keep(Hb0[k] + Hb1[k]));
-    }
-  }
-  if (needs_mask) {
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      ga[k] &= cm[k];
-      gb[k] &= cm[k];
-    }
-#pragma unroll
-    for (int i = 0; i < M; ++i)
-#pragma unroll
-      for (int k = 0; k < NP; ++k) D[i][k] &= cm[k];
-  }
-  if (ga_out)
-#pragma unroll
-    for (int k = 0; k < NP; ++k) ga[k] = 0;
-  if (gb_out)
-#pragma unroll
-    for (int k = 0; k < NP; ++k) gb[k] = 0;
-  if (out_top > 0 || out_bot < M) {
-#pragma unroll
-    for (int i = 0; i < M; ++i)
-      if (i < out_top || i >= out_bot)
-#pragma unroll
-        for (int k = 0; k < NP; ++k) D[i][k] = 0;
-  }
-  // second repetition over rows 0..M-1, ghost rows ga (row -1) and gb (row M)
-  {
-    u32 Hp[NP], Hq[NP], Sp[NP];
-    horiz<CH, NP>(ga, Hp);
-    horiz<CH, NP>(D[0], Hq);
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      Sp[k] = keep(Hp[k] + Hq[k]);  // S_{-1}
-      Hp[k] = Hq[k];                 // H_0
-    }
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      u32 Hn[NP];
-      if (i + 1 < M)
-        horiz<CH, NP>(D[i + 1], Hn);
-      else
-        horiz<CH, NP>(gb, Hn);
-#pragma unroll
-      for (int k = 0; k < NP; ++k) {
-        const u32 Sn = keep(Hp[k] + Hn[k]);
-        D[i][k] = trunc_sum<2>(Sp[k] + Sn);
-        Sp[k] = Sn;
-        Hp[k] = Hn[k];
-      }
     }
   }
   if (needs_mask) {

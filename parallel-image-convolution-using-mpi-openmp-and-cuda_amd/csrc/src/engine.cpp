@@ -545,7 +545,8 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
       // head streaming: copy streams for images submitted to an idle pipeline.
       // With >= 3 slots and opt.head_on_slot_streams the head's upload and
       // download run on the next two slots' streams (idle when the pipeline
-      // is): no hardware queue beyond the slots'.  Two more queues from the
+      // is; the download on the slot a burst reaches last): no hardware queue
+      // beyond the slots'.  Two more queues from the
       // runtime's pool made one image 0.77 ms with 4 slots, dedicated
       // (CU-masked) ones 0.85 ms, the slots' streams 0.56 ms
       // (profiles/r04/head/).  Otherwise: two pool streams.
@@ -655,8 +656,13 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
       const StreamPlan sp = e.stream_plan(reps, in_r0, in_r1);
       if (!sp.chunks.empty()) {
         e.set_cur(0);  // like process_graph: the whole input is uploaded, start in frame 0
-        hipStream_t up = head_on_slots_ ? computes_[static_cast<size_t>((k + 1) % slots())].get() : h2d_.get();
-        hipStream_t down = head_on_slots_ ? computes_[static_cast<size_t>((k + 2) % slots())].get() : d2h_.get();
+        // The downloads wait on every chunk's launches, so they go on the
+        // stream of the slot a burst reaches LAST (k - 1): the burst's next
+        // images do not queue behind the head's whole loop.  The uploads are
+        // done early and go on slot k + 1's.
+        const int n = slots();
+        hipStream_t up = head_on_slots_ ? computes_[static_cast<size_t>((k + 1) % n)].get() : h2d_.get();
+        hipStream_t down = head_on_slots_ ? computes_[static_cast<size_t>((k + n - 1) % n)].get() : d2h_.get();
         h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
         h2d_wait_.wait_on(up);
         hipStream_t done = e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down);

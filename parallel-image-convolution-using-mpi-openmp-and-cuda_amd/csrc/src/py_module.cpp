@@ -366,6 +366,9 @@ PYBIND11_MODULE(_pconv_native, m) {
   m.def("set_prefetch_mode", &set_prefetch_mode, py::arg("mode"),
         "Buffer-op tile kernel: -1 tuned against the others (default), 0 never, 1 forced (with a set_swar_shape "
         "shape it instantiates, that shape)");
+  m.def("set_stream_mode", &set_stream_mode, py::arg("mode"),
+        "Row-streaming kernel (stencil_stream.hip): -1 tuned against the tile kernels (default), 0 never, 1 forced "
+        "chained, 2 forced skewed (launches it instantiates: 4 / 8 / 12 steps).");
   m.def("set_tune_candidates", &set_tune_candidates, py::arg("n"),
         "How many of the latency model's best SWAR tile shapes the tuner times (default 6).");
   m.def("set_float_shape", &set_float_shape, py::arg("m") = 0, py::arg("nw") = 0,

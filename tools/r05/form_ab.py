@@ -7,9 +7,10 @@ For each loop (headline 1920x2520 RGB x40, rank 3 of the 8-way split,
 timed with each step form forced on that pick:
   form 0: one barrier per step, truncating every step;
   form 1: steps in pairs with a x16 intermediate (2 barriers per pair);
-  form 2: as 1 with ONE barrier per pair (two boundary rows per side,
-          ghost rows recomputed: swar_step2).
 Prints one JSON line per (loop, form): us per repetition (best of --repeat).
+A third form (ONE barrier per pair: two boundary rows per side, ghost rows
+recomputed) was timed too (profiles/r05/d/form_ab.jsonl), never won, and was
+removed from the kernels; set_swar_alt now clamps to 0 / 1.
 """
 import argparse
 import json
@@ -74,7 +75,7 @@ def main():
         n.set_autotune(False)
         n.set_swar_shape(*s)
         n.set_prefetch_mode(int(k[5]))
-        for form in (0, 1, 2):
+        for form in (0, 1):
             n.set_swar_alt(form)
             us = loop_us(n, which, a.iters if which != "grey32768" else 3, a.repeat)
             print(json.dumps({"loop": which, "form": form, "shape": list(s), "pf": int(k[5]),
