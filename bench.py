@@ -108,9 +108,10 @@ def parse():
                         "them, download finished rows meanwhile (H2D, reps and D2H of ONE image overlap; 0 = off). "
                         "With step graphs only an image submitted to an idle pipeline is streamed (the head of a "
                         "burst, every single image: latency_ms 0.56 vs 0.69 ms whole-image, profiles/r04/head/)")
-    p.add_argument("--stream-min-mb", type=float, default=0.0,
-                   help="head-stream only images of at least this many MB of input (small bands: the hand-offs "
-                        "of a streamed image cost more than they hide)")
+    p.add_argument("--stream-min-mb", type=float, default=8.0,
+                   help="head-stream only images of at least this many MiB of input: below it the hand-offs of a "
+                        "streamed image cost more than they hide (N=4 band 0.32 vs 0.23 ms as one graph, N=8 0.28 "
+                        "vs 0.15; N=1 0.58 vs 0.68: profiles/r05/e/burst.jsonl)")
     p.add_argument("--emulate", default=None, metavar="WORLD:RANK",
                    help="time ONE rank of a WORLD-way split on this GPU (pre-loaded halos, no peers): a "
                         "single-GPU proxy of the per-rank step; reported as emulated, never as the headline")

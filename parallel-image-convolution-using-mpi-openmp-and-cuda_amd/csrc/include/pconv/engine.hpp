@@ -76,9 +76,11 @@ struct EngineOptions {
   int stream_chunks = 0;
   // Head streaming only for images of at least this many input bytes: the
   // cross-stream hand-offs of a streamed image cost more than they hide on
-  // small bands (the 8-way band of the headline: 0.27 ms streamed vs 0.15
-  // ms as one graph, profiles/r05/b/e8*.json).
-  int64_t stream_min_bytes = 0;
+  // smaller ones.  One image of the headline split N ways, streamed vs one
+  // step graph (profiles/r05/e/burst.jsonl): N=1 14.5 MB 0.58 vs 0.68 ms,
+  // N=2 7.5 MB 0.385 vs 0.387, N=4 4.1 MB 0.32 vs 0.23, N=8 2.3 MB 0.28 vs
+  // 0.15 — so 8 MiB.
+  int64_t stream_min_bytes = int64_t(8) << 20;
   // ---- serving-pipeline policy (BandPipeline, slot-stream mode) ----
   // Slot streams on dedicated hardware queues (created with an all-CU mask):
   // from the runtime's shared pool, 4 slot streams landed on queues of which
@@ -275,6 +277,9 @@ class BandPipeline {
   void submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps);
   void drain();
   int64_t submitted() const { return count_; }
+  // Images head-streamed so far (submitted to an idle pipeline, at least
+  // EngineOptions::stream_min_bytes of input).
+  int64_t streamed_heads() const { return streamed_heads_; }
   // True when slots run their repetitions on separate compute streams.
   bool concurrent() const { return concurrent_; }
   bool graphs() const { return graphs_; }
@@ -299,6 +304,7 @@ class BandPipeline {
   // step-graph mode with stream_chunks > 1: images submitted while nothing is
   // in flight (after construction / drain) are row-streamed (head streaming)
   bool idle_ = true;
+  int64_t streamed_heads_ = 0;
   bool head_streaming_ = false;  // stream_chunks > 1 with step graphs
   bool head_on_slots_ = false;   // the head's copies on the next two slots' streams
   Event ev_head_, h2d_wait_;

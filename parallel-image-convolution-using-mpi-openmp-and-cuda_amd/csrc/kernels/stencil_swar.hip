@@ -345,9 +345,7 @@ bool known_pf_shape(const SwarShape& s) {
 }
 
 std::atomic<int> g_pf_mode{-1};  // -1 tune, 0 off, 1 forced
-std::atomic<int> g_stream_mode{-1};  // -1 tune, 0 off, 1 forced chained, 2 forced skewed
 
-int stream_mode() { return g_stream_mode.load(std::memory_order_relaxed); }
 
 int pf_mode() { return g_pf_mode.load(std::memory_order_relaxed); }
 
@@ -514,7 +512,6 @@ KernelRes kernel_res(SwarShape sh, int ch, int form) {
 // best shape in 6 of 6 configurations of the current kernel.
 void set_xcd_swizzle(bool on) { g_xcd_swizzle.store(on ? 1 : 0, std::memory_order_relaxed); }
 void set_swar_alt(int mode) { g_alt_mode.store(mode < 0 ? -1 : std::min(mode, 1), std::memory_order_relaxed); }
-void set_stream_mode(int mode) { g_stream_mode.store(mode < 0 ? -1 : std::min(mode, 2), std::memory_order_relaxed); }
 void set_prefetch_mode(int mode) { g_pf_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed); }
 std::vector<SwarShape> swar_prefetch_shapes() { return std::vector<SwarShape>(std::begin(kPfShapes), std::end(kPfShapes)); }
 
@@ -572,14 +569,10 @@ namespace {
 struct SwarChoice {
   SwarShape shape;
   int form = 1;  // step form of run_steps
-  int kern = 0;  // 0 tile kernel k_swar, 1 buffer-op k_swar_pf, 2 / 3 row-streaming chained / skewed
+  int kern = 0;  // 0 tile kernel k_swar, 1 buffer-op tile kernel k_swar_pf
 };
 
 void launch_choice(const StencilLaunch& a, Channels ch, hipStream_t stream, SwarChoice c) {
-  if (c.kern >= 2) {
-    launch_swar_stream(a, channel_count(ch), c.kern == 3, xcd_swizzle_enabled(), stream);
-    return;
-  }
   if (c.kern == 1) {
     switch (ch) {
       case Channels::Grey: launch_pf_ch<1>(a, stream, c.shape, c.form); break;
@@ -628,10 +621,6 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
   const int mode = alt_mode();
   SwarChoice fallback;
   fallback.form = default_form();
-  if (stream_mode() > 0 && swar_stream_ok(a, c)) {  // forced row-streaming kernel (tests, A/B)
-    fallback.kern = stream_mode() + 1;
-    return fallback;
-  }
   if (pf_mode() == 1 && pf_launch_ok(a, a.steps) && (override_shape(fallback.shape) || !autotune_enabled())) {
     // forced prefetch kernel, untuned: the overridden shape if it has a
     // prefetch instantiation, else the first prefetch shape that runs
@@ -695,15 +684,6 @@ SwarChoice tuned_choice(const StencilLaunch& a, Channels ch, hipStream_t stream,
             pfs.push_back(SwarChoice{r.second, form, 1});
     if (pf_mode() == 1 && !pfs.empty()) cands.clear();  // forced: only these candidates
     cands.insert(cands.end(), pfs.begin(), pfs.end());
-  }
-  // Row-streaming kernel, both level orders (kernels/stencil_stream.hip): no
-  // vertical halo and no barriers, fewer waves per SIMD (its level states).
-  if (stream_mode() != 0 && pf_mode() != 1 && swar_stream_ok(a, c)) {
-    SwarChoice sc = fallback;
-    sc.kern = 2;
-    cands.push_back(sc);
-    sc.kern = 3;
-    cands.push_back(sc);
   }
   SwarChoice best = cands.front();
   if (cands.size() > 1) {

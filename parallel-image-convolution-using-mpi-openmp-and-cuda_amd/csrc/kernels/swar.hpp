@@ -32,8 +32,7 @@ void set_autotune(bool on);
 void set_tune_candidates(int n);
 void clear_swar_tuning();
 // Tuned entries: ({channels, steps, rows, row_bytes, step_form, kernel}, shape); kernel 0: the tile
-// kernel k_swar, 1: the buffer-op tile kernel k_swar_pf, 2 / 3: the row-streaming kernel, chained /
-// skewed (shape unused).
+// kernel k_swar, 1: the buffer-op tile kernel k_swar_pf.
 std::vector<std::pair<std::vector<int64_t>, SwarShape>> swar_tuned();
 
 // Force a tile shape (lw = 0 restores the model) and list the instantiated ones.
@@ -57,14 +56,5 @@ void set_swar_alt(int mode);
 // set_swar_shape that it instantiates is used as is (tests).
 void set_prefetch_mode(int mode);
 std::vector<SwarShape> swar_prefetch_shapes();
-// Row-streaming kernel (k_swar_stream, kernels/stencil_stream.hip): one wave
-// per column strip pair and row segment, every repetition level kept as a
-// rolling state.  Instantiated for 4 / 8 / 12 steps per launch; `skew` picks
-// the level order (independent levels per row instead of one chain).
-bool swar_stream_ok(const StencilLaunch& a, int ch);
-void launch_swar_stream(const StencilLaunch& a, int ch, bool skew, bool xcd_swizzle, hipStream_t s);
-// Row-streaming kernel in the tuner: -1 among the timed candidates (default),
-// 0 never, 1 forced chained, 2 forced skewed (when the launch qualifies).
-void set_stream_mode(int mode);
 
 }  // namespace pconv

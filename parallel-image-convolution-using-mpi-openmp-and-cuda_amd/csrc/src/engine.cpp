@@ -673,6 +673,7 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
         idle_ = false;
         used_[k] = true;
         ++count_;
+        ++streamed_heads_;
         return;
       }
     }

@@ -366,9 +366,6 @@ PYBIND11_MODULE(_pconv_native, m) {
   m.def("set_prefetch_mode", &set_prefetch_mode, py::arg("mode"),
         "Buffer-op tile kernel: -1 tuned against the others (default), 0 never, 1 forced (with a set_swar_shape "
         "shape it instantiates, that shape)");
-  m.def("set_stream_mode", &set_stream_mode, py::arg("mode"),
-        "Row-streaming kernel (stencil_stream.hip): -1 tuned against the tile kernels (default), 0 never, 1 forced "
-        "chained, 2 forced skewed (launches it instantiates: 4 / 8 / 12 steps).");
   m.def("set_tune_candidates", &set_tune_candidates, py::arg("n"),
         "How many of the latency model's best SWAR tile shapes the tuner times (default 6).");
   m.def("set_float_shape", &set_float_shape, py::arg("m") = 0, py::arg("nw") = 0,
@@ -601,7 +598,7 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("graphs") = false, py::arg("step_graphs") = true,
            py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0,
            py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true,
-           py::arg("stream_min_bytes") = 0)
+           py::arg("stream_min_bytes") = EngineOptions{}.stream_min_bytes)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -628,6 +625,7 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_property_readonly("submitted", &BandPipeline::submitted)
       .def_property_readonly("concurrent", &BandPipeline::concurrent)
       .def_property_readonly("graphs", &BandPipeline::graphs)
+      .def_property_readonly("streamed_heads", &BandPipeline::streamed_heads)
       .def_property_readonly("step_graphs", &BandPipeline::step_graphs)
       .def_property_readonly("options",
                              [](BandPipeline& p) {

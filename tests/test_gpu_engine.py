@@ -307,7 +307,7 @@ def test_pipeline_streamed_rings(pconv_mod, rng, direct, slots, reps, world, ran
 
     w, h = 83, 120
     blur = DistributedBlur(w, h, "rgb", "gaussian", reps, rank=rank, world=world, device=0, slots=slots,
-                           preload_halo=True, transport="none", stream_chunks=4,
+                           preload_halo=True, transport="none", stream_chunks=4, stream_min_bytes=0,
                            step_graphs=False if direct else None)  # every image / the head image streamed
     b = blur.band
     imgs = [rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for _ in range(slots)]

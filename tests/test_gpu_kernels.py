@@ -286,64 +286,6 @@ def test_prefetch_kernel_tuned_large_frame(native, rng):
         torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("swizzle", [True, False])
-@pytest.mark.parametrize("mode", [1, 2])
-def test_stream_kernel_bit_exact(native, rng, mode, swizzle):
-    """The row-streaming kernel (k_swar_stream), forced chained (1) and skewed
-    (2), for every instantiated step count and channel layout: whole images
-    (one segment per strip pair and many; rows shorter than a strip, several
-    strip pairs), band regions whose ghost rows reach past the image top and
-    bottom and lie inside it, guard canaries, untouched rows outside
-    [r0, r1) — against the CPU fused reference."""
-    try:
-        native.set_xcd_swizzle(swizzle)
-        native.set_stream_mode(mode)
-        for channels in ("grey", "rgb", "rgba"):
-            c = CH[channels]
-            for steps in (4, 8, 12):
-                for (h, w) in [(5, 4), (131, 100), (997, 64), (60, 1200)]:
-                    img = rng.integers(0, 256, size=(h, w, c) if c > 1 else (h, w), dtype=np.uint8)
-                    gpu, cpu = _run_fused(native, img, steps, 0, h, steps, 0, h, variant="temporal")
-                    assert np.array_equal(gpu, cpu), (channels, steps, h, w)
-                halo = steps + 8
-                img = rng.integers(0, 256, size=(40, 100, c) if c > 1 else (40, 100), dtype=np.uint8)
-                for g_row0, height in ((30, 200), (0, 40), (0, 200), (160, 200)):
-                    for (r0, r1) in ((-5, 45), (0, 40), (3, 17)):
-                        gpu, cpu = _run_fused(native, img, steps, r0, r1, halo, g_row0, height, variant="temporal")
-                        fr0, fr1 = halo + r0, halo + r1
-                        assert np.array_equal(gpu[fr0:fr1], cpu[fr0:fr1]), (channels, steps, g_row0, r0, r1)
-                        assert (gpu[:fr0] == 0).all() and (gpu[fr1:] == 0).all(), "rows outside [r0, r1) written"
-    finally:
-        native.set_stream_mode(-1)
-        native.set_xcd_swizzle(True)
-        native.clear_swar_tuning()
-
-
-def test_stream_kernel_large_frame_and_tuner(native, rng):
-    """Both level orders on a frame with thousands of segments (the launch
-    sized to the chip), then the tuner's own pick with the row-streaming
-    kernel among its candidates; every choice is bit-exact."""
-    import torch
-
-    h, w = 1536, 4096
-    img = rng.integers(0, 256, size=(h, w), dtype=np.uint8)
-    try:
-        for mode in (1, 2):
-            native.set_stream_mode(mode)
-            gpu, cpu = _run_fused(native, img, 12, 0, h, 12, 0, h, variant="temporal")
-            assert np.array_equal(gpu, cpu), mode
-        native.set_stream_mode(-1)
-        native.clear_swar_tuning()
-        gpu, cpu = _run_fused(native, img, 12, 0, h, 12, 0, h, variant="temporal")
-        assert np.array_equal(gpu, cpu)
-        kerns = [k[5] for k, _ in native.swar_tuned() if k[1] == 12]
-        assert kerns and all(k in (0, 1, 2, 3) for k in kerns)
-    finally:
-        native.set_stream_mode(-1)
-        native.clear_swar_tuning()
-        torch.cuda.synchronize()
-
-
 def test_frame_beyond_2gib_offsets(pconv_mod, native):
     """64-bit offsets end to end: a 2.16 GB grey frame
     (65536 x 33000) through the fused kernel; rows near the top, the middle

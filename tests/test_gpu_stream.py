@@ -21,6 +21,7 @@ def _blur(w, h, ch, filt, reps, chunks, slots=2, mode="direct", **kw):
     is idle (the first of every burst here) and runs the others as graphs."""
     from pconv.parallel.dist_engine import DistributedBlur
 
+    kw.setdefault("stream_min_bytes", 0)  # head-stream these small images too
     b = DistributedBlur(w, h, ch, filt, reps, device=0, slots=slots, stream_chunks=chunks,
                         step_graphs=None if mode == "head" else False, **kw)
     assert b.pipe.graphs == (mode == "head")
@@ -96,6 +97,25 @@ def test_head_stream_modes(pconv_mod, rng, on_slots, slots):
     blur.load_image(img)
     for _ in range(3):
         assert np.array_equal(blur.step(reps).reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps))
+
+
+def test_head_stream_threshold(pconv_mod, rng):
+    """EngineOptions::stream_min_bytes (default 8 MiB): the headline frame
+    (14.5 MB) is head-streamed, its 8-way band (2.3 MB) runs as one step
+    graph unless the threshold is lowered; both bit-exact."""
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    w, h, reps = 1920, 2520, 8
+    img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+    ref = pconv_mod.numpy_convolve(img, reps).reshape(h, -1)
+    for world, rank, kw, streamed in ((1, 0, {}, True), (8, 3, {}, False), (8, 3, {"stream_min_bytes": 0}, True)):
+        b = DistributedBlur(w, h, "rgb", "gaussian", reps, rank=rank, world=world, device=0, slots=3,
+                            preload_halo=world > 1, transport="none", stream_chunks=4, **kw)
+        assert b.pipe.options["stream_min_bytes"] == kw.get("stream_min_bytes", 8 << 20)
+        b.load_image(img)
+        out = b.step(reps)
+        assert b.pipe.streamed_heads == (1 if streamed else 0), (world, kw)
+        assert np.array_equal(out, ref[b.band.y0:b.band.y0 + b.band.rows]), (world, kw)
 
 
 @pytest.mark.parametrize("mode", ["direct", "head"])
