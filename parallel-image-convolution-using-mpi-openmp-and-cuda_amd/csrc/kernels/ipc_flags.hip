@@ -66,31 +66,47 @@ __device__ void ack_wait(IpcMailbox* mine, IpcMailbox* up_mb, IpcMailbox* down_m
 }
 
 // Copy of `n16` 16-byte granules per side by `nthreads` threads starting
-// at thread `t0`: four loads in flight per side before their stores (a
-// remote source costs a round trip per load; restrict lets the loads run
-// ahead of the stores).
-__device__ __forceinline__ void pull_rows(uint4* __restrict__ dst_up, const uint4* __restrict__ src_up,
-                                          uint4* __restrict__ dst_down, const uint4* __restrict__ src_down,
-                                          int64_t n16, int64_t t0, int64_t nthreads) {
+// at thread `t0`: four loads per side in flight before their stores.  A
+// remote source costs a round trip per dependent load, and with the grid
+// form's sizing a thread has ~2 granules per side, so the slice must be ONE
+// round trip: the sides are template parameters and neither loads nor
+// stores are predicated (past the end an index wraps to an earlier granule,
+// which is copied again with the same bytes) — with per-side or
+// per-granule branches the compiler sank every load into its store's block
+// behind its own s_waitcnt vmcnt(0), one round trip per granule.
+__device__ __forceinline__ int64_t wrap(int64_t j, int64_t n) { return j < n ? j : min(j - n, n - 1); }
+
+template <bool UP, bool DOWN>
+__device__ __forceinline__ void pull_sides(uint4* __restrict__ dst_up, const uint4* __restrict__ src_up,
+                                           uint4* __restrict__ dst_down, const uint4* __restrict__ src_down,
+                                           int64_t n16, int64_t t0, int64_t nthreads) {
   constexpr int U = 4;
-  int64_t i = t0;
-  for (; i + (U - 1) * nthreads < n16; i += U * nthreads) {
+  for (int64_t i = t0; i < n16; i += U * nthreads) {
     uint4 a[U], b[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (src_up) a[u] = src_up[i + u * nthreads];
-      if (src_down) b[u] = src_down[i + u * nthreads];
+      const int64_t j = wrap(i + u * nthreads, n16);
+      if constexpr (UP) a[u] = src_up[j];
+      if constexpr (DOWN) b[u] = src_down[j];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (src_up) dst_up[i + u * nthreads] = a[u];
-      if (src_down) dst_down[i + u * nthreads] = b[u];
+      const int64_t j = wrap(i + u * nthreads, n16);
+      if constexpr (UP) dst_up[j] = a[u];
+      if constexpr (DOWN) dst_down[j] = b[u];
     }
   }
-  for (; i < n16; i += nthreads) {
-    if (src_up) dst_up[i] = src_up[i];
-    if (src_down) dst_down[i] = src_down[i];
-  }
+}
+
+__device__ __forceinline__ void pull_rows(uint4* __restrict__ dst_up, const uint4* __restrict__ src_up,
+                                          uint4* __restrict__ dst_down, const uint4* __restrict__ src_down,
+                                          int64_t n16, int64_t t0, int64_t nthreads) {
+  if (src_up && src_down)
+    pull_sides<true, true>(dst_up, src_up, dst_down, src_down, n16, t0, nthreads);
+  else if (src_up)
+    pull_sides<true, false>(dst_up, src_up, dst_down, src_down, n16, t0, nthreads);
+  else if (src_down)
+    pull_sides<false, true>(dst_up, src_up, dst_down, src_down, n16, t0, nthreads);
 }
 
 // Grid form: G workgroups, ONE dispatch.  `count` changes only at the very
@@ -173,8 +189,9 @@ __global__ __launch_bounds__(64) void k_ipc_ack_wait(IpcMailbox* mine, IpcMailbo
 }  // namespace
 
 int ipc_grid_workgroups(int64_t bytes) {
-  // ~8 KB per workgroup and side (two passes of 256 lanes x 16 B), 8..64
-  return static_cast<int>(std::min<int64_t>(64, std::max<int64_t>(8, (bytes / 16 + 511) / 512)));
+  // 16 KB per workgroup and side: every lane's four granules per side in
+  // flight at once (pull_sides), 8..64 workgroups
+  return static_cast<int>(std::min<int64_t>(64, std::max<int64_t>(8, (bytes / 16 + 1023) / 1024)));
 }
 
 void launch_ipc_exchange(IpcPull form, IpcMailbox* mine, IpcMailbox* up_mb, IpcMailbox* down_mb, uint32_t* err,
