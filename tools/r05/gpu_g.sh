@@ -15,5 +15,5 @@ timeout -k 10 200 python -u tools/r05/ipc_probe.py --workgroups 0,8,16,29,32,64 
 cat $OUT/ipc_probe.jsonl
 for m in grid single; do
   timeout -k 10 300 python -u bench.py --emulate 8:3 --emulate-halo ipc --ipc-pull $m --steps 300 --warmup 10 > $OUT/e8_ipc_$m.json 2> $OUT/e8_ipc_$m.err || { echo "bench failed"; tail -5 $OUT/e8_ipc_$m.err; exit 1; }
-  python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['ms_per_step'], d['copy_floor']['pair_ms'], d['mismatches'])" $OUT/e8_ipc_$m.json
+  python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['ms_per_step'], d['copy_floor']['pair_ms'], d.get('mismatches'))" $OUT/e8_ipc_$m.json
 done
