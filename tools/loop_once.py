@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Run one device-resident loop (for profilers): W H channels reps fuse iters.
-Environment knobs of the kernels apply (PCONV_SWAR_SHAPE, PCONV_PREFETCH, ...)."""
+The kernel choice is the tuner's; force one through the kernel setters
+(pconv.native.set_swar_shape / set_prefetch_mode / set_swar_alt) in a copy
+of this script (no environment variable changes the kernels)."""
 import os
 import sys
 

@@ -195,10 +195,10 @@ def cmd_mpi_cpu(a):
                     threads = None
                     if a.unbound:  # round-2 policy (A/B): unbound ranks, team = CPUs // ranks
                         threads = max(1, ncpu // n) if backend == "omp" else 1
-                        env.update(OMP_NUM_THREADS=str(threads), PCONV_CPU_BIND="0")
+                        env.update(OMP_NUM_THREADS=str(threads))
                         extra = ["--threads", str(threads)] if backend == "omp" else []
-                    if a.bind != "default":
-                        env["PCONV_CPU_BIND"] = "1" if a.bind == "on" else "0"
+                    if a.bind == "on" and not a.unbound:  # run.py --cpu-bind (default: unbound teams)
+                        extra.append("--cpu-bind")
                     if a.wait:
                         env["OMP_WAIT_POLICY"] = a.wait
                     if a.spin is not None:
