@@ -271,6 +271,7 @@ def test_bench_policy_flags():
         sys.argv = ["bench.py"]
         a = bench.parse()
         assert (a.cu_mask_queues, a.head_on_slot_streams, a.ipc_pull, a.numa_bind) == (True, True, "grid", "on")
+        assert a.stream_min_mb == 8.0 and a.stream_chunks == 4  # head streaming for images >= 8 MiB
         sys.argv = ["bench.py", "--pool-queues", "--head-pool-streams", "--ipc-pull", "sdma",
                     "--numa-bind", "off"]
         a = bench.parse()
