@@ -129,6 +129,10 @@ def parse():
     p.add_argument("--halo-modes", default=",".join(HALO_MODES),
                    help="comma list of the halo modes timed after the headline at N>1: " + ", ".join(HALO_MODES))
     p.add_argument("--exchange-timeout", type=float, default=30.0, help="seconds before a mode's drain aborts")
+    p.add_argument("--resident-loop", choices=["on", "off"], default="on",
+                   help="N>1, halo mode 'event': also time the reference's MPI loop on the resident bands (reps with "
+                        "the ghost rows exchanged every halo-depth reps through the transport, no PCIe), "
+                        "reported as halo_modes.event.resident_loop and resident_loop")
     p.add_argument("--halo-select", choices=["auto", "off", "exchange"] + list(HALO_MODES), default="auto",
                    help="N>1: report as the headline the fastest bit-exact halo mode when it is at least 3 %% faster "
                         "than the pre-loaded pipeline (auto; the halo mode chosen by measurement, like the kernel "
@@ -274,6 +278,45 @@ def mode_kwargs(a, mode: str, fuse: int) -> dict:
     return kw
 
 
+def resident_loop(blur, a) -> dict:
+    """The reference's MPI loop (mpi/mpi_convolution.c:156-240, loop-only
+    timing) on the bands already resident on the GPUs: `reps` repetitions
+    with the ghost rows exchanged every `halo` repetitions through the mode's
+    transport (RCCL over xGMI between real GPUs), no PCIe; K loops between
+    barriers, max over ranks.  Ghost contents are whatever the frames hold
+    (timing only: the pipelined mode's images were oracle-checked)."""
+    import torch
+
+    from pconv.parallel.bootstrap import barrier, max_over_ranks
+
+    eng = blur.engine
+    steps = a.loop_steps if a.loop_steps is not None else a.steps
+
+    def once():
+        eng.set_halo_valid(False)  # exchange every `halo` reps, as the reference does every rep
+        eng.run(a.reps)
+
+    for _ in range(2):
+        once()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    t = time.perf_counter()
+    for _ in range(steps):
+        once()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    elapsed = max_over_ranks(time.perf_counter() - t)
+    st = eng.stats
+    px = a.width * a.height * a.reps
+    return {"ms_per_image": round(elapsed / steps * 1e3, 4), "mpix_per_s": round(px * steps / elapsed / 1e6, 2),
+            "steps": steps, "exchanges_per_image": int(st.exchanges), "launches_per_image": int(st.launches),
+            "halo_rows": int(eng.halo),
+            # per rank: the ghost rows it receives per exchange (both sides for an interior band)
+            "ghost_bytes_per_exchange": gather_ints(int(eng.halo) * int(blur.row_bytes) *
+                                                    (int(eng.band.up >= 0) + int(eng.band.down >= 0)))}
+
+
 def measure_mode(a, mode, ref_rows, world, rank, device, transport, fuse, oracle=None):
     """Time K steps of one halo mode exactly like the headline (barrier +
     device sync on both sides, max over ranks) and compare its newest image
@@ -317,6 +360,11 @@ def measure_mode(a, mode, ref_rows, world, rank, device, transport, fuse, oracle
                    slot_streams=bool(xb.pipe.graphs), step_graphs=bool(xb.pipe.step_graphs),
                    concurrent_images=bool(xb.pipe.concurrent),
                    overlap_split=mode == "overlap" or (mode == "event" and not a.no_overlap))
+        if mode == "event" and a.resident_loop == "on":
+            try:
+                res["resident_loop"] = resident_loop(xb, a)
+            except Exception as e:  # noqa: BLE001  (the mode's own timing stands)
+                res["resident_loop"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     except Exception as e:  # reported, never fatal for the headline line
         res["status"] = f"error: {type(e).__name__}: {e}"[:400]
     finally:
@@ -746,6 +794,9 @@ def main():
             pending["mode"] = None
             if out is not None:
                 results[m] = r
+        if out is not None and "resident_loop" in results.get("event", {}):
+            # the reference's loop-only MPI semantics, ghost rows crossing between the GPUs
+            out["resident_loop"] = dict(results["event"]["resident_loop"], transport=results["event"]["transport"])
         # Halo mode chosen by measurement: every rank sees the same reduced
         # numbers, so they agree; rank 0 reports.
         if out is not None:

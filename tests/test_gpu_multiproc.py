@@ -112,6 +112,13 @@ def test_bench_torchrun_rehearsal(world, extra):
         assert r["mismatches"] == 0, (m, r)  # every mode against the oracle, not only the headline's bytes
         if m != head:
             assert r["mismatches_vs_headline"] == 0 and r["exchanges_per_step"] >= 1, (m, r)
+    # the reference's loop-only MPI timing on the resident bands, exchanges through the event mode's transport
+    if head != "event":
+        rl = meta["resident_loop"]
+        assert rl == dict(modes["event"]["resident_loop"], transport=modes["event"]["transport"])
+        assert rl["ms_per_image"] > 0 and rl["exchanges_per_image"] >= 40 // rl["halo_rows"], rl
+        g = rl["ghost_bytes_per_exchange"]  # per rank: one side at the image edges, two inside
+        assert len(g) == world and g[0] == g[-1] and all(x == 2 * g[0] for x in g[1:-1]), g
     # overlap: a T-deep ghost zone, one exchange per fused launch (the reference's per-rep loop, T at a time)
     assert modes["overlap"]["halo_depth"] == modes["overlap"]["fuse"]
     assert modes["overlap"]["exchanges_per_step"] >= 40 // modes["overlap"]["fuse"]
