@@ -281,22 +281,40 @@ def mode_kwargs(a, mode: str, fuse: int) -> dict:
 def resident_loop(blur, a) -> dict:
     """The reference's MPI loop (mpi/mpi_convolution.c:156-240, loop-only
     timing) on the bands already resident on the GPUs: `reps` repetitions
-    with the ghost rows exchanged every `halo` repetitions through the mode's
-    transport (RCCL over xGMI between real GPUs), no PCIe; K loops between
-    barriers, max over ranks.  Ghost contents are whatever the frames hold
-    (timing only: the pipelined mode's images were oracle-checked)."""
+    with the ghost rows exchanged every `halo` repetitions through the
+    pipeline's transport (RCCL over xGMI between real GPUs), no PCIe.  Its own
+    engine runs the exchanges on the compute stream, so with a capturable
+    transport (RCCL) the whole loop — exchanges and launches — replays as ONE
+    cached graph per image (EngineOptions::capture_exchanges).  K loops
+    between barriers, max over ranks; ghost contents are whatever the frames
+    hold (timing only: the pipelined mode's images were oracle-checked)."""
+    import numpy as np
     import torch
 
+    import pconv
     from pconv.parallel.bootstrap import barrier, max_over_ranks
 
-    eng = blur.engine
+    n = pconv.native
+    b = blur.band
+    eng = n.BandEngine.for_band(a.width, a.height, a.channels, a.filter, b, blur.device, halo=int(blur.engine.halo),
+                                fuse=int(blur.engine.fuse), overlap=False, variant=a.variant, graph=True,
+                                capture_exchanges=True)
+    if blur.comm is not None:
+        eng.attach_rccl(blur.comm)
+        transport = "rccl"
+    elif blur.transport is not None:
+        eng.attach_transport(blur.transport)
+        transport = type(blur.transport).__name__
+    else:
+        raise RuntimeError("resident loop: the pipeline has no halo transport")
+    eng.upload(np.ascontiguousarray(blur.inputs[0][:b.rows]).reshape(-1), 0, b.rows)
     steps = a.loop_steps if a.loop_steps is not None else a.steps
 
     def once():
         eng.set_halo_valid(False)  # exchange every `halo` reps, as the reference does every rep
         eng.run(a.reps)
 
-    for _ in range(2):
+    for _ in range(2):  # the first run captures the graph (tuning first)
         once()
     eng.synchronize()
     torch.cuda.synchronize()
@@ -309,12 +327,14 @@ def resident_loop(blur, a) -> dict:
     elapsed = max_over_ranks(time.perf_counter() - t)
     st = eng.stats
     px = a.width * a.height * a.reps
-    return {"ms_per_image": round(elapsed / steps * 1e3, 4), "mpix_per_s": round(px * steps / elapsed / 1e6, 2),
-            "steps": steps, "exchanges_per_image": int(st.exchanges), "launches_per_image": int(st.launches),
-            "halo_rows": int(eng.halo),
-            # per rank: the ghost rows it receives per exchange (both sides for an interior band)
-            "ghost_bytes_per_exchange": gather_ints(int(eng.halo) * int(blur.row_bytes) *
-                                                    (int(eng.band.up >= 0) + int(eng.band.down >= 0)))}
+    out = {"ms_per_image": round(elapsed / steps * 1e3, 4), "mpix_per_s": round(px * steps / elapsed / 1e6, 2),
+           "steps": steps, "exchanges_per_image": int(st.exchanges), "launches_per_image": int(st.launches),
+           "halo_rows": int(eng.halo), "one_graph_per_image": int(eng.cached_graphs) > 0, "transport": transport,
+           # per rank: the ghost rows it receives per exchange (both sides for an interior band)
+           "ghost_bytes_per_exchange": gather_ints(int(eng.halo) * int(blur.row_bytes) *
+                                                   (int(b.up >= 0) + int(b.down >= 0)))}
+    del eng
+    return out
 
 
 def measure_mode(a, mode, ref_rows, world, rank, device, transport, fuse, oracle=None):
@@ -734,6 +754,11 @@ def main():
                 how = "IPC pulls of its own rows" if a.emulate_halo == "ipc" else "RCCL send/recv to self"
                 out["emulated"] += f"; halos exchanged with the rank itself ({how}): real exchange costs, ghost " \
                                    "contents not those of its neighbours"
+    if a.emulate and a.emulate_halo == "event" and a.resident_loop == "on":
+        # the resident MPI loop of this rank's band, ghost rows through RCCL send/recv to itself
+        rl = resident_loop(blur, a)
+        if out is not None:
+            out["resident_loop"] = rl
 
     import threading
 
@@ -796,7 +821,7 @@ def main():
                 results[m] = r
         if out is not None and "resident_loop" in results.get("event", {}):
             # the reference's loop-only MPI semantics, ghost rows crossing between the GPUs
-            out["resident_loop"] = dict(results["event"]["resident_loop"], transport=results["event"]["transport"])
+            out["resident_loop"] = results["event"]["resident_loop"]
         # Halo mode chosen by measurement: every rank sees the same reduced
         # numbers, so they agree; rank 0 reports.
         if out is not None:

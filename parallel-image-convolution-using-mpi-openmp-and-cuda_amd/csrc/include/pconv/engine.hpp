@@ -52,6 +52,12 @@ struct EngineOptions {
   int fuse = 1;            // T (reps per launch; > 1 needs the temporal kernel)
   bool overlap = true;     // interior || halo
   bool use_graph = false;  // capture the rep loop into a hipGraph (no transport)
+  // With use_graph: exchange phases run on the compute stream (no separate
+  // communication stream) and, with a capturable transport (RCCL, IPC), are
+  // captured with the launches into the cached rep-loop graph — the
+  // reference's MPI loop on resident bands as one graph launch per image
+  // (bench.py resident_loop).
+  bool capture_exchanges = false;
   KernelVariant variant = KernelVariant::Auto;
   // Borrowed streams (nullptr: the engine creates its own).  A process has
   // few hardware queues (GPU_MAX_HW_QUEUES, 4 by default); pipeline slots

@@ -54,7 +54,7 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
   // Communication stream only when the band has neighbours (or is borrowed).
   if (opt_.comm_stream) {
     ms_ = opt_.comm_stream;
-  } else if (band_.up >= 0 || band_.down >= 0) {
+  } else if ((band_.up >= 0 || band_.down >= 0) && !opt_.capture_exchanges) {
     own_ms_ = Stream::create(-1);  // communication gets the higher priority
     ms_ = own_ms_.get();
   } else {
@@ -290,7 +290,10 @@ void BandEngine::run(int reps) {
   wall_t0_ = wall_seconds();
   if (opt_.timing) ev_t0_.record(cs_);
   bool graph = opt_.use_graph && !ph.empty();
-  for (const auto& p : ph) graph = graph && p.exchange_depth == 0;
+  // exchanges join the graph only on the compute stream and through a
+  // capturable transport (opt_.capture_exchanges)
+  const bool cap_x = opt_.capture_exchanges && ms_ == cs_ && transport_ && transport_->capturable();
+  for (const auto& p : ph) graph = graph && (p.exchange_depth == 0 || cap_x);
   if (graph) {
     const auto key = std::make_pair(reps, cur_);
     auto it = graphs_.find(key);
@@ -308,6 +311,7 @@ void BandEngine::run(int reps) {
     } else {
       for (const auto& p : ph) {
         stats_.launches += static_cast<int>(p.launches.size());
+        if (p.exchange_depth > 0) ++stats_.exchanges;
         cur_ ^= 1;
       }
     }

@@ -547,7 +547,7 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_static(
           "for_band",
           [](int64_t w, int64_t h, const std::string& ch, py::object filter, const Band& band, int device, int halo,
-             int fuse, bool overlap, const std::string& variant) {
+             int fuse, bool overlap, const std::string& variant, bool graph, bool capture_exchanges) {
             // An explicit band (tests: e.g. a single rank whose up/down
             // neighbour is itself, to drive RCCL send/recv-to-self).
             EngineOptions o;
@@ -556,11 +556,13 @@ PYBIND11_MODULE(_pconv_native, m) {
             o.fuse = fuse;
             o.overlap = overlap;
             o.variant = parse_variant(variant);
+            o.use_graph = graph;
+            o.capture_exchanges = capture_exchanges;
             return std::make_unique<BandEngine>(make_geom(w, h, ch), band, make_filter(filter), o);
           },
           py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter"), py::arg("band"),
           py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1, py::arg("overlap") = true,
-          py::arg("variant") = "auto")
+          py::arg("variant") = "auto", py::arg("graph") = false, py::arg("capture_exchanges") = false)
       .def("attach_rccl",
            [](BandEngine& e, std::shared_ptr<RcclComm> c) {
              e.set_transport(std::make_shared<RcclTransport>(std::move(c)));

@@ -151,6 +151,37 @@ def test_rccl_mid_image_band_consumes_exchanged_rows(pconv_mod, rng, self_comm, 
         assert bad == 0, f"{bad} bytes differ from the reflected-ghost oracle"
 
 
+@pytest.mark.parametrize("ch,w", [("rgb", 57), ("grey", 1920)])
+@pytest.mark.parametrize("reps,halo,fuse", [(13, 4, 4), (20, 8, 8), (40, 40, 8), (24, 12, 8)])
+def test_rccl_band_exchanges_captured_in_the_loop_graph(pconv_mod, rng, self_comm, ch, w, reps, halo, fuse):
+    """EngineOptions::capture_exchanges (bench.py's resident loop): the
+    exchange phases run on the compute stream and ncclSend/ncclRecv are
+    captured with the launches into the cached rep-loop graph — the first
+    run captures, later runs (both frame parities) replay; every run equals
+    the reflected-ghost oracle byte for byte and counts its exchanges."""
+    n = pconv_mod.native
+    c = {"grey": 1, "rgb": 3}[ch]
+    y0, rows, height = 37, 48, 130
+    eng = n.BandEngine.for_band(w, height, ch, "gaussian", _mid_band(n, y0, rows), 0, halo, fuse, False, "auto",
+                                graph=True, capture_exchanges=True)
+    eng.attach_rccl(self_comm)
+    assert eng.comm_stream == eng.compute_stream  # exchanges in stream order with the launches
+    owned = rng.integers(0, 256, size=(rows, w * c), dtype=np.uint8)
+    plan = eng.plan(reps)
+    n_ex = len([p for p in plan if p.exchange_depth])
+    ref = reflected_ghost_oracle(n, plan, eng.halo, owned, y0, height, ch)
+    for i in range(4):  # capture, replay, and the other frame parity
+        eng.upload(owned.reshape(-1), 0, rows)
+        eng.run(reps)
+        self_comm.wait(eng.compute_stream, 60.0)
+        eng.synchronize()
+        assert eng.stats.exchanges == n_ex and eng.cached_graphs >= 1, (i, eng.stats.exchanges, eng.cached_graphs)
+        out = np.empty_like(owned)
+        eng.download(out.reshape(-1), 0, rows)
+        eng.synchronize()
+        assert np.array_equal(out, ref), i
+
+
 @pytest.mark.parametrize("bands", [2, 3, 5, 8])
 @pytest.mark.parametrize("halo,fuse,overlap,preload", [(1, 1, True, False), (4, 4, True, False), (8, 4, True, True),
                                                        (6, 3, False, False), (16, 8, True, False)])

@@ -115,8 +115,9 @@ def test_bench_torchrun_rehearsal(world, extra):
     # the reference's loop-only MPI timing on the resident bands, exchanges through the event mode's transport
     if head != "event":
         rl = meta["resident_loop"]
-        assert rl == dict(modes["event"]["resident_loop"], transport=modes["event"]["transport"])
+        assert rl == modes["event"]["resident_loop"] and rl["transport"] == "GlooHostTransport", rl
         assert rl["ms_per_image"] > 0 and rl["exchanges_per_image"] >= 40 // rl["halo_rows"], rl
+        assert rl["one_graph_per_image"] is False  # host-staged halos cannot be captured
         g = rl["ghost_bytes_per_exchange"]  # per rank: one side at the image edges, two inside
         assert len(g) == world and g[0] == g[-1] and all(x == 2 * g[0] for x in g[1:-1]), g
     # overlap: a T-deep ghost zone, one exchange per fused launch (the reference's per-rep loop, T at a time)
@@ -231,3 +232,30 @@ def test_slot_exchange_pipeline_one_gpu(pconv_mod, world, halo, fuse, reps, slot
     for rank, y0, outs in res:
         for o in outs:
             assert np.array_equal(o, ref[y0:y0 + o.shape[0]]), rank
+
+
+@pytest.mark.parametrize("halo", ["preload", "event", "slot_exchange", "ipc"])
+def test_bench_emulated_rank_halo_modes(halo):
+    """`bench.py --emulate 8:3 --emulate-halo MODE`: one rank's step of the
+    8-way split with its exchanges really issued (RCCL send/recv or IPC pulls
+    to itself); with `event` also the resident MPI loop of its band through
+    RCCL (resident_loop).  The pre-loaded proxy is oracle-checked."""
+    import json
+    import subprocess
+    import sys
+
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--emulate", "8:3", "--emulate-halo", halo,
+           "--steps", "10", "--warmup", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["config"]["halo_mode"] == halo and d["ms_per_step"] > 0 and "8-way split" in d["emulated"]
+    if halo == "preload":
+        assert d["mismatches"] == 0
+    if halo == "event":
+        rl = d["resident_loop"]
+        assert rl["transport"] == "rccl" and rl["ms_per_image"] > 0 and rl["exchanges_per_image"] >= 1, rl
+        assert rl["one_graph_per_image"] is True  # RCCL send/recv captured with the launches
+        assert rl["ghost_bytes_per_exchange"] == [2 * rl["halo_rows"] * 1920 * 3], rl
+    else:
+        assert "resident_loop" not in d
