@@ -108,6 +108,9 @@ def parse():
                         "them, download finished rows meanwhile (H2D, reps and D2H of ONE image overlap; 0 = off). "
                         "With step graphs only an image submitted to an idle pipeline is streamed (the head of a "
                         "burst, every single image: latency_ms 0.56 vs 0.69 ms whole-image, profiles/r04/head/)")
+    p.add_argument("--head-one-upload-stream", dest="head_alt_uploads", action="store_false", default=True,
+                   help="streamed head image: all chunk uploads on one slot's stream (default with >= 4 slots: "
+                        "alternating over two, one image 0.546-0.549 vs 0.559-0.568 ms, profiles/r05/l/)")
     p.add_argument("--stream-min-mb", type=float, default=8.0,
                    help="head-stream only images of at least this many MiB of input: below it the hand-offs of a "
                         "streamed image cost more than they hide (N=4 band 0.32 vs 0.23 ms as one graph, N=8 0.28 "
@@ -257,6 +260,7 @@ def policy_kwargs(a) -> dict:
     """Pipeline policy flags -> DistributedBlur / native EngineOptions (echoed in the JSON config)."""
     return dict(cu_mask_queues=getattr(a, "cu_mask_queues", True),
                 head_on_slot_streams=getattr(a, "head_on_slot_streams", True),
+                head_alt_uploads=getattr(a, "head_alt_uploads", True),
                 ipc_pull=getattr(a, "ipc_pull", "grid"))
 
 
@@ -718,6 +722,7 @@ def main():
                 "exchanges_per_step": int(stats.exchanges),
                 "cu_mask_queues": bool(a.cu_mask_queues),
                 "head_on_slot_streams": bool(a.head_on_slot_streams),
+                "head_alt_uploads": bool(a.head_alt_uploads),
                 "ipc_pull": a.ipc_pull,
                 "numa_bind": a.numa_bind == "on",
             },

@@ -96,6 +96,13 @@ struct EngineOptions {
   // streams (idle while the pipeline is) instead of two more pool streams
   // (0.56 vs 0.77 ms per image with 4 slots, profiles/r04/head/).
   bool head_on_slot_streams = true;
+  // With the head's copies on the slots' streams and >= 4 slots: its chunk
+  // uploads alternate between slots k+1 and k+2's streams, so one chunk's
+  // copy + event does not leave the copy engine idle before the next.  One
+  // image 0.546-0.549 vs 0.559-0.568 ms over 3 interleaved rounds, the
+  // driver's window 0.334-0.348 vs 0.337-0.351 ms; alternating the downloads
+  // too was slower (0.564-0.580, both 0.602-0.625: profiles/r05/l/).
+  bool head_alt_uploads = true;
 };
 
 struct RunStats {
@@ -187,8 +194,9 @@ class BandEngine {
   // stream, downloads of the finished rows on `down` (cross-stream events per
   // chunk).  The caller orders `up` after any earlier use of these frames.
   // Returns the stream whose completion means the whole image is done.
+  // `up2` (optional): odd chunks' uploads alternate onto it.
   hipStream_t enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
-                               const StreamPlan& sp, hipStream_t up, hipStream_t down);
+                               const StreamPlan& sp, hipStream_t up, hipStream_t down, hipStream_t up2 = nullptr);
   // Phase-by-phase execution for multi-band emulation on one device.
   std::vector<Phase> plan(int reps) const;
   void exec_exchange(const Phase& p);

@@ -345,7 +345,8 @@ StreamPlan BandEngine::stream_plan(int reps, int64_t in_r0, int64_t in_r1) const
 }
 
 hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
-                                         const StreamPlan& sp, hipStream_t up, hipStream_t down) {
+                                         const StreamPlan& sp, hipStream_t up, hipStream_t down,
+                                         hipStream_t up2) {
   TraceRange tr("pconv.streamed_image");
   PCONV_CHECK(!sp.chunks.empty(), "enqueue_streamed: empty stream plan");
   PCONV_CHECK(sp.chunks.front().up_lo == in_r0 && sp.chunks.back().up_hi == in_r1,
@@ -384,16 +385,17 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
       copy(host_out + ch.down_lo * rb, rb, out_frame + ch.down_lo * p, p, ch.down_hi - ch.down_lo,
            hipMemcpyDeviceToHost, s);
   };
+  auto up_of = [&](size_t c) { return (c & 1) && up2 ? up2 : up; };
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     copy(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, ch.up_hi - ch.up_lo,
-         hipMemcpyHostToDevice, up);
-    if (up != cs_) up_evs_[c].record(up);
+         hipMemcpyHostToDevice, up_of(c));
+    if (up_of(c) != cs_) up_evs_[c].record(up_of(c));
   }
   bool pending = false;  // launches not yet covered by a download-side event
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
-    if (up != cs_) up_evs_[c].wait_on(cs_);
+    if (up_of(c) != cs_) up_evs_[c].wait_on(cs_);
     launches(ch);
     if (!ch.launches.empty()) pending = true;
     if (ch.down_hi > ch.down_lo && host_out) {
@@ -667,9 +669,14 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
         const int n = slots();
         hipStream_t up = head_on_slots_ ? computes_[static_cast<size_t>((k + 1) % n)].get() : h2d_.get();
         hipStream_t down = head_on_slots_ ? computes_[static_cast<size_t>((k + n - 1) % n)].get() : d2h_.get();
+        // odd chunks' uploads on slot k+2's stream (EngineOptions::head_alt_uploads)
+        hipStream_t up2 = head_on_slots_ && n >= 4 && e.options().head_alt_uploads
+                              ? computes_[static_cast<size_t>((k + 2) % n)].get()
+                              : nullptr;
         h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
         h2d_wait_.wait_on(up);
-        hipStream_t done = e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down);
+        if (up2) h2d_wait_.wait_on(up2);
+        hipStream_t done = e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down, up2);
         if (done != e.compute_stream()) {
           ev_head_.record(done);
           ev_head_.wait_on(e.compute_stream());

@@ -84,14 +84,17 @@ def test_streamed_preloaded_bands(pconv_mod, rng, mode, world, rank):
     _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps)
 
 
-@pytest.mark.parametrize("on_slots", [False, True])
+@pytest.mark.parametrize("on_slots,alt", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("slots", [2, 3, 4])
-def test_head_stream_modes(pconv_mod, rng, on_slots, slots):
+def test_head_stream_modes(pconv_mod, rng, on_slots, alt, slots):
     """head_on_slot_streams: the streamed head image's copies on two pool
     streams, or on the next two slots' streams (falls back below 3 slots);
-    bursts and single images (blur.step) bit-exact."""
+    head_alt_uploads (>= 4 slots): its chunk uploads alternating over two
+    slots' streams; bursts and single images (blur.step) bit-exact."""
     w, h, reps = 96, 120, 40
-    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=slots, mode="head", head_on_slot_streams=on_slots)
+    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=slots, mode="head", head_on_slot_streams=on_slots,
+                 head_alt_uploads=alt)
+    assert blur.pipe.options["head_alt_uploads"] is alt
     _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps, rounds=3)
     img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
     blur.load_image(img)
