@@ -32,11 +32,16 @@ if lines:
                per_rank=len(d["per_rank_ms_per_step"]), h2d_bytes=d.get("h2d_bytes_per_step"),
                d2h_bytes=d.get("d2h_bytes_per_step"), halo_select=d.get("halo_select", {}).get("mode"),
                modes={m: (r.get("status"), r.get("ms_per_step"), r.get("mismatches")) for m, r in
-                      d.get("halo_modes", {}).items()})
+                      d.get("halo_modes", {}).items()},
+               resident_loop=d.get("resident_loop"))
 print(json.dumps(rec))
 PY
   return $rc
 }
-run headline 600 | tee -a $OUT/summary.jsonl || exit 1
-run rgb8192 600 --width 8192 --height 8192 --channels rgb --reps 100 | tee -a $OUT/summary.jsonl || exit 1
-run grey32768 600 --width 32768 --height 32768 --channels grey --reps 200 | tee -a $OUT/summary.jsonl || exit 1
+ONLY=${1:-all}  # one config name, or all
+want() { [ "$ONLY" = all ] || [ "$ONLY" = "$1" ]; }
+if want headline; then run headline 600 | tee -a $OUT/summary.jsonl || exit 1; fi
+if want rgb8192; then run rgb8192 600 --width 8192 --height 8192 --channels rgb --reps 100 | tee -a $OUT/summary.jsonl || exit 1; fi
+if want grey32768; then
+  run grey32768 600 --width 32768 --height 32768 --channels grey --reps 200 | tee -a $OUT/summary.jsonl || exit 1
+fi
