@@ -133,9 +133,9 @@ def parse():
                    help="comma list of the halo modes timed after the headline at N>1: " + ", ".join(HALO_MODES))
     p.add_argument("--exchange-timeout", type=float, default=30.0, help="seconds before a mode's drain aborts")
     p.add_argument("--resident-loop", choices=["on", "off"], default="on",
-                   help="N>1, halo mode 'event': also time the reference's MPI loop on the resident bands (reps with "
-                        "the ghost rows exchanged every halo-depth reps through the transport, no PCIe), "
-                        "reported as halo_modes.event.resident_loop and resident_loop")
+                   help="N>1, halo modes 'event' and 'ipc': also time the reference's MPI loop on the resident bands "
+                        "(reps with the ghost rows exchanged every halo-depth reps through RCCL / HIP-IPC, no PCIe), "
+                        "reported as halo_modes.<mode>.resident_loop, resident_loop and resident_loop_ipc")
     p.add_argument("--halo-select", choices=["auto", "off", "exchange"] + list(HALO_MODES), default="auto",
                    help="N>1: report as the headline the fastest bit-exact halo mode when it is at least 3 %% faster "
                         "than the pre-loaded pipeline (auto; the halo mode chosen by measurement, like the kernel "
@@ -282,7 +282,7 @@ def mode_kwargs(a, mode: str, fuse: int) -> dict:
     return kw
 
 
-def resident_loop(blur, a) -> dict:
+def resident_loop(blur, a, ipc: bool = False) -> dict:
     """The reference's MPI loop (mpi/mpi_convolution.c:156-240, loop-only
     timing) on the bands already resident on the GPUs: `reps` repetitions
     with the ghost rows exchanged every `halo` repetitions through the
@@ -291,7 +291,10 @@ def resident_loop(blur, a) -> dict:
     transport (RCCL) the whole loop — exchanges and launches — replays as ONE
     cached graph per image (EngineOptions::capture_exchanges).  K loops
     between barriers, max over ranks; ghost contents are whatever the frames
-    hold (timing only: the pipelined mode's images were oracle-checked)."""
+    hold (timing only: the pipelined mode's images were oracle-checked).
+    `ipc`: the ghost rows pulled by the CUs from the neighbours' frames
+    through HIP-IPC instead (its own transports, `--ipc-pull` form), also
+    captured."""
     import numpy as np
     import torch
 
@@ -303,7 +306,14 @@ def resident_loop(blur, a) -> dict:
     eng = n.BandEngine.for_band(a.width, a.height, a.channels, a.filter, b, blur.device, halo=int(blur.engine.halo),
                                 fuse=int(blur.engine.fuse), overlap=False, variant=a.variant, graph=True,
                                 capture_exchanges=True)
-    if blur.comm is not None:
+    ts = []
+    if ipc:
+        from pconv.parallel.bootstrap import make_ipc_transports
+
+        ts = make_ipc_transports([eng], a.exchange_timeout, pull=a.ipc_pull)
+        eng.attach_transport(ts[0])
+        transport = f"ipc-{a.ipc_pull}"
+    elif blur.comm is not None:
         eng.attach_rccl(blur.comm)
         transport = "rccl"
     elif blur.transport is not None:
@@ -328,6 +338,8 @@ def resident_loop(blur, a) -> dict:
         once()
     eng.synchronize()
     torch.cuda.synchronize()
+    for x in ts:
+        x.check()  # a timed-out device-side wait raises
     elapsed = max_over_ranks(time.perf_counter() - t)
     st = eng.stats
     px = a.width * a.height * a.reps
@@ -337,7 +349,8 @@ def resident_loop(blur, a) -> dict:
            # per rank: the ghost rows it receives per exchange (both sides for an interior band)
            "ghost_bytes_per_exchange": gather_ints(int(eng.halo) * int(blur.row_bytes) *
                                                    (int(b.up >= 0) + int(b.down >= 0)))}
-    del eng
+    del ts, eng
+    barrier()  # every rank's transports are closed before any frame goes away
     return out
 
 
@@ -384,9 +397,9 @@ def measure_mode(a, mode, ref_rows, world, rank, device, transport, fuse, oracle
                    slot_streams=bool(xb.pipe.graphs), step_graphs=bool(xb.pipe.step_graphs),
                    concurrent_images=bool(xb.pipe.concurrent),
                    overlap_split=mode == "overlap" or (mode == "event" and not a.no_overlap))
-        if mode == "event" and a.resident_loop == "on":
+        if mode in ("event", "ipc") and a.resident_loop == "on":
             try:
-                res["resident_loop"] = resident_loop(xb, a)
+                res["resident_loop"] = resident_loop(xb, a, ipc=mode == "ipc")
             except Exception as e:  # noqa: BLE001  (the mode's own timing stands)
                 res["resident_loop"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     except Exception as e:  # reported, never fatal for the headline line
@@ -759,11 +772,11 @@ def main():
                 how = "IPC pulls of its own rows" if a.emulate_halo == "ipc" else "RCCL send/recv to self"
                 out["emulated"] += f"; halos exchanged with the rank itself ({how}): real exchange costs, ghost " \
                                    "contents not those of its neighbours"
-    if a.emulate and a.emulate_halo == "event" and a.resident_loop == "on":
-        # the resident MPI loop of this rank's band, ghost rows through RCCL send/recv to itself
-        rl = resident_loop(blur, a)
+    if a.emulate and a.emulate_halo in ("event", "ipc") and a.resident_loop == "on":
+        # the resident MPI loop of this rank's band, ghost rows through RCCL send/recv / IPC pulls to itself
+        rl = resident_loop(blur, a, ipc=a.emulate_halo == "ipc")
         if out is not None:
-            out["resident_loop"] = rl
+            out["resident_loop" if a.emulate_halo == "event" else "resident_loop_ipc"] = rl
 
     import threading
 
@@ -824,9 +837,11 @@ def main():
             pending["mode"] = None
             if out is not None:
                 results[m] = r
+        # the reference's loop-only MPI semantics, ghost rows crossing between the GPUs (RCCL / IPC)
         if out is not None and "resident_loop" in results.get("event", {}):
-            # the reference's loop-only MPI semantics, ghost rows crossing between the GPUs
             out["resident_loop"] = results["event"]["resident_loop"]
+        if out is not None and "resident_loop" in results.get("ipc", {}):
+            out["resident_loop_ipc"] = results["ipc"]["resident_loop"]
         # Halo mode chosen by measurement: every rank sees the same reduced
         # numbers, so they agree; rank 0 reports.
         if out is not None:

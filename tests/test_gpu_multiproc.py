@@ -120,6 +120,10 @@ def test_bench_torchrun_rehearsal(world, extra):
         assert rl["one_graph_per_image"] is False  # host-staged halos cannot be captured
         g = rl["ghost_bytes_per_exchange"]  # per rank: one side at the image edges, two inside
         assert len(g) == world and g[0] == g[-1] and all(x == 2 * g[0] for x in g[1:-1]), g
+        ri = meta["resident_loop_ipc"]  # the same loop with HIP-IPC pulls, captured
+        assert ri == modes["ipc"]["resident_loop"] and ri["transport"] == "ipc-grid", ri
+        assert ri["ms_per_image"] > 0 and ri["exchanges_per_image"] == rl["exchanges_per_image"], ri
+        assert ri["one_graph_per_image"] is True and ri["ghost_bytes_per_exchange"] == g
     # overlap: a T-deep ghost zone, one exchange per fused launch (the reference's per-rep loop, T at a time)
     assert modes["overlap"]["halo_depth"] == modes["overlap"]["fuse"]
     assert modes["overlap"]["exchanges_per_step"] >= 40 // modes["overlap"]["fuse"]
@@ -252,10 +256,11 @@ def test_bench_emulated_rank_halo_modes(halo):
     assert d["config"]["halo_mode"] == halo and d["ms_per_step"] > 0 and "8-way split" in d["emulated"]
     if halo == "preload":
         assert d["mismatches"] == 0
-    if halo == "event":
-        rl = d["resident_loop"]
-        assert rl["transport"] == "rccl" and rl["ms_per_image"] > 0 and rl["exchanges_per_image"] >= 1, rl
-        assert rl["one_graph_per_image"] is True  # RCCL send/recv captured with the launches
+    if halo in ("event", "ipc"):
+        rl = d["resident_loop" if halo == "event" else "resident_loop_ipc"]
+        assert rl["transport"] == ("rccl" if halo == "event" else "ipc-grid"), rl
+        assert rl["ms_per_image"] > 0 and rl["exchanges_per_image"] >= 1, rl
+        assert rl["one_graph_per_image"] is True  # the exchange captured with the launches
         assert rl["ghost_bytes_per_exchange"] == [2 * rl["halo_rows"] * 1920 * 3], rl
     else:
-        assert "resident_loop" not in d
+        assert "resident_loop" not in d and "resident_loop_ipc" not in d
