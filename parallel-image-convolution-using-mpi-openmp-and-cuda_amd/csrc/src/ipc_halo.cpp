@@ -111,6 +111,7 @@ void IpcHaloTransport::connect(const std::vector<uint8_t>& up_handles, const std
   PCONV_CHECK(!connected_, "ipc transport: already connected");
   const Band& b = eng_->band();
   const FrameLayout& L = eng_->layout();
+  // Returns true for a self-neighbour.
   auto open = [&](const std::vector<uint8_t>& hs, uint8_t** out, IpcMailbox** mail) {
     PCONV_CHECK(hs.size() == kIpcHandleBytes, "ipc transport: bad handle blob");
     if (hs == handles_) {
@@ -120,7 +121,7 @@ void IpcHaloTransport::connect(const std::vector<uint8_t>& up_handles, const std
       for (int i = 0; i < 2; ++i) out[i] = own_base_[i];
       *mail = reinterpret_cast<IpcMailbox*>(mail_.data());
       own_ = true;
-      return;
+      return true;
     }
     for (int i = 0; i < 3; ++i) {
       hipIpcMemHandle_t h;
@@ -132,18 +133,26 @@ void IpcHaloTransport::connect(const std::vector<uint8_t>& up_handles, const std
       else
         *mail = static_cast<IpcMailbox*>(p);
     }
+    return false;
+  };
+  // The neighbour's frame layout: a peer rank's band of the row split, or —
+  // for a self-neighbour — this engine's own frames.  (The emulated band of
+  // a W-way split carries world 1, so row_band(height, 1, 0) would describe
+  // the whole image: the first version read the "neighbour's" boundary rows
+  // that far past the band's own frame.)
+  auto peer_layout = [&](bool self, int peer) {
+    return self ? L : FrameLayout::make(L.row_bytes, row_band(eng_->geom().height, world_, peer).rows, L.halo);
   };
   if (b.up >= 0) {
     PCONV_CHECK(!up_handles.empty(), "ipc transport: band has an upper neighbour but no handles");
-    open(up_handles, peer_up_, &peer_mail_up_);
-    lay_up_ = FrameLayout::make(L.row_bytes, row_band(eng_->geom().height, world_, b.up).rows, L.halo);
-    PCONV_CHECK(lay_up_.pitch == L.pitch, "ipc transport: neighbour pitch differs");
+    lay_up_ = peer_layout(open(up_handles, peer_up_, &peer_mail_up_), b.up);
+    PCONV_CHECK(lay_up_.pitch == L.pitch && lay_up_.halo == L.halo, "ipc transport: neighbour frame layout differs");
   }
   if (b.down >= 0) {
     PCONV_CHECK(!down_handles.empty(), "ipc transport: band has a lower neighbour but no handles");
-    open(down_handles, peer_down_, &peer_mail_down_);
-    lay_down_ = FrameLayout::make(L.row_bytes, row_band(eng_->geom().height, world_, b.down).rows, L.halo);
-    PCONV_CHECK(lay_down_.pitch == L.pitch, "ipc transport: neighbour pitch differs");
+    lay_down_ = peer_layout(open(down_handles, peer_down_, &peer_mail_down_), b.down);
+    PCONV_CHECK(lay_down_.pitch == L.pitch && lay_down_.halo == L.halo,
+                "ipc transport: neighbour frame layout differs");
   }
   connected_ = true;
 }
@@ -154,6 +163,8 @@ void IpcHaloTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream
   const FrameLayout& L = e.layout();
   const Band& b = e.band();
   PCONV_CHECK(depth >= 1 && depth <= L.halo && depth <= b.rows, "ipc halo: bad depth");
+  PCONV_CHECK((b.up < 0 || depth <= lay_up_.rows) && (b.down < 0 || depth <= lay_down_.rows),
+              "ipc halo: depth exceeds a neighbour's band");
   const int me = rank_ * slots_ + slot_;
   const int up = b.up >= 0 ? b.up * slots_ + slot_ : -1;
   const int down = b.down >= 0 ? b.down * slots_ + slot_ : -1;

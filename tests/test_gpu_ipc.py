@@ -154,3 +154,46 @@ def test_ipc_pull_probe(pconv_mod, form, workgroups, host_source):
     n = pconv_mod.native
     ms = n.ipc_pull_probe(form, 40 * 5760, host_source, 20, 0, workgroups)
     assert 0 < ms < 50, ms
+
+
+@pytest.mark.parametrize("pull", ["grid", "single", "sdma"])
+@pytest.mark.parametrize("world,rank", [(8, 3), (4, 0), (2, 1)])
+def test_ipc_self_neighbour_emulated_band_byte_placement(pconv_mod, rng, pull, world, rank):
+    """The one-GPU emulation of rank `rank` of a `world`-way split (bench.py
+    --emulate W:R --emulate-halo ipc): its band carries world 1 with itself
+    as up and down neighbour, so the transport must take the neighbour's
+    frame layout from the engine itself, not from row_band(height, 1, 0)
+    (the whole image: the first version read that far past the band's
+    frame).  Ghost rows above = the band's own last `halo` rows, below = its
+    first `halo` rows, every byte; also captured in the rep-loop graph."""
+    import torch
+
+    from pconv.parallel.bootstrap import make_ipc_transports
+
+    n = pconv_mod.native
+    w, h, halo = 57, 400, 12
+    b = n.row_band(h, world, rank)
+    b.up, b.down, b.rank, b.world = 0, 0, 0, 1
+    eng = n.BandEngine.for_band(w, h, "rgb", "gaussian", b, 0, halo, 4, False, "auto", graph=True,
+                                capture_exchanges=True)
+    (t,) = make_ipc_transports([eng], 10.0, pull=pull)
+    eng.attach_transport(t)
+    rb = w * 3
+    owned = rng.integers(0, 256, size=(b.rows, rb), dtype=np.uint8)
+    eng.upload(owned.reshape(-1), 0, b.rows)
+    eng.exchange_now(eng.compute_stream)
+    eng.synchronize()
+    t.check()
+    got = np.empty((b.rows + 2 * halo, rb), np.uint8)
+    eng.read_frame(got.reshape(-1), -halo, b.rows + halo)
+    assert np.array_equal(got[:halo], owned[-halo:]), "ghost rows above"
+    assert np.array_equal(got[halo:halo + b.rows], owned)
+    assert np.array_equal(got[-halo:], owned[:halo]), "ghost rows below"
+    for _ in range(3):  # exchanges captured with the launches: capture, replay, other parity
+        eng.set_halo_valid(False)
+        eng.run(8)
+        eng.synchronize()
+        t.check()
+        assert eng.stats.exchanges >= 1 and eng.cached_graphs >= 1
+    del t, eng
+    torch.cuda.synchronize()
