@@ -202,7 +202,11 @@ void launch_ipc_exchange(IpcPull form, IpcMailbox* mine, IpcMailbox* up_mb, IpcM
   for (const void* p : {static_cast<const void*>(dst_up), static_cast<const void*>(src_up),
                         static_cast<const void*>(dst_down), static_cast<const void*>(src_down)})
     PCONV_CHECK(reinterpret_cast<uintptr_t>(p) % 16 == 0, "ipc exchange: unaligned row pointer");
-  PCONV_CHECK(!src_up == !up_mb && !src_down == !down_mb, "ipc exchange: rows without a mailbox (or the reverse)");
+  // rows need their neighbour's mailbox; a mailbox without rows only as this
+  // rank's own (a self-neighbour signalling both sides)
+  PCONV_CHECK((!src_up || up_mb) && (!src_down || down_mb) && (src_up || !up_mb || up_mb == mine) &&
+                  (src_down || !down_mb || down_mb == mine),
+              "ipc exchange: rows without a mailbox (or the reverse)");
   PCONV_CHECK((!src_up || dst_up) && (!src_down || dst_down), "ipc exchange: source without destination");
   auto* du = reinterpret_cast<uint4*>(dst_up);
   auto* dd = reinterpret_cast<uint4*>(dst_down);

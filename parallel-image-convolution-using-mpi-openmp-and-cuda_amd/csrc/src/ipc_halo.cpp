@@ -184,9 +184,15 @@ void IpcHaloTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream
   // allocations, which the runtime refuses as a captured SDMA copy: the grid
   // form pulls instead.
   const IpcPull form = pull_ == IpcPull::Sdma && own_ ? IpcPull::Grid : pull_;
-  launch_ipc_exchange(form, reinterpret_cast<IpcMailbox*>(mail_.data()), up >= 0 ? peer_mail_up_ : nullptr,
-                      down >= 0 ? peer_mail_down_ : nullptr, &dflags_[me].err, timeout_ticks_, dst_up, src_up,
-                      dst_down, src_down, static_cast<int64_t>(n), stream);
+  // Mailboxes: the neighbours'.  A self-neighbour signals its own mailbox on
+  // BOTH sides, rows or not: an emulated edge band has one neighbour (itself),
+  // and there is no upper rank to store the "lower neighbour's rows final"
+  // word its one-sided wait reads (the first version timed out).
+  auto* mine_mb = reinterpret_cast<IpcMailbox*>(mail_.data());
+  IpcMailbox* mb_up = own_ ? mine_mb : (up >= 0 ? peer_mail_up_ : nullptr);
+  IpcMailbox* mb_down = own_ ? mine_mb : (down >= 0 ? peer_mail_down_ : nullptr);
+  launch_ipc_exchange(form, mine_mb, mb_up, mb_down, &dflags_[me].err, timeout_ticks_, dst_up, src_up, dst_down,
+                      src_down, static_cast<int64_t>(n), stream);
   ++enqueued_;
 }
 
