@@ -314,6 +314,71 @@ void test_cli() {
   EXPECT(usage_text("conv").rfind("Error Input!", 0) == 0);
 }
 
+// Round-5 flags: every pipeline / kernel policy is a flag (no environment
+// variable changes behaviour), with its range checked.
+void test_cli_policy_flags() {
+  const auto d = parse_cli({"conv", "img.raw", "64", "48", "5", "grey"});
+  EXPECT(d.tune == -1 && d.ring_chunk_bytes == (int64_t(32) << 20) && d.auto_gpu_min_s == 0.1);
+  EXPECT(d.cu_mask_queues && d.head_on_slot_streams && d.ipc_pull == "grid" && d.numa_bind);
+  const auto c = parse_cli({"conv", "img.raw", "64", "48", "5", "grey", "--tune", "off", "--ring-chunk-bytes", "0",
+                            "--auto-gpu-min", "0.5", "--pool-queues", "--head-pool-streams", "--ipc-pull", "sdma",
+                            "--no-numa-bind", "--stream-chunks", "6", "--transport", "ipc"});
+  EXPECT(c.tune == 0 && c.ring_chunk_bytes == 0 && c.auto_gpu_min_s == 0.5);
+  EXPECT(!c.cu_mask_queues && !c.head_on_slot_streams && c.ipc_pull == "sdma" && !c.numa_bind);
+  EXPECT(c.stream_chunks == 6 && c.transport == "ipc");
+  EXPECT(parse_cli({"conv", "i", "8", "8", "1", "grey", "--tune", "on"}).tune == 1);
+  EXPECT(throws([] { parse_cli({"conv", "i", "8", "8", "1", "grey", "--ipc-pull", "warp"}); }));
+  EXPECT(throws([] { parse_cli({"conv", "i", "8", "8", "1", "grey", "--tune", "maybe"}); }));
+  EXPECT(throws([] { parse_cli({"conv", "i", "8", "8", "1", "grey", "--stream-chunks", "-1"}); }));  // wave mode removed
+  EXPECT(throws([] { parse_cli({"conv", "i", "8", "8", "1", "grey", "--ring-chunk-bytes", "-5"}); }));
+}
+
+// The streamed plan on CPU frames: uploads in chunks, every level advanced as
+// far as the uploaded rows allow (plan_streamed), the result equal to the
+// whole-image oracle — the schedule the GPU's head streaming runs.
+void test_streamed_plan_cpu() {
+  const Filter f = Filter::gaussian();
+  const int64_t w = 19, h = 53;
+  const int ch = 3;
+  const ImageGeom geo{w, h, Channels::Rgb};
+  const int64_t rb = geo.row_bytes();
+  const auto img = random_bytes(static_cast<size_t>(w * h * ch), 7);
+  for (int chunks : {2, 3, 4, 7})
+    for (int T : {1, 4, 8})
+      for (int reps : {1, 9, 20}) {
+        PlanConfig cfg;
+        cfg.halo_depth = T;
+        cfg.fuse = T;
+        cfg.overlap = false;
+        cfg = normalize_plan_config(cfg, 0, 16);
+        const Band band = row_band(h, 1, 0);
+        const auto ph = plan_band(band, reps, cfg);
+        const StreamPlan sp = plan_streamed(ph, 0, h, h, stream_cuts(0, h, chunks));
+        const FrameLayout lay = FrameLayout::make(rb, h, cfg.halo_depth);
+        std::vector<uint8_t> fr[2] = {std::vector<uint8_t>(static_cast<size_t>(lay.bytes()), 0),
+                                      std::vector<uint8_t>(static_cast<size_t>(lay.bytes()), 0)};
+        // rows are taken from the result frame right after the chunk that
+        // declares them final (down_lo/down_hi), as the GPU's downloads are
+        std::vector<uint8_t> got(img.size(), 0xEE);
+        const auto& out = fr[sp.levels & 1];
+        for (const auto& c : sp.chunks) {
+          for (int64_t row = c.up_lo; row < c.up_hi; ++row)
+            std::memcpy(fr[0].data() + lay.offset(row), img.data() + row * rb, rb);
+          for (size_t i = 0; i < c.launches.size(); ++i) {
+            const int src = (c.levels[i] - 1) & 1;
+            const auto& l = c.launches[i];
+            cpu_fused_launch(f, geo.channels, lay, fr[src].data(), fr[src ^ 1].data(), l.lo, l.hi, l.steps, 0, h,
+                             CpuBackend::Serial);
+          }
+          for (int64_t row = c.down_lo; row < c.down_hi; ++row)
+            std::memcpy(got.data() + row * rb, out.data() + lay.offset(row), rb);
+        }
+        const bool ok = got == naive(f, img, w, h, ch, reps);
+        if (!ok) std::fprintf(stderr, "streamed plan mismatch: chunks=%d T=%d reps=%d\n", chunks, T, reps);
+        EXPECT(ok);
+      }
+}
+
 }  // namespace
 
 int main() {
@@ -324,6 +389,8 @@ int main() {
   test_raw_io();
   test_synthetic();
   test_cli();
+  test_cli_policy_flags();
+  test_streamed_plan_cpu();
   std::printf("native tests: %d checks, %d failures\n", g_checks, g_failures);
   return g_failures ? 1 : 0;
 }
