@@ -81,9 +81,11 @@ class DistributedBlur:
         """Pipeline policy (native EngineOptions, echoed by bench.py's JSON
         config): `cu_mask_queues` puts every slot stream on its own hardware
         queue; `head_on_slot_streams` runs a streamed head image's copies on
-        the next slots' streams; `stream_min_bytes` (None: the native default,
-        8 MiB) is the smallest input head-streamed; `ipc_pull` is the IPC
-        transport's pull form (grid | single | sdma, ipc_halo.hpp)."""
+        the next slots' streams and `head_alt_uploads` alternates its chunk
+        uploads over two of them (>= 4 slots); `stream_min_bytes` (None: the
+        native default, 8 MiB) is the smallest input head-streamed;
+        `ipc_pull` is the IPC transport's pull form (grid | single | sdma,
+        ipc_halo.hpp)."""
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
