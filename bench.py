@@ -166,6 +166,12 @@ def parse():
                         "workgroups; single: one workgroup; sdma: flag kernels around SDMA peer copies)")
     p.add_argument("--numa-bind", choices=["on", "off"], default="on",
                    help="restrict each rank to its GPU's NUMA node (default on)")
+    p.add_argument("--diag-windows", type=int, default=8, metavar="W",
+                   help="after the timed region, replay the identical K-image window W times unmarked and W times "
+                        "with per-image completion marks; reported under 'windows' (0 = off)")
+    p.add_argument("--mark-timed", action="store_true",
+                   help="diagnostics: completion marks in the TIMED window too (adds one event per image; the "
+                        "line is flagged 'timed_window_marked')")
     p.add_argument("--native", action="store_true",
                    help="run the same serving step on the native stack: the in-tree `conv --bench` (ROCm's HIP "
                         "runtime, no torch; its fork launcher for N > 1) and print its JSON line")
@@ -479,6 +485,86 @@ def copy_floor_ms(in_bytes: int, out_bytes: int, device: int, iters: int = 8):
     return h2d, d2h
 
 
+def copy_floors(measure, world: int, rank: int):
+    """A copy floor per rank twice: SOLO (rank r measures while every other
+    rank waits between barriers, one rank at a time) and CONCURRENT (every
+    rank at once, between two barriers).  With one GPU per rank on its own
+    PCIe link, concurrent = solo; a larger concurrent floor means the ranks
+    share something on the host side (host DRAM bandwidth, a PCIe switch) —
+    what the first 8-GPU line must separate from link rates.  Every rank must
+    call it; returns (solo per rank, concurrent per rank)."""
+    from pconv.parallel.bootstrap import barrier
+
+    solo = -1.0
+    for r in range(world):
+        barrier()
+        if r == rank:
+            solo = measure()
+    barrier()
+    conc = measure() if world > 1 else solo
+    barrier()
+    return gather_floats(solo), gather_floats(conc)
+
+
+def kfd_queue_count():
+    """Hardware (HSA user-mode) queues this process holds, from the KFD's
+    per-process sysfs (None when not readable): slot streams on CU-masked
+    queues, the runtime's pool, and any queue torch or RCCL created."""
+    try:
+        return len(os.listdir(f"/sys/class/kfd/kfd/proc/{os.getpid()}/queues"))
+    except OSError:
+        return None
+
+
+def tuned_picks():
+    """The SWAR tuner's choice per launch key: [channels, steps, rows, row
+    bytes, step form, kernel (0 k_swar, 1 k_swar_pf), lanes, rows/wave, waves]."""
+    import pconv
+
+    return [list(k) + list(sh) for k, sh in pconv.native.swar_tuned()]
+
+
+def window_diagnostics(blur, a, count: int) -> dict:
+    """Replay the timed window (K images submitted to an idle pipeline,
+    drained, barriers + device syncs around it, max over ranks) `count` times
+    as it ran, then `count` times with per-image completion marks (one timing
+    event after each image on the stream it completes on).  The slowest and
+    fastest marked windows keep their per-image completion times, so a slow
+    window shows whether every image is slower (a rate) or a few stall (a gap).
+    Outside the timed region; diagnostics only."""
+    import torch
+
+    from pconv.parallel.bootstrap import barrier, max_over_ranks
+
+    def window(marked: bool):
+        if marked:
+            blur.pipe.enable_marks(a.steps)
+        barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.steps):
+            blur.submit(a.reps)
+        blur.drain()
+        torch.cuda.synchronize()
+        barrier()
+        ms = max_over_ranks(time.perf_counter() - t) / a.steps * 1e3
+        return ms, (blur.pipe.marks() if marked else None)
+
+    plain = [round(window(False)[0], 4) for _ in range(count)]
+    marked = [window(True) for _ in range(count)]
+
+    def detail(ms, rows):
+        done = [round(r[1], 4) for r in rows]
+        return {"ms_per_step": round(ms, 4), "slots": [int(r[0]) for r in rows],
+                "head_streamed": [int(r[2]) for r in rows], "completion_ms": done,
+                "deltas_ms": [round(y - x, 4) for x, y in zip([0.0] + done[:-1], done)]}
+
+    slow = max(marked, key=lambda m: m[0])
+    fast = min(marked, key=lambda m: m[0])
+    return {"ms_per_step": plain, "marked_ms_per_step": [round(m[0], 4) for m in marked],
+            "slowest_marked": detail(*slow), "fastest_marked": detail(*fast)}
+
+
 def hw_queue_budget(a) -> int:
     """GPU_MAX_HW_QUEUES for this process.  With CU-masked slot streams (the
     default) every image slot has its own dedicated hardware queue outside
@@ -612,6 +698,8 @@ def main():
 
     # ---- timed: K end-to-end steps (H2D + reps + D2H per image, `slots`
     # images in flight), all K complete inside the region; max over ranks
+    if a.mark_timed:
+        blur.pipe.enable_marks(a.steps)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -623,6 +711,10 @@ def main():
     mine = time.perf_counter() - t0
     elapsed = max_over_ranks(mine)
     per_rank = gather_floats(mine)  # diagnostics: load balance across ranks
+    timed_marks = blur.pipe.marks() if a.mark_timed else None
+    queues_at_timed = kfd_queue_count()
+    # ---- diagnostics (not timed): the same window replayed, plain and marked
+    windows = window_diagnostics(blur, a, a.diag_windows) if a.diag_windows > 0 else None
     # PCIe bytes per image of every rank (band + pre-loaded ghost rows in, owned rows out): whether an N>1
     # line is link-bound or host-memory-bound
     h2d_bytes, d2h_bytes = gather_ints(blur.h2d_bytes_per_image), gather_ints(blur.d2h_bytes_per_image)
@@ -659,13 +751,18 @@ def main():
     d2h_ms = max_over_ranks(d2h_ms / 1e3) * 1e3
     # ... and both directions at once, pitched like the pipeline's copies: the
     # floor a PCIe-bound step converges to (diagnostic only: never fatal)
-    try:
-        pair_ms = pconv.native.copy_pair_floor_ms(device, blur.row_bytes, blur.inputs[0].size // blur.row_bytes,
-                                                  b.rows, 8)
-    except Exception as e:  # noqa: BLE001
-        print(f"bench: copy pair floor not measured: {e}", file=sys.stderr)
-        pair_ms = -1.0
-    pair_ms = max_over_ranks(pair_ms / 1e3) * 1e3
+    def pair_floor():
+        try:
+            return pconv.native.copy_pair_floor_ms(device, blur.row_bytes, blur.inputs[0].size // blur.row_bytes,
+                                                   b.rows, 8)
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: copy pair floor not measured: {e}", file=sys.stderr)
+            return -1.0
+
+    # per rank: alone on the node (one rank at a time) and with every rank copying at once (N > 1: whether
+    # the ranks' host paths are independent, or share host DRAM / a switch)
+    pair_solo, pair_conc = copy_floors(pair_floor, ctx.world, ctx.rank)
+    pair_ms = max(pair_conc)
     if a.emulate:
         world = 1
 
@@ -744,7 +841,10 @@ def main():
                            "floor_ms": round(max(h2d_ms, d2h_ms), 4),
                            # one pitched H2D + one pitched D2H of a step issued together (the PCIe-bound
                            # pipeline's floor; null if the measurement failed)
-                           "pair_ms": round(pair_ms, 4) if pair_ms > 0 else None},
+                           "pair_ms": round(pair_ms, 4) if pair_ms > 0 else None,
+                           # per rank: alone (one rank at a time), and all ranks at once between two barriers
+                           "pair_ms_solo": [round(x, 4) for x in pair_solo],
+                           "pair_ms_concurrent": [round(x, 4) for x in pair_conc]},
             "loop_only": {
                 "ms_per_step": round(loop_elapsed / ls * 1e3, 4) if ls else None,
                 "mpix_per_s": round(loop_value, 2) if loop_value else None,  # (reps 0: copy-only diagnostics)
@@ -759,7 +859,16 @@ def main():
             "h2d_bytes_per_step": h2d_bytes,
             "d2h_bytes_per_step": d2h_bytes,
             "rank0_cpus_bound": cpu_bind,
+            # the timed window replayed (plain, then with per-image completion marks), the tuner's picks and
+            # the hardware queues this process held during the timed window: a slow window explains itself
+            "windows": windows,
+            "tuned": tuned_picks(),
+            "hw_queues": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"), "kfd_queues": queues_at_timed},
         }
+        if timed_marks is not None:
+            out["timed_window_marked"] = {"completion_ms": [round(r[1], 4) for r in timed_marks],
+                                          "slots": [int(r[0]) for r in timed_marks],
+                                          "head_streamed": [int(r[2]) for r in timed_marks]}
         if mismatches is not None:
             out["mismatches"] = mismatches
             out["check"] = "newest image of every rank vs the CPU oracle (OpenMP, bit-exact float32 semantics), " \

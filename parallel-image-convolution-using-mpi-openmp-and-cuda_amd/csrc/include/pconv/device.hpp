@@ -60,6 +60,9 @@ class DeviceBuffer {
  public:
   DeviceBuffer() = default;
   explicit DeviceBuffer(size_t bytes);
+  // hipExtMallocWithFlags (hipDeviceMallocFinegrained / hipDeviceMallocUncached):
+  // device memory with explicit coherence, e.g. words other GPUs store into.
+  DeviceBuffer(size_t bytes, unsigned flags);
   ~DeviceBuffer();
   DeviceBuffer(DeviceBuffer&& o) noexcept { *this = std::move(o); }
   DeviceBuffer& operator=(DeviceBuffer&& o) noexcept;

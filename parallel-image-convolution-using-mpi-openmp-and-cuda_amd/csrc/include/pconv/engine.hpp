@@ -304,9 +304,20 @@ class BandPipeline {
   // between the stages: a few microseconds per image of extra work.
   void enable_trace(int images);
   std::vector<std::vector<double>> trace();
+  // Completion marks (any mode, captured step graphs included): the next
+  // `images` submits each record a timing event on the stream their image
+  // completes on, right after the image's work (a marker between two graph
+  // launches; the graphs themselves are untouched), and the first also one
+  // before it.  marks() (after drain()) returns per image {slot, ms from the
+  // first image's issue to its completion, 1 if it was head-streamed}: a
+  // diagnostic pass only (bench.py's window replays), never the timed one.
+  void enable_marks(int images);
+  std::vector<std::vector<double>> marks();
 
  private:
   void trace_mark(int stage, hipStream_t s);
+  void completion_mark(int k, bool before, bool streamed);
+  void submit_image(int k, const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps);
   Stream h2d_, d2h_, comm_;
   std::vector<Stream> computes_;
   std::vector<Stream> slot_comms_;  // slot_comm: one communication stream per slot
@@ -327,6 +338,9 @@ class BandPipeline {
   std::vector<Event> trace_ev_;  // 4 per traced image
   std::vector<int> trace_slot_;
   int64_t trace_first_ = 0;
+  std::vector<Event> mark_ev_;  // [0] = before the first image, [1 + i] = image i done
+  std::vector<std::pair<int, bool>> mark_info_;  // (slot, head-streamed) per marked image
+  int64_t mark_first_ = 0;
 };
 
 // N row bands of one image on ONE device, halos moved by D2D copies.  Used to

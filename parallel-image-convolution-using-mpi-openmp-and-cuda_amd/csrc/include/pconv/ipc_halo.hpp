@@ -39,6 +39,21 @@
 //     copies cannot be skipped after a timed-out wait: a neighbour that
 //     stalls (but keeps its frames mapped) yields stale rows and the raised
 //     error, as in the other forms.
+// Visibility across devices.  The mailbox is UNCACHED device memory
+// (hipDeviceMallocUncached; fine-grained if the runtime cannot export that):
+// a neighbour's system-scope release store into it travels over xGMI to this
+// GPU's memory, and this rank's system-scope acquire poll reads memory, not a
+// cache line — no L2 of either GPU can hold a stale word.  The rows: the
+// neighbour's earlier kernels wrote them into its (coarse-grained) frames and
+// their end-of-kernel release wrote its L2 back before its signal store was
+// issued (stream order, and the store is a release); this rank's acquire
+// invalidates its own L2, so the pull reads the rows from the neighbour's
+// memory, not a line cached by an earlier exchange.  self_test() checks all of
+// it once at connect.
+// Sdma form and a neighbour that EXITS: its copies run even after a timed-out
+// wait, so a neighbour gone with its frames unmapped can fault a replay.  It
+// is never the default or a fallback; check() after every drain raises
+// before the next image is issued.
 // The exchange number lives in device memory, so a captured graph replays
 // correctly.  Every wait has a wall-clock timeout: an expired wait sets the
 // rank's error word (a host shared-memory segment the host checks) and
@@ -123,6 +138,19 @@ class IpcHaloTransport : public HaloTransport {
   // Open the neighbours' frames (empty vector: no neighbour on that side).
   void connect(const std::vector<uint8_t>& up_handles, const std::vector<uint8_t>& down_handles);
   bool connected() const { return connected_; }
+  // Collective with the neighbours (every rank calls it once per transport,
+  // in the same slot order, after every rank connected): one exchange of
+  // sentinel rows through the real protocol — signal words stored into the
+  // neighbours' mailboxes, rows pulled from their allocations, acks — with a
+  // short timeout, the pulled bytes compared.  Raises a named error at once
+  // (instead of the first real exchange timing out after timeout_s) when a
+  // neighbour's stores or rows are not visible to this rank.
+  void self_test(double timeout_s = 5.0);
+  bool self_tested() const { return self_tested_; }
+  // "uncached" | "fine-grained" | "coarse-grained" (the runtime exported neither)
+  const std::string& mailbox_kind() const { return mailbox_kind_; }
+  // The neighbours' devices (-1: none on that side; this device for a self-neighbour).
+  int peer_device(int side) const { return peer_dev_[side & 1]; }
 
   void exchange(BandEngine& e, int64_t depth, hipStream_t stream) override;
   const char* name() const override { return "ipc"; }
@@ -150,7 +178,12 @@ class IpcHaloTransport : public HaloTransport {
   bool connected_ = false;
   bool own_ = false;  // a neighbour is this engine itself (one-process emulation)
   IpcPull pull_ = IpcPull::Grid;
+  static constexpr size_t kMailboxBytes = size_t(2) << 20;
+  static constexpr int64_t kProbeOffset = 4096, kProbeBytes = 4096;  // self-test rows in the mailbox allocation
   DeviceBuffer mail_;                       // this rank's mailbox (exported)
+  std::string mailbox_kind_;
+  int peer_dev_[2] = {-1, -1};
+  bool self_tested_ = false;
   IpcMailbox* peer_mail_up_ = nullptr;      // the neighbours' mailboxes (opened)
   IpcMailbox* peer_mail_down_ = nullptr;
   uint8_t* own_base_[2] = {nullptr, nullptr};  // this engine's frames (the destructor never touches the engine)

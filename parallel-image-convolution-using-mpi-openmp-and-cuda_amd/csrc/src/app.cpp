@@ -652,6 +652,7 @@ void run_rank(const CliConfig& c, SharedState* sh, uint8_t* halo_slots, int64_t 
     ipct->connect(blob(b.up), blob(b.down));
     eng.set_transport(ipct);
     shm_barrier(sh, world, c.timeout_s);
+    ipct->self_test(std::min(5.0, c.timeout_s));  // fails fast, named, on a visibility gap
     if (rank == 0) ipc_unlink_segment(sh->ipc_segment);  // every rank has it mapped
   } else {
     if (rank == 0) {

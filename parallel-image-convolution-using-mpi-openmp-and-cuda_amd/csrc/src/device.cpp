@@ -116,6 +116,14 @@ DeviceBuffer::DeviceBuffer(size_t bytes) : bytes_(bytes) {
   }
 }
 
+DeviceBuffer::DeviceBuffer(size_t bytes, unsigned flags) : bytes_(bytes) {
+  if (bytes) {
+    void* p = nullptr;
+    PCONV_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, flags));
+    ptr_ = static_cast<uint8_t*>(p);
+  }
+}
+
 DeviceBuffer::~DeviceBuffer() {
   if (ptr_) (void)hipFree(ptr_);
 }

@@ -621,7 +621,52 @@ void BandPipeline::set_transport(std::shared_ptr<HaloTransport> t) {
 void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
   TraceRange tr("pconv.pipeline.submit");
   const int k = static_cast<int>(count_ % static_cast<int64_t>(slots_.size()));
-  BandEngine& e = *slots_[k];
+  if (mark_ev_.empty()) {
+    submit_image(k, host_in, in_r0, in_r1, host_out, reps);
+    return;
+  }
+  completion_mark(k, true, false);
+  const int64_t heads = streamed_heads_;
+  submit_image(k, host_in, in_r0, in_r1, host_out, reps);
+  completion_mark(k, false, streamed_heads_ != heads);
+}
+
+void BandPipeline::completion_mark(int k, bool before, bool streamed) {
+  const int64_t i = count_ - mark_first_ - (before ? 0 : 1);  // this image's index among the marked ones
+  if (i < 0 || i + 1 >= static_cast<int64_t>(mark_ev_.size())) return;
+  if (before && i != 0) return;
+  hipStream_t s = graphs_ ? slots_[static_cast<size_t>(k)]->compute_stream() : (before ? h2d_.get() : d2h_.get());
+  if (before) {
+    mark_ev_[0].record(s);
+    return;
+  }
+  mark_ev_[static_cast<size_t>(i + 1)].record(s);
+  mark_info_.emplace_back(k, streamed);
+}
+
+void BandPipeline::enable_marks(int images) {
+  PCONV_CHECK(images >= 0, "mark capacity must be >= 0");
+  mark_ev_.clear();
+  mark_info_.clear();
+  if (images == 0) return;
+  for (int i = 0; i <= images; ++i) mark_ev_.push_back(Event::create(true));
+  mark_first_ = count_;
+}
+
+std::vector<std::vector<double>> BandPipeline::marks() {
+  drain();
+  std::vector<std::vector<double>> out;
+  for (size_t i = 0; i < mark_info_.size(); ++i)
+    out.push_back({static_cast<double>(mark_info_[i].first), Event::elapsed_ms(mark_ev_[0], mark_ev_[i + 1]),
+                   mark_info_[i].second ? 1.0 : 0.0});
+  mark_ev_.clear();
+  mark_info_.clear();
+  return out;
+}
+
+void BandPipeline::submit_image(int k, const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
+                                int reps) {
+  BandEngine& e = *slots_[static_cast<size_t>(k)];
   if (graphs_ && !step_graphs_) {
     // Everything of this image on the slot's stream; halo exchanges (if the
     // ghost rows are not pre-loaded) through this slot's own transport, in

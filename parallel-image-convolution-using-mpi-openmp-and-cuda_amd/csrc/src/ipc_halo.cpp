@@ -80,10 +80,37 @@ IpcHaloTransport::IpcHaloTransport(BandEngine& e, const std::string& segment, in
   int khz = 0;
   PCONV_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e.options().device));
   timeout_ticks_ = static_cast<uint64_t>(timeout_s * static_cast<double>(khz > 0 ? khz : 100000) * 1000.0);
-  // A whole 2 MiB allocation (never sub-allocated by the runtime) so that
-  // its IPC handle names exactly this buffer.
-  mail_ = DeviceBuffer(size_t(2) << 20);
-  PCONV_HIP_CHECK(hipMemset(mail_.data(), 0, sizeof(IpcMailbox)));
+  // The mailbox: a whole 2 MiB allocation (never sub-allocated by the
+  // runtime, so its IPC handle names exactly this buffer) of UNCACHED device
+  // memory — neighbours on other GPUs store into it over xGMI, and no cache
+  // of either side may keep a stale copy (ipc_halo.hpp, "Visibility").
+  // Fine-grained memory is the second choice; plain (coarse-grained) memory
+  // only if the runtime exports neither, and then the connect self-test is
+  // what stands between a visibility gap and a 30 s timeout.
+  hipIpcMemHandle_t mh{};
+  const std::pair<unsigned, const char*> kinds[] = {{hipDeviceMallocUncached, "uncached"},
+                                                    {hipDeviceMallocFinegrained, "fine-grained"}};
+  for (const auto& k : kinds) {
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, kMailboxBytes, k.first) != hipSuccess) {
+      (void)hipGetLastError();
+      continue;
+    }
+    if (hipIpcGetMemHandle(&mh, p) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipFree(p);
+      continue;
+    }
+    (void)hipFree(p);  // exportable: allocate it for real (RAII) below
+    mail_ = DeviceBuffer(kMailboxBytes, k.first);
+    mailbox_kind_ = k.second;
+    break;
+  }
+  if (mailbox_kind_.empty()) {
+    mail_ = DeviceBuffer(kMailboxBytes);
+    mailbox_kind_ = "coarse-grained";
+  }
+  PCONV_HIP_CHECK(hipMemset(mail_.data(), 0, kMailboxBytes));
   PCONV_HIP_CHECK(hipDeviceSynchronize());  // zeroed before any neighbour can store into it
   handles_.resize(kIpcHandleBytes);
   for (int i = 0; i < 3; ++i) {
@@ -111,8 +138,16 @@ void IpcHaloTransport::connect(const std::vector<uint8_t>& up_handles, const std
   PCONV_CHECK(!connected_, "ipc transport: already connected");
   const Band& b = eng_->band();
   const FrameLayout& L = eng_->layout();
+  const int dev = eng_->options().device;
+  // A self-neighbour is self on EVERY side that has a neighbour (one-process
+  // emulation): exchange() then signals this rank's own mailbox on both
+  // sides.  A band with one self side and one real peer would signal itself
+  // instead of that peer and read the peer's rows without its level word.
+  const bool self_up = b.up >= 0 && up_handles == handles_, self_down = b.down >= 0 && down_handles == handles_;
+  PCONV_CHECK(!(self_up || self_down) || ((b.up < 0 || self_up) && (b.down < 0 || self_down)),
+              "ipc transport: a self-neighbour on one side and a peer rank on the other");
   // Returns true for a self-neighbour.
-  auto open = [&](const std::vector<uint8_t>& hs, uint8_t** out, IpcMailbox** mail) {
+  auto open = [&](const std::vector<uint8_t>& hs, uint8_t** out, IpcMailbox** mail, int* peer_dev) {
     PCONV_CHECK(hs.size() == kIpcHandleBytes, "ipc transport: bad handle blob");
     if (hs == handles_) {
       // This engine is its own neighbour (one-process emulation of a rank
@@ -120,6 +155,7 @@ void IpcHaloTransport::connect(const std::vector<uint8_t>& up_handles, const std
       // like RCCL send/recv to self).  A process cannot open its own handle.
       for (int i = 0; i < 2; ++i) out[i] = own_base_[i];
       *mail = reinterpret_cast<IpcMailbox*>(mail_.data());
+      *peer_dev = dev;
       own_ = true;
       return true;
     }
@@ -133,6 +169,17 @@ void IpcHaloTransport::connect(const std::vector<uint8_t>& up_handles, const std
       else
         *mail = static_cast<IpcMailbox*>(p);
     }
+    // The neighbour's device: on another GPU its frames and mailbox are
+    // reached over xGMI, which needs peer access between the two devices.
+    hipPointerAttribute_t at{};
+    PCONV_HIP_CHECK(hipPointerGetAttributes(&at, out[0]));
+    *peer_dev = at.device;
+    if (at.device != dev && at.device >= 0) {
+      int can = 0;
+      PCONV_HIP_CHECK(hipDeviceCanAccessPeer(&can, dev, at.device));
+      PCONV_CHECK(can != 0, "ipc transport: device " + std::to_string(dev) + " cannot access the neighbour's device " +
+                                std::to_string(at.device) + " (no peer path for its frames and mailbox)");
+    }
     return false;
   };
   // The neighbour's frame layout: a peer rank's band of the row split, or —
@@ -145,12 +192,12 @@ void IpcHaloTransport::connect(const std::vector<uint8_t>& up_handles, const std
   };
   if (b.up >= 0) {
     PCONV_CHECK(!up_handles.empty(), "ipc transport: band has an upper neighbour but no handles");
-    lay_up_ = peer_layout(open(up_handles, peer_up_, &peer_mail_up_), b.up);
+    lay_up_ = peer_layout(open(up_handles, peer_up_, &peer_mail_up_, &peer_dev_[0]), b.up);
     PCONV_CHECK(lay_up_.pitch == L.pitch && lay_up_.halo == L.halo, "ipc transport: neighbour frame layout differs");
   }
   if (b.down >= 0) {
     PCONV_CHECK(!down_handles.empty(), "ipc transport: band has a lower neighbour but no handles");
-    lay_down_ = peer_layout(open(down_handles, peer_down_, &peer_mail_down_), b.down);
+    lay_down_ = peer_layout(open(down_handles, peer_down_, &peer_mail_down_, &peer_dev_[1]), b.down);
     PCONV_CHECK(lay_down_.pitch == L.pitch && lay_down_.halo == L.halo,
                 "ipc transport: neighbour frame layout differs");
   }
@@ -194,6 +241,72 @@ void IpcHaloTransport::exchange(BandEngine& e, int64_t depth, hipStream_t stream
   launch_ipc_exchange(form, mine_mb, mb_up, mb_down, &dflags_[me].err, timeout_ticks_, dst_up, src_up, dst_down,
                       src_down, static_cast<int64_t>(n), stream);
   ++enqueued_;
+}
+
+namespace {
+
+// Connect self-test sentinel: byte i of (rank, slot)'s probe rows.
+uint8_t probe_byte(int rank, int slot, int64_t i) {
+  return static_cast<uint8_t>((rank * 131 + slot * 17 + i * 7 + 1) & 0xff);
+}
+
+}  // namespace
+
+void IpcHaloTransport::self_test(double timeout_s) {
+  TraceRange tr("pconv.halo.ipc_self_test");
+  PCONV_CHECK(connected_, "ipc transport: self-test before connect");
+  const Band& b = eng_->band();
+  if (b.up < 0 && b.down < 0) return;
+  set_device(eng_->options().device);
+  // Probe rows in the mailbox allocation past the signalling words: [out]
+  // this rank's sentinel, [in_up] / [in_down] what it pulls from its
+  // neighbours' [out].  The frames are never touched (they may hold data).
+  constexpr int64_t P = kProbeBytes;
+  uint8_t* base = mail_.data();
+  std::vector<uint8_t> out(static_cast<size_t>(P));
+  for (int64_t i = 0; i < P; ++i) out[static_cast<size_t>(i)] = probe_byte(rank_, slot_, i);
+  PCONV_HIP_CHECK(hipMemcpy(base + kProbeOffset, out.data(), out.size(), hipMemcpyHostToDevice));
+  PCONV_HIP_CHECK(hipMemset(base + kProbeOffset + P, 0, static_cast<size_t>(2 * P)));
+  PCONV_HIP_CHECK(hipDeviceSynchronize());
+  auto peer_probe = [&](IpcMailbox* m) { return reinterpret_cast<const uint8_t*>(m) + kProbeOffset; };
+  const uint8_t* src_up = b.up >= 0 ? peer_probe(peer_mail_up_) : nullptr;
+  const uint8_t* src_down = b.down >= 0 ? peer_probe(peer_mail_down_) : nullptr;
+  uint8_t* dst_up = b.up >= 0 ? base + kProbeOffset + P : nullptr;
+  uint8_t* dst_down = b.down >= 0 ? base + kProbeOffset + 2 * P : nullptr;
+  auto* mine_mb = reinterpret_cast<IpcMailbox*>(mail_.data());
+  IpcMailbox* mb_up = own_ ? mine_mb : (b.up >= 0 ? peer_mail_up_ : nullptr);
+  IpcMailbox* mb_down = own_ ? mine_mb : (b.down >= 0 ? peer_mail_down_ : nullptr);
+  int khz = 0;
+  PCONV_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, eng_->options().device));
+  const uint64_t ticks = static_cast<uint64_t>(timeout_s * static_cast<double>(khz > 0 ? khz : 100000) * 1000.0);
+  const IpcPull form = pull_ == IpcPull::Sdma && own_ ? IpcPull::Grid : pull_;
+  Stream st = Stream::create(0);
+  launch_ipc_exchange(form, mine_mb, mb_up, mb_down, &dflags_[rank_ * slots_ + slot_].err, ticks, dst_up, src_up,
+                      dst_down, src_down, P, st.get());
+  ++enqueued_;
+  PCONV_HIP_CHECK(hipStreamSynchronize(st.get()));
+  const auto* f = static_cast<const volatile IpcFlags*>(host_);
+  const uint32_t err = f[rank_ * slots_ + slot_].err;
+  const std::string who = "ipc transport connect self-test (rank " + std::to_string(rank_) + ", slot " +
+                          std::to_string(slot_) + ", device " + std::to_string(eng_->options().device) +
+                          ", neighbours' devices " + std::to_string(peer_dev_[0]) + " / " +
+                          std::to_string(peer_dev_[1]) + ", " + mailbox_kind_ + " mailbox): ";
+  PCONV_CHECK(err == 0, who + (err == 1 ? "no neighbour's level word became visible within " : "no neighbour's ack "
+                                                                                                "became visible within ") +
+                            std::to_string(timeout_s) + " s (a neighbour that is not running its self-test, or a "
+                                                        "store across devices this GPU's poll never observes)");
+  std::vector<uint8_t> in(static_cast<size_t>(2 * P));
+  PCONV_HIP_CHECK(hipMemcpy(in.data(), base + kProbeOffset + P, in.size(), hipMemcpyDeviceToHost));
+  for (int side = 0; side < 2; ++side) {
+    const int peer = side == 0 ? b.up : b.down;
+    if (peer < 0) continue;
+    const int pr = own_ ? rank_ : peer;
+    for (int64_t i = 0; i < P; ++i)
+      PCONV_CHECK(in[static_cast<size_t>(side * P + i)] == probe_byte(pr, slot_, i),
+                  who + "the sentinel rows pulled from the " + (side == 0 ? "upper" : "lower") +
+                      " neighbour differ at byte " + std::to_string(i) + " (a read across devices returned stale data)");
+  }
+  self_tested_ = true;
 }
 
 uint32_t IpcHaloTransport::device_count() const {

@@ -625,6 +625,10 @@ PYBIND11_MODULE(_pconv_native, m) {
           },
           py::arg("in_ptr"), py::arg("in_r0"), py::arg("in_r1"), py::arg("out_ptr"), py::arg("reps"))
       .def("drain", &BandPipeline::drain, py::call_guard<py::gil_scoped_release>())
+      .def("enable_marks", &BandPipeline::enable_marks, py::arg("images"),
+           "Completion marks of the next `images` submits (a diagnostic pass; see marks()).")
+      .def("marks", &BandPipeline::marks, py::call_guard<py::gil_scoped_release>(),
+           "Drain, then per marked image [slot, ms from the first image's issue to its completion, head-streamed].")
       .def_property_readonly("submitted", &BandPipeline::submitted)
       .def_property_readonly("concurrent", &BandPipeline::concurrent)
       .def_property_readonly("graphs", &BandPipeline::graphs)
@@ -702,6 +706,12 @@ PYBIND11_MODULE(_pconv_native, m) {
            },
            py::arg("up"), py::arg("down"))
       .def_property_readonly("connected", &IpcHaloTransport::connected)
+      .def("self_test", &IpcHaloTransport::self_test, py::arg("timeout_s") = 5.0,
+           py::call_guard<py::gil_scoped_release>(),
+           "collective: one exchange of sentinel rows with the neighbours, compared; raises a named error")
+      .def_property_readonly("self_tested", &IpcHaloTransport::self_tested)
+      .def_property_readonly("mailbox_kind", &IpcHaloTransport::mailbox_kind)
+      .def("peer_device", &IpcHaloTransport::peer_device, py::arg("side"))
       .def_property_readonly("enqueued", &IpcHaloTransport::enqueued)
       .def_property_readonly("device_count", &IpcHaloTransport::device_count)
       .def("check", &IpcHaloTransport::check, "raise if a wait of this rank timed out (after the stream drained)");

@@ -137,6 +137,12 @@ def make_ipc_transports(engines, timeout_s: float = 30.0, group=None, pull: str 
         down = every[b.down][k] if b.down >= 0 else b""
         t.connect(up, down)
     barrier(group)
+    # One exchange of sentinel rows per transport (slot order, like every
+    # rank): a neighbour's stores or rows this rank cannot see raise a named
+    # error now instead of timing out the first real exchange.
+    for t in ts:
+        t.self_test(min(5.0, float(timeout_s)))
+    barrier(group)
     return ts
 
 

@@ -280,3 +280,59 @@ def test_bench_policy_flags():
     kw = bench.policy_kwargs(a)
     assert kw == dict(cu_mask_queues=False, head_on_slot_streams=False, head_alt_uploads=True, ipc_pull="sdma")
     assert bench.mode_kwargs(a, "ipc", 8)["ipc_pull"] == "sdma"
+
+
+def _floor_worker(rank, world, port, q):
+    import importlib.util
+    import sys
+    import time
+
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        spec = importlib.util.spec_from_file_location("bench_floor", os.path.join(ROOT, "bench.py"))
+        bench = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(bench)
+        spans = []
+
+        def measure():  # a stand-in copy floor: 0.2 s of "copying", returns ms
+            t0 = time.time()
+            time.sleep(0.2)
+            spans.append((t0, time.time()))
+            return 200.0 + rank
+
+        solo, conc = bench.copy_floors(measure, world, rank)
+        q.put((rank, solo, conc, spans))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_copy_floors_solo_and_concurrent():
+    """bench.py's copy floors at N > 1: every rank measures
+    once ALONE (one rank at a time between barriers: no two solo spans
+    overlap) and once with all ranks AT ONCE (the concurrent spans all
+    overlap); both come back as per-rank lists on every rank, the fields
+    `pair_ms_solo` / `pair_ms_concurrent` of every N > 1 line."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_floor_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for rank, solo, conc, spans in res:
+        assert solo == [200.0, 201.0, 202.0] and conc == [200.0, 201.0, 202.0]
+        assert len(spans) == 2
+    solo_spans = sorted(r[3][0] for r in res)
+    for (a0, a1), (b0, b1) in zip(solo_spans, solo_spans[1:]):
+        assert a1 <= b0, "solo floors overlapped"
+    conc_spans = [r[3][1] for r in res]
+    assert max(s[0] for s in conc_spans) < min(s[1] for s in conc_spans), "concurrent floors did not overlap"

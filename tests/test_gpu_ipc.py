@@ -43,15 +43,21 @@ def _worker(rank, world, port, cfg, q):
 
     ctx = init_distributed("gloo")
     try:
+        if cfg.get("devices"):  # one GPU per rank (the 8-GPU node's layout)
+            import torch
+
+            torch.cuda.set_device(rank % cfg["devices"])
         blur = DistributedBlur(cfg["w"], cfg["h"], cfg["ch"], cfg["filter"], cfg["reps"], rank=rank, world=world,
-                               device=0, halo=cfg["halo"], fuse=cfg["fuse"], slots=cfg["slots"], transport="ipc",
+                               device=rank % cfg["devices"] if cfg.get("devices") else 0, halo=cfg["halo"], fuse=cfg["fuse"], slots=cfg["slots"], transport="ipc",
                                slot_exchange=True, graph_capture=cfg["graph"], slot_comm=cfg["overlap"],
                                overlap=cfg["overlap"], ipc_timeout_s=cfg.get("timeout", 30.0),
                                ipc_pull=cfg.get("pull", "grid"))
         assert all(t.pull == cfg.get("pull", "grid") for t in blur.ipc)
+        info = {"self_tested": [t.self_tested for t in blur.ipc], "mailbox": [t.mailbox_kind for t in blur.ipc],
+                "peer_devices": [(t.peer_device(0), t.peer_device(1)) for t in blur.ipc]}
         if cfg.get("stall") and rank == world - 1:
             barrier()  # set-up done; this rank then never exchanges
-            q.put((rank, None, None, 0))
+            q.put((rank, None, None, 0, info))
             barrier()
             return
         barrier()
@@ -64,7 +70,7 @@ def _worker(rank, world, port, cfg, q):
             err = str(e)
         outs = [blur.outputs[k].copy() for k in ks[-cfg["slots"]:]]
         # exchanges the device performed (graph replays included), summed over slots
-        q.put((rank, blur.band.y0, outs if err is None else err, sum(t.device_count for t in blur.ipc)))
+        q.put((rank, blur.band.y0, outs if err is None else err, sum(t.device_count for t in blur.ipc), info))
         barrier()  # every rank done with its neighbours' frames before any exits
         del blur
     finally:
@@ -116,11 +122,48 @@ def test_ipc_halo_bit_exact(pconv_mod, world, ch, filt, halo, fuse, reps, graph,
     img = pconv_mod.synthetic_image(w, h, ch, seed=11)
     ref = pconv_mod.numpy_convolve(img, reps, filt).reshape(h, -1)
     per_image = -(-reps // halo)  # exchanges per image (ghost zone of `halo` rows)
-    for rank, y0, outs, n_exch in res:
+    for rank, y0, outs, n_exch, info in res:
         assert not isinstance(outs, str), f"rank {rank}: {outs}"
         for o in outs:
             assert np.array_equal(o, ref[y0:y0 + o.shape[0]]), (rank, world)
-        assert n_exch == per_image * cfg["images"], (rank, n_exch)
+        # + the connect self-test's one exchange per slot
+        assert n_exch == per_image * cfg["images"] + slots, (rank, n_exch)
+        assert all(info["self_tested"]) and all(k in ("uncached", "fine-grained") for k in info["mailbox"]), info
+
+
+def test_ipc_connect_self_test_and_mailbox(pconv_mod):
+    """Every transport runs the connect self-test (sentinel rows through the
+    real protocol) and its mailbox is explicitly coherent device memory
+    (uncached, or fine-grained): the words a neighbour on another GPU stores
+    over xGMI.  Neighbours' devices are reported per side."""
+    cfg = dict(w=40, h=96, ch="rgb", filter="gaussian", reps=4, halo=4, fuse=4, slots=2, graph=True,
+               overlap=False, seed=5, images=2)
+    res = _run(pconv_mod, 3, cfg)
+    for rank, _, outs, _, info in res:
+        assert not isinstance(outs, str), outs
+        assert info["self_tested"] == [True, True], info
+        assert set(info["mailbox"]) <= {"uncached", "fine-grained"}, info
+        up, down = info["peer_devices"][0]
+        assert (up == 0) == (rank > 0) and (down == 0) == (rank < 2), info  # -1 where no neighbour
+
+
+def test_ipc_cross_device_exchange(pconv_mod):
+    """One rank per GPU (frames and mailboxes reached over xGMI): the
+    self-test and a bit-exact 2-way image.  Needs >= 2 visible GPUs."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs (the gpurun box has one)")
+    cfg = dict(w=57, h=160, ch="rgb", filter="gaussian", reps=19, halo=4, fuse=4, slots=2, graph=True,
+               overlap=True, seed=7, images=3, devices=2)
+    res = _run(pconv_mod, 2, cfg)
+    img = pconv_mod.synthetic_image(57, 160, "rgb", seed=7)
+    ref = pconv_mod.numpy_convolve(img, 19, "gaussian").reshape(160, -1)
+    for rank, y0, outs, _, info in res:
+        assert not isinstance(outs, str), outs
+        assert info["peer_devices"][0] == ((-1, 1) if rank == 0 else (0, -1)), info
+        for o in outs:
+            assert np.array_equal(o, ref[y0:y0 + o.shape[0]])
 
 
 @pytest.mark.parametrize("pull", ["grid", "single", "sdma"])
