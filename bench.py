@@ -136,6 +136,15 @@ def parse():
                    help="N>1, halo modes 'event' and 'ipc': also time the reference's MPI loop on the resident bands "
                         "(reps with the ghost rows exchanged every halo-depth reps through RCCL / HIP-IPC, no PCIe), "
                         "reported as halo_modes.<mode>.resident_loop, resident_loop and resident_loop_ipc")
+    p.add_argument("--resident-overlap", choices=["on", "off"], default="off",
+                   help="resident loop: split each exchange phase into the interior launch beside the exchange and "
+                        "the edge strips after it, captured as ONE graph with a fork/join (on), or exchange then "
+                        "launches in stream order (off, default: the forked graph measured 4-5x slower on this "
+                        "runtime, 0.33-0.42 vs 0.04-0.10 ms per image, profiles/r06/b/)")
+    p.add_argument("--resident-images", type=int, default=2,
+                   help="resident loop: this many independent images' loops concurrently (own engines, streams and "
+                        "transports) — one image's exchange overlaps another's launches; ms_per_image = elapsed / "
+                        "images; with more than one, 'one_image' holds the single-image loop too")
     p.add_argument("--halo-select", choices=["auto", "off", "exchange"] + list(HALO_MODES), default="auto",
                    help="N>1: report as the headline the fastest bit-exact halo mode when it is at least 3 %% faster "
                         "than the pre-loaded pipeline (auto; the halo mode chosen by measurement, like the kernel "
@@ -172,6 +181,10 @@ def parse():
     p.add_argument("--mark-timed", action="store_true",
                    help="diagnostics: completion marks in the TIMED window too (adds one event per image; the "
                         "line is flagged 'timed_window_marked')")
+    p.add_argument("--qualify-staging", choices=["on", "off"], default="on",
+                   help="time every slot's pinned staging buffers through the copy engines at set-up and replace any "
+                        "that copies >5%% slower than the best (DistributedBlur._qualify_staging); 'staging' in the "
+                        "JSON line")
     p.add_argument("--native", action="store_true",
                    help="run the same serving step on the native stack: the in-tree `conv --bench` (ROCm's HIP "
                         "runtime, no torch; its fork launcher for N > 1) and print its JSON line")
@@ -289,6 +302,19 @@ def mode_kwargs(a, mode: str, fuse: int) -> dict:
 
 
 def resident_loop(blur, a, ipc: bool = False) -> dict:
+    """The resident loop with `--resident-images` concurrent images (the
+    reported ms_per_image), and — when that is more than one — also one
+    image alone, the reference's single-image loop ('one_image')."""
+    nimg = max(1, int(a.resident_images))
+    out = resident_loop_n(blur, a, ipc, nimg)
+    if nimg > 1:
+        one = resident_loop_n(blur, a, ipc, 1)
+        out["one_image"] = {k: one[k] for k in ("ms_per_image", "mpix_per_s", "exchanges_per_image",
+                                                "launches_per_image")}
+    return out
+
+
+def resident_loop_n(blur, a, ipc: bool, nimg: int) -> dict:
     """The reference's MPI loop (mpi/mpi_convolution.c:156-240, loop-only
     timing) on the bands already resident on the GPUs: `reps` repetitions
     with the ghost rows exchanged every `halo` repetitions through the
@@ -305,57 +331,76 @@ def resident_loop(blur, a, ipc: bool = False) -> dict:
     import torch
 
     import pconv
-    from pconv.parallel.bootstrap import barrier, max_over_ranks
+    from pconv.parallel.bootstrap import barrier, make_rccl_comm, max_over_ranks
 
     n = pconv.native
     b = blur.band
-    eng = n.BandEngine.for_band(a.width, a.height, a.channels, a.filter, b, blur.device, halo=int(blur.engine.halo),
-                                fuse=int(blur.engine.fuse), overlap=False, variant=a.variant, graph=True,
-                                capture_exchanges=True)
-    ts = []
+    overlap = a.resident_overlap == "on"
+    # `nimg` independent images, each its own engine (frames, compute and
+    # communication streams) and its own transport, their loops concurrent
+    engs = [n.BandEngine.for_band(a.width, a.height, a.channels, a.filter, b, blur.device,
+                                  halo=int(blur.engine.halo), fuse=int(blur.engine.fuse), overlap=overlap,
+                                  variant=a.variant, graph=True, capture_exchanges=True) for _ in range(nimg)]
+    ts, comms = [], []
     if ipc:
         from pconv.parallel.bootstrap import make_ipc_transports
 
-        ts = make_ipc_transports([eng], a.exchange_timeout, pull=a.ipc_pull)
-        eng.attach_transport(ts[0])
+        ts = make_ipc_transports(engs, a.exchange_timeout, pull=a.ipc_pull)
+        for e, x in zip(engs, ts):
+            e.attach_transport(x)
         transport = f"ipc-{a.ipc_pull}"
     elif blur.comm is not None:
-        eng.attach_rccl(blur.comm)
+        comms = [blur.comm] + [make_rccl_comm(blur.device) for _ in range(nimg - 1)]
+        for e, c in zip(engs, comms):
+            e.attach_rccl(c)
         transport = "rccl"
     elif blur.transport is not None:
-        eng.attach_transport(blur.transport)
+        if nimg > 1:
+            raise RuntimeError("resident loop: concurrent images need a capturable transport (rccl, ipc)")
+        engs[0].attach_transport(blur.transport)
         transport = type(blur.transport).__name__
     else:
         raise RuntimeError("resident loop: the pipeline has no halo transport")
-    eng.upload(np.ascontiguousarray(blur.inputs[0][:b.rows]).reshape(-1), 0, b.rows)
+    for e in engs:
+        e.upload(np.ascontiguousarray(blur.inputs[0][:b.rows]).reshape(-1), 0, b.rows)
     steps = a.loop_steps if a.loop_steps is not None else a.steps
 
     def once():
-        eng.set_halo_valid(False)  # exchange every `halo` reps, as the reference does every rep
-        eng.run(a.reps)
+        for e in engs:
+            e.set_halo_valid(False)  # exchange every `halo` reps, as the reference does every rep
+            e.run(a.reps)
+
+    def sync():
+        for e in engs:
+            e.synchronize()
 
     for _ in range(2):  # the first run captures the graph (tuning first)
         once()
-    eng.synchronize()
+    sync()
     torch.cuda.synchronize()
     barrier()
     t = time.perf_counter()
     for _ in range(steps):
         once()
-    eng.synchronize()
+    sync()
     torch.cuda.synchronize()
     for x in ts:
         x.check()  # a timed-out device-side wait raises
     elapsed = max_over_ranks(time.perf_counter() - t)
+    eng = engs[0]
     st = eng.stats
     px = a.width * a.height * a.reps
-    out = {"ms_per_image": round(elapsed / steps * 1e3, 4), "mpix_per_s": round(px * steps / elapsed / 1e6, 2),
-           "steps": steps, "exchanges_per_image": int(st.exchanges), "launches_per_image": int(st.launches),
+    images = steps * nimg
+    out = {"ms_per_image": round(elapsed / images * 1e3, 4), "mpix_per_s": round(px * images / elapsed / 1e6, 2),
+           "steps": steps, "concurrent_images": nimg, "overlap_split": overlap,
+           "exchanges_per_image": int(st.exchanges), "launches_per_image": int(st.launches),
            "halo_rows": int(eng.halo), "one_graph_per_image": int(eng.cached_graphs) > 0, "transport": transport,
            # per rank: the ghost rows it receives per exchange (both sides for an interior band)
            "ghost_bytes_per_exchange": gather_ints(int(eng.halo) * int(blur.row_bytes) *
                                                    (int(b.up >= 0) + int(b.down >= 0)))}
-    del ts, eng
+    del ts, eng, engs
+    comms = comms[1:]
+    del comms
     barrier()  # every rank's transports are closed before any frame goes away
     return out
 
@@ -506,14 +551,37 @@ def copy_floors(measure, world: int, rank: int):
     return gather_floats(solo), gather_floats(conc)
 
 
+def staging_numa(blur) -> dict:
+    """NUMA placement of every slot's pinned staging pages (move_pages
+    query): {"gpu_node": n, "in": [{node: pages}...], "out": [...]}."""
+    try:
+        import pconv
+
+        n = pconv.native
+        node = lambda b: {str(k): v for k, v in n.page_nodes(b.ptr, len(b)).items()}  # noqa: E731
+        return {"gpu_node": n.device_numa_node(blur.device), "in": [node(b) for b in blur._in],
+                "out": [node(b) for b in blur._out]}
+    except Exception as e:  # noqa: BLE001  (diagnostics only)
+        return {"error": str(e)[:200]}
+
+
 def kfd_queue_count():
     """Hardware (HSA user-mode) queues this process holds, from the KFD's
     per-process sysfs (None when not readable): slot streams on CU-masked
     queues, the runtime's pool, and any queue torch or RCCL created."""
-    try:
-        return len(os.listdir(f"/sys/class/kfd/kfd/proc/{os.getpid()}/queues"))
+    pids = [os.getpid()]
+    try:  # the KFD names processes by their PID in the host's namespace: NSpid lists every level
+        for line in open("/proc/self/status"):
+            if line.startswith("NSpid:"):
+                pids = [int(x) for x in line.split()[1:]] + pids
     except OSError:
-        return None
+        pass
+    for pid in pids:
+        try:
+            return len(os.listdir(f"/sys/class/kfd/kfd/proc/{pid}/queues"))
+        except OSError:
+            continue
+    return None
 
 
 def tuned_picks():
@@ -561,8 +629,21 @@ def window_diagnostics(blur, a, count: int) -> dict:
 
     slow = max(marked, key=lambda m: m[0])
     fast = min(marked, key=lambda m: m[0])
-    return {"ms_per_step": plain, "marked_ms_per_step": [round(m[0], 4) for m in marked],
-            "slowest_marked": detail(*slow), "fastest_marked": detail(*fast)}
+    out = {"ms_per_step": plain, "marked_ms_per_step": [round(m[0], 4) for m in marked],
+           "slowest_marked": detail(*slow), "fastest_marked": detail(*fast)}
+    # each slot's own pinned staging buffers through the copy floor: H2D alone, D2H alone, the pair (a slot whose
+    # buffers copy slower than the others' shows here)
+    try:
+        import pconv
+
+        rows_in = blur.inputs[0].shape[0]
+        out["slot_buffer_copy_ms"] = [
+            [round(x, 4) for x in pconv.native.copy_floor_on(blur.device, blur._in[k].ptr, blur._out[k].ptr,
+                                                             blur.row_bytes, rows_in, blur.band.rows, 6)]
+            for k in range(blur.slots)]
+    except Exception as e:  # noqa: BLE001  (diagnostics only)
+        out["slot_buffer_copy_ms"] = f"not measured: {e}"[:200]
+    return out
 
 
 def hw_queue_budget(a) -> int:
@@ -603,6 +684,7 @@ def run_native(a) -> int:
     cmd += [] if a.cu_mask_queues else ["--pool-queues"]
     cmd += [] if a.head_on_slot_streams else ["--head-pool-streams"]
     cmd += [] if a.numa_bind == "on" else ["--no-numa-bind"]
+    cmd += [] if a.qualify_staging == "on" else ["--no-qualify-staging"]
     if a.emulate:
         cmd[cmd.index("--gpus") + 1] = "1"
         cmd += ["--emulate", a.emulate]  # one rank of a WORLD-way split, alone (per-rank proxy)
@@ -682,7 +764,8 @@ def main():
                                transport=head_transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
                                step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
                                graph_capture=a.graph_capture == "on", stream_chunks=a.stream_chunks,
-                               stream_min_bytes=int(a.stream_min_mb * 2 ** 20), **policy_kwargs(a))
+                               stream_min_bytes=int(a.stream_min_mb * 2 ** 20),
+                               qualify_staging=a.qualify_staging == "on", **policy_kwargs(a))
     blur.load_synthetic(a.seed)
     # --emulate-rccl: hold a (1-rank) RCCL communicator through the timed
     # region, as every real N>1 rank of the exchange path does.
@@ -835,6 +918,7 @@ def main():
                 "head_alt_uploads": bool(a.head_alt_uploads),
                 "ipc_pull": a.ipc_pull,
                 "numa_bind": a.numa_bind == "on",
+                "qualify_staging": a.qualify_staging == "on",
             },
             "latency_ms": round(latency_ms, 4),
             "copy_floor": {"h2d_ms": round(h2d_ms, 4), "d2h_ms": round(d2h_ms, 4),
@@ -864,6 +948,10 @@ def main():
             "windows": windows,
             "tuned": tuned_picks(),
             "hw_queues": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"), "kfd_queues": queues_at_timed},
+            # staging qualification (set-up): every slot's pinned buffers timed, slow ones replaced
+            "staging": blur.staging,
+            # where each slot's pinned pages live (NUMA node -> pages) and the GPU's own node
+            "staging_numa": staging_numa(blur),
         }
         if timed_marks is not None:
             out["timed_window_marked"] = {"completion_ms": [round(r[1], 4) for r in timed_marks],

@@ -70,6 +70,7 @@ struct CliConfig {
   bool head_on_slot_streams = true;       // --bench: streamed head image's copies on the next slots' streams
   std::string ipc_pull = "grid";          // --transport ipc: pull form (grid | single | sdma)
   bool numa_bind = true;                  // N > 1: each rank on its GPU's NUMA node
+  bool qualify_staging = true;            // --bench: time every slot's pinned buffers, replace slow ones
 };
 
 // Parse argv.  Throws pconv::Error with the message to print on bad input.

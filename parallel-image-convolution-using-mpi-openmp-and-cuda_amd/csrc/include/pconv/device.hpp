@@ -11,6 +11,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <map>
 #include <string>
 #include <utility>
 #include <vector>
@@ -55,6 +56,36 @@ int bind_to_device_numa(int device);
 // (~94 GB/s in both directions together on the measured boxes), so this, not
 // the slower solo copy, is what a PCIe-bound step converges to.
 double copy_pair_floor_ms(int device, int64_t row_bytes, int64_t rows_in, int64_t rows_out, int iters);
+// The same copies from / into GIVEN pinned host buffers (nullptr: fresh
+// ones), each direction alone and both together, ms per copy / pair: whether
+// one slot's staging buffers are slower than another's.
+// NUMA node of every page of a host range (move_pages(2) query, nothing
+// moved): node -> pages; a negative key is -errno for pages the kernel could
+// not report, <= -1000 when the query itself failed.  And a GPU's own node
+// (sysfs numa_node of its PCI function, -1 if unknown).
+std::map<int, int64_t> page_nodes(const void* p, size_t bytes);
+int device_numa_node(int device);
+struct CopyFloor {
+  double h2d_ms = 0, d2h_ms = 0, pair_ms = 0;
+};
+CopyFloor copy_floor_on(int device, uint8_t* host_in, uint8_t* host_out, int64_t row_bytes, int64_t rows_in,
+                        int64_t rows_out, int iters);
+
+class PinnedBuffer;
+// Staging qualification (the C++ twin of DistributedBlur._qualify_staging,
+// for `conv --bench`): every slot's pinned input / output buffer through the
+// copy engines once; a buffer more than `tolerance` slower than the best of
+// its direction is replaced by a fresh allocation (rejected ones held until
+// the search ends), up to `attempts` rounds.  Measured on MI355X boxes: in
+// some processes one pinned buffer uploads at ~42 instead of ~55 GB/s and
+// paces a whole pipeline (docs/ROUND6.md §1).
+struct StagingReport {
+  std::vector<CopyFloor> first, final;
+  int replaced = 0;
+};
+StagingReport qualify_staging(int device, std::vector<PinnedBuffer>& ins, std::vector<PinnedBuffer>& outs,
+                              int64_t row_bytes, int64_t rows_in, int64_t rows_out, double tolerance = 1.05,
+                              int attempts = 3);
 
 class DeviceBuffer {
  public:

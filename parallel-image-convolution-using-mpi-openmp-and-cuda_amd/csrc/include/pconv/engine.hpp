@@ -56,7 +56,10 @@ struct EngineOptions {
   // communication stream) and, with a capturable transport (RCCL, IPC), are
   // captured with the launches into the cached rep-loop graph — the
   // reference's MPI loop on resident bands as one graph launch per image
-  // (bench.py resident_loop).
+  // (bench.py resident_loop).  With `overlap` the engine keeps a
+  // communication stream and each exchange phase is captured as a fork: the
+  // interior launch beside the exchange, the edge strips after it (the
+  // reference's Isend/Irecv + inner compute + Wait + edges, one graph).
   bool capture_exchanges = false;
   KernelVariant variant = KernelVariant::Auto;
   // Borrowed streams (nullptr: the engine creates its own).  A process has

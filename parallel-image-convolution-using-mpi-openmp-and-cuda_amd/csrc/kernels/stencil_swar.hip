@@ -248,7 +248,11 @@ __global__ __launch_bounds__(64 * NW) void k_swar_pf(const uint8_t* __restrict__
   }
 }
 
-// Instantiated tile shapes (LW, M, NW).
+// Instantiated tile shapes (LW, M, NW).  Taller tiles for large frames
+// (fewer ghost rows per tile) were built and timed on 32768^2 grey at fuse 12
+// in round 6 and all lost to {4,20,8} (105.4 us/rep): {4,24,8} 110.4-141.6
+// (3 waves/SIMD), {4,16,16} 133-137, {4,20,16} 126.6-135.8 (one 16-wave
+// workgroup per CU: barrier across 16 waves); profiles/r06/b/shape_sweep.jsonl.
 constexpr SwarShape kShapes[] = {
     {8, 8, 8}, {8, 8, 4}, {8, 16, 4}, {8, 4, 8},              // 8-byte lanes: large images
     {4, 8, 8}, {4, 6, 8}, {4, 5, 8}, {4, 4, 8}, {4, 3, 8}, {4, 4, 16},  // 4-byte lanes: small bands

@@ -869,6 +869,8 @@ void bench_rank(const CliConfig& c, BenchShared* sh, uint8_t* image, int rank) {
     ins.emplace_back(static_cast<size_t>(in_rows * rb));
     outs.emplace_back(static_cast<size_t>(b.rows * rb));
   }
+  // set-up: a slow pinned buffer would pace the whole pipeline (docs/ROUND6.md §1)
+  if (c.qualify_staging) (void)qualify_staging(device, ins, outs, rb, in_rows, b.rows);
   load_rows(c, g, b.y0 - above, in_rows, ins[0].data(), rb);
   for (int k = 1; k < c.slots; ++k) std::memcpy(ins[k].data(), ins[0].data(), ins[0].size());
   int64_t n = 0;

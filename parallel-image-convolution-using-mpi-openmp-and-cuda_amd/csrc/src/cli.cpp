@@ -75,6 +75,8 @@ std::string help_text(const std::string& prog) {
          "  --tune {auto,on,off}      SWAR tile-shape tuning (auto: off for a one-shot run, on in a server)\n"
          "  --ring-chunk-bytes B      one-shot staging ring chunk (default 32 MiB; 0 = one pinned image)\n"
          "  --no-numa-bind            N > 1: leave each rank's CPU affinity alone\n"
+         "  --no-qualify-staging      --bench: keep the first pinned staging buffers (default: time each slot's\n"
+         "                            buffers at set-up and replace any >5% slower than the best)\n"
 
          "\n"
          "       " + prog + " --serve SOCKET [--device D] [--idle-timeout S] [--max-engines N]\n"
@@ -204,6 +206,8 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       if (v.empty() || *end != '\0' || !(c.auto_gpu_min_s >= 0)) PCONV_FAIL("invalid --auto-gpu-min '" + v + "'");
     } else if (a == "--no-numa-bind") {
       c.numa_bind = false;
+    } else if (a == "--no-qualify-staging") {
+      c.qualify_staging = false;
     } else if (a == "--warmup") {
       c.warmup = static_cast<int>(parse_int(next("--warmup"), "--warmup", 0, 100));
     } else {

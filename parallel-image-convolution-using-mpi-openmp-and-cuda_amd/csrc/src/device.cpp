@@ -3,8 +3,13 @@
 
 #include <dlfcn.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
+#include <map>
+#include <vector>
 #include <cctype>
 #include <cstdlib>
 #include <fstream>
@@ -72,25 +77,63 @@ int bind_to_device_numa(int device) {
   return sched_setaffinity(0, sizeof(keep), &keep) == 0 ? n : 0;
 }
 
-double copy_pair_floor_ms(int device, int64_t row_bytes, int64_t rows_in, int64_t rows_out, int iters) {
-  PCONV_CHECK(row_bytes > 0 && rows_in > 0 && rows_out > 0 && iters > 0, "copy_pair_floor_ms: empty copy");
+std::map<int, int64_t> page_nodes(const void* p, size_t bytes) {
+  std::map<int, int64_t> out;
+  const long page = sysconf(_SC_PAGESIZE);
+  if (!p || bytes == 0 || page <= 0) return out;
+  const uintptr_t a0 = reinterpret_cast<uintptr_t>(p) / static_cast<uintptr_t>(page) * static_cast<uintptr_t>(page);
+  const uintptr_t a1 = reinterpret_cast<uintptr_t>(p) + bytes;
+  std::vector<void*> pages;
+  for (uintptr_t a = a0; a < a1; a += static_cast<uintptr_t>(page)) pages.push_back(reinterpret_cast<void*>(a));
+  std::vector<int> status(pages.size(), -1);
+  // move_pages with no target nodes only reports where each page lives
+  const long r = syscall(SYS_move_pages, 0, static_cast<unsigned long>(pages.size()), pages.data(), nullptr,
+                         status.data(), 0);
+  if (r != 0) {
+    out[-1000 - errno] = static_cast<int64_t>(pages.size());  // the query itself failed (errno encoded)
+    return out;
+  }
+  for (int st : status) ++out[st];  // node, or -errno for a page the kernel cannot report
+  return out;
+}
+
+int device_numa_node(int device) {
+  std::ifstream f("/sys/bus/pci/devices/" + device_pci_bus_id(device) + "/numa_node");
+  int n = -1;
+  if (f) f >> n;
+  return n;
+}
+
+CopyFloor copy_floor_on(int device, uint8_t* host_in, uint8_t* host_out, int64_t row_bytes, int64_t rows_in,
+                        int64_t rows_out, int iters) {
+  PCONV_CHECK(row_bytes > 0 && rows_in > 0 && rows_out > 0 && iters > 0, "copy floor: empty copy");
   set_device(device);
   const int64_t pitch = (row_bytes + 16 + 127) / 128 * 128;  // a padded frame pitch like the engine's
   DeviceBuffer din(static_cast<size_t>(pitch * rows_in)), dout(static_cast<size_t>(pitch * rows_out));
-  PinnedBuffer hin(static_cast<size_t>(row_bytes * rows_in)), hout(static_cast<size_t>(row_bytes * rows_out));
+  PinnedBuffer hin_own, hout_own;
+  if (!host_in) {
+    hin_own = PinnedBuffer(static_cast<size_t>(row_bytes * rows_in));
+    host_in = hin_own.data();
+  }
+  if (!host_out) {
+    hout_own = PinnedBuffer(static_cast<size_t>(row_bytes * rows_out));
+    host_out = hout_own.data();
+  }
   Stream s1 = Stream::create(0), s2 = Stream::create(0);
   Event e0 = Event::create(true), a = Event::create(true), b = Event::create(true);
-  auto pairs = [&](int n) {
+  auto run = [&](int n, bool up, bool down) {
     PCONV_HIP_CHECK(hipDeviceSynchronize());
     e0.record(s1.get());
     e0.wait_on(s2.get());
     for (int i = 0; i < n; ++i) {
-      PCONV_HIP_CHECK(hipMemcpy2DAsync(din.data() + 16, static_cast<size_t>(pitch), hin.data(),
-                                       static_cast<size_t>(row_bytes), static_cast<size_t>(row_bytes),
-                                       static_cast<size_t>(rows_in), hipMemcpyHostToDevice, s1.get()));
-      PCONV_HIP_CHECK(hipMemcpy2DAsync(hout.data(), static_cast<size_t>(row_bytes), dout.data() + 16,
-                                       static_cast<size_t>(pitch), static_cast<size_t>(row_bytes),
-                                       static_cast<size_t>(rows_out), hipMemcpyDeviceToHost, s2.get()));
+      if (up)
+        PCONV_HIP_CHECK(hipMemcpy2DAsync(din.data() + 16, static_cast<size_t>(pitch), host_in,
+                                         static_cast<size_t>(row_bytes), static_cast<size_t>(row_bytes),
+                                         static_cast<size_t>(rows_in), hipMemcpyHostToDevice, s1.get()));
+      if (down)
+        PCONV_HIP_CHECK(hipMemcpy2DAsync(host_out, static_cast<size_t>(row_bytes), dout.data() + 16,
+                                         static_cast<size_t>(pitch), static_cast<size_t>(row_bytes),
+                                         static_cast<size_t>(rows_out), hipMemcpyDeviceToHost, s2.get()));
     }
     a.record(s1.get());
     b.record(s2.get());
@@ -98,8 +141,55 @@ double copy_pair_floor_ms(int device, int64_t row_bytes, int64_t rows_in, int64_
     b.sync();
     return std::max(Event::elapsed_ms(e0, a), Event::elapsed_ms(e0, b)) / n;
   };
-  (void)pairs(2);  // warm: first-use queue / engine set-up
-  return std::min(pairs(iters), pairs(iters));
+  (void)run(2, true, true);  // warm: first-use queue / engine set-up
+  CopyFloor f;
+  f.h2d_ms = std::min(run(iters, true, false), run(iters, true, false));
+  f.d2h_ms = std::min(run(iters, false, true), run(iters, false, true));
+  f.pair_ms = std::min(run(iters, true, true), run(iters, true, true));
+  return f;
+}
+
+StagingReport qualify_staging(int device, std::vector<PinnedBuffer>& ins, std::vector<PinnedBuffer>& outs,
+                              int64_t row_bytes, int64_t rows_in, int64_t rows_out, double tolerance, int attempts) {
+  PCONV_CHECK(ins.size() == outs.size() && !ins.empty(), "qualify_staging: one input and one output per slot");
+  auto rates = [&] {
+    std::vector<CopyFloor> r;
+    for (size_t k = 0; k < ins.size(); ++k)
+      r.push_back(copy_floor_on(device, ins[k].data(), outs[k].data(), row_bytes, rows_in, rows_out, 4));
+    return r;
+  };
+  StagingReport rep;
+  rep.first = rates();
+  rep.final = rep.first;
+  std::vector<PinnedBuffer> held;  // rejected buffers stay allocated until the search ends
+  for (int a = 0; a < attempts; ++a) {
+    double bh = 1e30, bd = 1e30;
+    for (const auto& f : rep.final) {
+      bh = std::min(bh, f.h2d_ms);
+      bd = std::min(bd, f.d2h_ms);
+    }
+    int bad = 0;
+    for (size_t k = 0; k < ins.size(); ++k) {
+      if (rep.final[k].h2d_ms > tolerance * bh) {
+        held.push_back(std::move(ins[k]));
+        ins[k] = PinnedBuffer(static_cast<size_t>(rows_in * row_bytes));
+        ++bad;
+      }
+      if (rep.final[k].d2h_ms > tolerance * bd) {
+        held.push_back(std::move(outs[k]));
+        outs[k] = PinnedBuffer(static_cast<size_t>(rows_out * row_bytes));
+        ++bad;
+      }
+    }
+    if (bad == 0) break;
+    rep.replaced += bad;
+    rep.final = rates();
+  }
+  return rep;
+}
+
+double copy_pair_floor_ms(int device, int64_t row_bytes, int64_t rows_in, int64_t rows_out, int iters) {
+  return copy_floor_on(device, nullptr, nullptr, row_bytes, rows_in, rows_out, iters).pair_ms;
 }
 
 std::string device_name(int device) {

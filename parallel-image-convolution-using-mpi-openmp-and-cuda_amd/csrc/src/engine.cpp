@@ -54,7 +54,9 @@ BandEngine::BandEngine(const ImageGeom& geom, const Band& band, const Filter& fi
   // Communication stream only when the band has neighbours (or is borrowed).
   if (opt_.comm_stream) {
     ms_ = opt_.comm_stream;
-  } else if ((band_.up >= 0 || band_.down >= 0) && !opt_.capture_exchanges) {
+  } else if ((band_.up >= 0 || band_.down >= 0) && (!opt_.capture_exchanges || opt_.overlap)) {
+    // (captured exchanges with overlap: the interior launch of an exchange
+    // phase is forked onto this stream inside the capture, enqueue_phase)
     own_ms_ = Stream::create(-1);  // communication gets the higher priority
     ms_ = own_ms_.get();
   } else {
@@ -290,9 +292,11 @@ void BandEngine::run(int reps) {
   wall_t0_ = wall_seconds();
   if (opt_.timing) ev_t0_.record(cs_);
   bool graph = opt_.use_graph && !ph.empty();
-  // exchanges join the graph only on the compute stream and through a
-  // capturable transport (opt_.capture_exchanges)
-  const bool cap_x = opt_.capture_exchanges && ms_ == cs_ && transport_ && transport_->capturable();
+  // exchanges join the graph only through a capturable transport
+  // (opt_.capture_exchanges): on the compute stream, or — with a
+  // communication stream (overlap) — forked: the exchange on the capturing
+  // stream beside the interior launch, the edges after it (enqueue_phase)
+  const bool cap_x = opt_.capture_exchanges && transport_ && transport_->capturable();
   for (const auto& p : ph) graph = graph && (p.exchange_depth == 0 || cap_x);
   if (graph) {
     const auto key = std::make_pair(reps, cur_);
@@ -465,6 +469,9 @@ void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in
     StepGraph sg;
     PCONV_HIP_CHECK(hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0));
     PCONV_HIP_CHECK(hipGraphDestroy(g));
+    // its device-side set-up now, not inside the first launch (a slot's graph
+    // runs its first image in the warm-up, its second in a timed window)
+    PCONV_HIP_CHECK(hipGraphUpload(sg.exec, cs_));
     sg.end_cur = cur_;
     sg.launches = stats_.launches;
     sg.exchanges = stats_.exchanges;

@@ -303,6 +303,22 @@ PYBIND11_MODULE(_pconv_native, m) {
   m.def("copy_pair_floor_ms", &copy_pair_floor_ms, py::arg("device"), py::arg("row_bytes"), py::arg("rows_in"),
         py::arg("rows_out"), py::arg("iters") = 8,
         "ms per pitched H2D + D2H pair issued concurrently on two streams (the pipeline's PCIe floor)");
+  m.def(
+      "page_nodes", [](uintptr_t p, size_t bytes) { return page_nodes(reinterpret_cast<const void*>(p), bytes); },
+      py::arg("ptr"), py::arg("bytes"), "NUMA node -> pages of a host range (move_pages query; negative: -errno)");
+  m.def("device_numa_node", &device_numa_node, py::arg("device"));
+  m.def(
+      "copy_floor_on",
+      [](int device, uintptr_t host_in, uintptr_t host_out, int64_t row_bytes, int64_t rows_in, int64_t rows_out,
+         int iters) {
+        py::gil_scoped_release nogil;
+        const CopyFloor f = copy_floor_on(device, reinterpret_cast<uint8_t*>(host_in),
+                                          reinterpret_cast<uint8_t*>(host_out), row_bytes, rows_in, rows_out, iters);
+        return std::make_tuple(f.h2d_ms, f.d2h_ms, f.pair_ms);
+      },
+      py::arg("device"), py::arg("host_in"), py::arg("host_out"), py::arg("row_bytes"), py::arg("rows_in"),
+      py::arg("rows_out"), py::arg("iters") = 8,
+      "(H2D alone, D2H alone, concurrent pair) ms with the given pinned host buffers (0: fresh ones)");
   m.def("bind_to_device_numa", &bind_to_device_numa,
         "Restrict this process to the CPUs local to the GPU (returns the CPUs kept; 0: unchanged)");
 

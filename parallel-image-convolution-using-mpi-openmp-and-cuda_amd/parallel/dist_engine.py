@@ -77,7 +77,7 @@ class DistributedBlur:
                  self_neighbours: bool = False, slot_comm: bool = False, stream_chunks: int = 0,
                  ipc_timeout_s: float = 30.0, ipc_pull: str = "grid", cu_mask_queues: bool = True,
                  head_on_slot_streams: bool = True, stream_min_bytes: Optional[int] = None,
-                 head_alt_uploads: bool = True):
+                 head_alt_uploads: bool = True, qualify_staging: bool = False):
         """Pipeline policy (native EngineOptions, echoed by bench.py's JSON
         config): `cu_mask_queues` puts every slot stream on its own hardware
         queue; `head_on_slot_streams` runs a streamed head image's copies on
@@ -85,7 +85,9 @@ class DistributedBlur:
         uploads over two of them (>= 4 slots); `stream_min_bytes` (None: the
         native default, 8 MiB) is the smallest input head-streamed;
         `ipc_pull` is the IPC transport's pull form (grid | single | sdma,
-        ipc_halo.hpp)."""
+        ipc_halo.hpp).  `qualify_staging`: time every slot's pinned staging
+        buffers through the copy engines once and replace any that copies
+        slower than the best (see _qualify_staging)."""
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
@@ -170,6 +172,9 @@ class DistributedBlur:
         # one pinned input/output buffer per slot (in-flight images never share)
         self._in = [n.PinnedBuffer(in_rows * self.row_bytes) for _ in range(self.slots)]
         self._out = [n.PinnedBuffer(b.rows * self.row_bytes) for _ in range(self.slots)]
+        self.staging = None
+        if qualify_staging:
+            self.staging = self._qualify_staging(in_rows)
         self.inputs = [np.asarray(x).reshape(in_rows, self.row_bytes) for x in self._in]
         self.outputs = [np.asarray(x).reshape(b.rows, self.row_bytes) for x in self._out]
         self.input, self.output = self.inputs[0], self.outputs[0]
@@ -215,6 +220,45 @@ class DistributedBlur:
                 self.pipe.attach_transport(self.transport)
             else:
                 raise ValueError(f"unknown transport {transport!r} (rccl|ipc|gloo-host|none)")
+
+    def _qualify_staging(self, in_rows: int, tolerance: float = 1.05, attempts: int = 3) -> dict:
+        """Pinned staging buffers are not all equal: measured on MI355X
+        boxes, in some processes ONE slot's input buffer uploaded at ~42
+        instead of ~55 GB/s (0.342 vs 0.263 ms for the headline image, alone
+        on the link) and that slot's images paced the whole pipeline —
+        the slow mode of the driver's 20-image window (profiles/r06/).  So
+        every slot's buffers go through the copy engines once (H2D alone,
+        D2H alone: copy_floor_on), and a buffer more than `tolerance` slower
+        than the best of its direction is replaced by a fresh allocation —
+        the rejected ones stay allocated until the search ends, so the
+        allocator cannot hand the same pages back — up to `attempts` rounds.
+        Set-up only (before any image is loaded); returns what it measured."""
+        n = require_native()
+        rb, out_rows = self.row_bytes, self.band.rows
+
+        def rates():
+            return [n.copy_floor_on(self.device, self._in[k].ptr, self._out[k].ptr, rb, in_rows, out_rows, 4)
+                    for k in range(self.slots)]
+
+        held, first, replaced = [], rates(), 0
+        now = first
+        for _ in range(attempts):
+            best_h, best_d = min(r[0] for r in now), min(r[1] for r in now)
+            bad_in = [k for k, r in enumerate(now) if r[0] > tolerance * best_h]
+            bad_out = [k for k, r in enumerate(now) if r[1] > tolerance * best_d]
+            if not bad_in and not bad_out:
+                break
+            for k in bad_in:
+                held.append(self._in[k])
+                self._in[k] = n.PinnedBuffer(in_rows * rb)
+            for k in bad_out:
+                held.append(self._out[k])
+                self._out[k] = n.PinnedBuffer(out_rows * rb)
+            replaced += len(bad_in) + len(bad_out)
+            now = rates()
+        del held
+        r4 = lambda v: [[round(x, 4) for x in r] for r in v]  # noqa: E731
+        return {"h2d_d2h_pair_ms_first": r4(first), "h2d_d2h_pair_ms": r4(now), "replaced": replaced}
 
     # ------------------------------------------------------------ inputs
     @property

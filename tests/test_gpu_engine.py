@@ -215,6 +215,32 @@ def test_pipeline_slot_streams_direct_and_graph(pconv_mod, rng, capture):
         assert np.array_equal(blur.outputs[k].reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps))
 
 
+def test_pipeline_staging_qualification(pconv_mod, rng):
+    """DistributedBlur(qualify_staging=True): every slot's pinned buffers are
+    timed through the copy engines at set-up (H2D alone, D2H alone, pair) and
+    slow ones replaced; the numpy views follow the buffers that survived, so
+    images loaded afterwards come back bit-exact from every slot."""
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    w, h, reps = 301, 120, 9
+    blur = DistributedBlur(w, h, "rgb", "gaussian", reps, rank=0, world=1, device=0, slots=4, step_graphs=True,
+                           qualify_staging=True)
+    st = blur.staging
+    assert st is not None and st["replaced"] >= 0
+    for key in ("h2d_d2h_pair_ms_first", "h2d_d2h_pair_ms"):
+        assert len(st[key]) == 4 and all(len(r) == 3 and min(r) > 0 for r in st[key]), st
+    for k in range(4):
+        assert blur.inputs[k].ctypes.data == blur._in[k].ptr and blur.outputs[k].ctypes.data == blur._out[k].ptr
+    imgs = [rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for _ in range(4)]
+    ks = []
+    for img in imgs:
+        blur.load_image(img, slot=blur._next)
+        ks.append(blur.submit(reps))
+    blur.drain()
+    for img, k in zip(imgs, ks):
+        assert np.array_equal(blur.outputs[k].reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps))
+
+
 def test_xcd_swizzle_off_and_model_table(pconv_mod, native, rng):
     """Tile order without the XCD remap gives the same bytes; the shape model
     sees the runtime's real VGPR / LDS numbers for every instantiation."""

@@ -153,19 +153,23 @@ def test_rccl_mid_image_band_consumes_exchanged_rows(pconv_mod, rng, self_comm, 
 
 @pytest.mark.parametrize("ch,w", [("rgb", 57), ("grey", 1920)])
 @pytest.mark.parametrize("reps,halo,fuse", [(13, 4, 4), (20, 8, 8), (40, 40, 8), (24, 12, 8)])
-def test_rccl_band_exchanges_captured_in_the_loop_graph(pconv_mod, rng, self_comm, ch, w, reps, halo, fuse):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_rccl_band_exchanges_captured_in_the_loop_graph(pconv_mod, rng, self_comm, ch, w, reps, halo, fuse, overlap):
     """EngineOptions::capture_exchanges (bench.py's resident loop): the
-    exchange phases run on the compute stream and ncclSend/ncclRecv are
-    captured with the launches into the cached rep-loop graph — the first
-    run captures, later runs (both frame parities) replay; every run equals
-    the reflected-ghost oracle byte for byte and counts its exchanges."""
+    exchange phases' ncclSend/ncclRecv are captured with the launches into
+    the cached rep-loop graph — in stream order on the compute stream, or
+    (overlap) forked: the interior launch on the communication stream beside
+    the exchange, the edge strips after it — the first run captures, later
+    runs (both frame parities) replay; every run equals the reflected-ghost
+    oracle byte for byte and counts its exchanges."""
     n = pconv_mod.native
     c = {"grey": 1, "rgb": 3}[ch]
     y0, rows, height = 37, 48, 130
-    eng = n.BandEngine.for_band(w, height, ch, "gaussian", _mid_band(n, y0, rows), 0, halo, fuse, False, "auto",
+    eng = n.BandEngine.for_band(w, height, ch, "gaussian", _mid_band(n, y0, rows), 0, halo, fuse, overlap, "auto",
                                 graph=True, capture_exchanges=True)
     eng.attach_rccl(self_comm)
-    assert eng.comm_stream == eng.compute_stream  # exchanges in stream order with the launches
+    # exchanges in stream order with the launches, or beside the interior launch
+    assert (eng.comm_stream == eng.compute_stream) == (not overlap)
     owned = rng.integers(0, 256, size=(rows, w * c), dtype=np.uint8)
     plan = eng.plan(reps)
     n_ex = len([p for p in plan if p.exchange_depth])

@@ -34,3 +34,7 @@ for e in 8:3 4:1 2:0; do
     done
   done
 done
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_engine.py -k "staging or slot_streams" tests/test_gpu_stream.py -k "native_bench or staging or slot_streams" \
+  > $OUT/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|ERROR" $OUT/tests.log | head -20; tail -5 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
