@@ -185,6 +185,9 @@ def parse():
                    help="time every slot's pinned staging buffers through the copy engines at set-up and replace any "
                         "that copies >5%% slower than the best (DistributedBlur._qualify_staging); 'staging' in the "
                         "JSON line")
+    p.add_argument("--flush-staging", choices=["on", "off"], default="off",
+                   help="after the input images are written into the pinned staging buffers, clflush them out of "
+                        "every CPU cache (DistributedBlur(flush_staging=True))")
     p.add_argument("--native", action="store_true",
                    help="run the same serving step on the native stack: the in-tree `conv --bench` (ROCm's HIP "
                         "runtime, no torch; its fork launcher for N > 1) and print its JSON line")
@@ -765,7 +768,8 @@ def main():
                                step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
                                graph_capture=a.graph_capture == "on", stream_chunks=a.stream_chunks,
                                stream_min_bytes=int(a.stream_min_mb * 2 ** 20),
-                               qualify_staging=a.qualify_staging == "on", **policy_kwargs(a))
+                               qualify_staging=a.qualify_staging == "on", flush_staging=a.flush_staging == "on",
+                               **policy_kwargs(a))
     blur.load_synthetic(a.seed)
     # --emulate-rccl: hold a (1-rank) RCCL communicator through the timed
     # region, as every real N>1 rank of the exchange path does.
@@ -919,6 +923,7 @@ def main():
                 "ipc_pull": a.ipc_pull,
                 "numa_bind": a.numa_bind == "on",
                 "qualify_staging": a.qualify_staging == "on",
+                "flush_staging": a.flush_staging == "on",
             },
             "latency_ms": round(latency_ms, 4),
             "copy_floor": {"h2d_ms": round(h2d_ms, 4), "d2h_ms": round(d2h_ms, 4),

@@ -65,6 +65,10 @@ double copy_pair_floor_ms(int device, int64_t row_bytes, int64_t rows_in, int64_
 // (sysfs numa_node of its PCI function, -1 if unknown).
 std::map<int, int64_t> page_nodes(const void* p, size_t bytes);
 int device_numa_node(int device);
+// Write back and evict a host range from every CPU cache (clflush per line):
+// staging rows the CPU has just written stop being dirty lines that each DMA
+// read of the copy engines must fetch from a core's cache.
+void flush_host_cache(const void* p, size_t bytes);
 struct CopyFloor {
   double h2d_ms = 0, d2h_ms = 0, pair_ms = 0;
 };

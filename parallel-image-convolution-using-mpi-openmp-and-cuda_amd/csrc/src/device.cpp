@@ -2,6 +2,7 @@
 #include "pconv/device.hpp"
 
 #include <dlfcn.h>
+#include <emmintrin.h>
 #include <sched.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -95,6 +96,19 @@ std::map<int, int64_t> page_nodes(const void* p, size_t bytes) {
   }
   for (int st : status) ++out[st];  // node, or -errno for a page the kernel cannot report
   return out;
+}
+
+void flush_host_cache(const void* p, size_t bytes) {
+  if (!p || bytes == 0) return;
+  constexpr uintptr_t kLine = 64;
+  const uintptr_t a0 = reinterpret_cast<uintptr_t>(p) & ~(kLine - 1);
+  const uintptr_t a1 = reinterpret_cast<uintptr_t>(p) + bytes;
+  const int64_t lines = static_cast<int64_t>((a1 - a0 + kLine - 1) / kLine);
+  // clflush evicts the line from every cache of the coherence domain (written
+  // back if dirty), whichever core holds it; chunks in parallel.
+#pragma omp parallel for schedule(static) if (lines > (int64_t(1) << 16))
+  for (int64_t i = 0; i < lines; ++i) _mm_clflush(reinterpret_cast<const void*>(a0 + static_cast<uintptr_t>(i) * kLine));
+  _mm_mfence();
 }
 
 int device_numa_node(int device) {

@@ -308,6 +308,13 @@ PYBIND11_MODULE(_pconv_native, m) {
       py::arg("ptr"), py::arg("bytes"), "NUMA node -> pages of a host range (move_pages query; negative: -errno)");
   m.def("device_numa_node", &device_numa_node, py::arg("device"));
   m.def(
+      "flush_host_cache",
+      [](uintptr_t p, size_t bytes) {
+        py::gil_scoped_release nogil;
+        flush_host_cache(reinterpret_cast<const void*>(p), bytes);
+      },
+      py::arg("ptr"), py::arg("bytes"), "clflush a host range out of every CPU cache (staging written by the CPU)");
+  m.def(
       "copy_floor_on",
       [](int device, uintptr_t host_in, uintptr_t host_out, int64_t row_bytes, int64_t rows_in, int64_t rows_out,
          int iters) {

@@ -77,7 +77,7 @@ class DistributedBlur:
                  self_neighbours: bool = False, slot_comm: bool = False, stream_chunks: int = 0,
                  ipc_timeout_s: float = 30.0, ipc_pull: str = "grid", cu_mask_queues: bool = True,
                  head_on_slot_streams: bool = True, stream_min_bytes: Optional[int] = None,
-                 head_alt_uploads: bool = True, qualify_staging: bool = False):
+                 head_alt_uploads: bool = True, qualify_staging: bool = False, flush_staging: bool = False):
         """Pipeline policy (native EngineOptions, echoed by bench.py's JSON
         config): `cu_mask_queues` puts every slot stream on its own hardware
         queue; `head_on_slot_streams` runs a streamed head image's copies on
@@ -178,6 +178,7 @@ class DistributedBlur:
         self.inputs = [np.asarray(x).reshape(in_rows, self.row_bytes) for x in self._in]
         self.outputs = [np.asarray(x).reshape(b.rows, self.row_bytes) for x in self._out]
         self.input, self.output = self.inputs[0], self.outputs[0]
+        self.flush_staging = bool(flush_staging)
         self._next = 0
         self._pending = False  # submitted images not yet drained
         self.comm = None
@@ -284,12 +285,22 @@ class DistributedBlur:
         if self._pending:
             self.drain()
 
+    def _flushed(self, slots) -> None:
+        """flush_staging: the input rows the CPU just wrote leave every CPU
+        cache, so the copy engines' reads of them never fetch dirty lines from
+        the cores that wrote them."""
+        if self.flush_staging:
+            n = require_native()
+            for i in slots:
+                n.flush_host_cache(self._in[i].ptr, len(self._in[i]))
+
     def load_image(self, image: np.ndarray, slot: Optional[int] = None) -> None:
         self._quiesce()
         a, b = self.input_rows
         rows = np.ascontiguousarray(image, dtype=np.uint8).reshape(self.height, self.row_bytes)[a:b]
         for i in ([slot] if slot is not None else range(self.slots)):
             self.inputs[i][:] = rows
+        self._flushed([slot] if slot is not None else range(self.slots))
 
     def load_file(self, path: str) -> None:
         self._quiesce()
@@ -298,6 +309,7 @@ class DistributedBlur:
                                        b - a)
         for i in range(1, self.slots):
             self.inputs[i][:] = self.inputs[0]
+        self._flushed(range(self.slots))
 
     def load_synthetic(self, seed: int = 0) -> None:
         self._quiesce()
@@ -306,6 +318,7 @@ class DistributedBlur:
                                     a, b - a)
         for i in range(1, self.slots):
             self.inputs[i][:] = self.inputs[0]
+        self._flushed(range(self.slots))
 
     # ------------------------------------------------------------ compute
     def submit(self, reps: int) -> int:
