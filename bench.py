@@ -185,9 +185,11 @@ def parse():
                    help="time every slot's pinned staging buffers through the copy engines at set-up and replace any "
                         "that copies >5%% slower than the best (DistributedBlur._qualify_staging); 'staging' in the "
                         "JSON line")
-    p.add_argument("--flush-staging", choices=["on", "off"], default="off",
+    p.add_argument("--flush-staging", choices=["on", "off"], default="on",
                    help="after the input images are written into the pinned staging buffers, clflush them out of "
-                        "every CPU cache (DistributedBlur(flush_staging=True))")
+                        "every CPU cache (DistributedBlur(flush_staging=True)): rows left dirty in the caches of the "
+                        "cores that wrote them made that buffer's uploads ~5-15%% slower for the whole process "
+                        "(profiles/r06/e/)")
     p.add_argument("--native", action="store_true",
                    help="run the same serving step on the native stack: the in-tree `conv --bench` (ROCm's HIP "
                         "runtime, no torch; its fork launcher for N > 1) and print its JSON line")
@@ -688,6 +690,7 @@ def run_native(a) -> int:
     cmd += [] if a.head_on_slot_streams else ["--head-pool-streams"]
     cmd += [] if a.numa_bind == "on" else ["--no-numa-bind"]
     cmd += [] if a.qualify_staging == "on" else ["--no-qualify-staging"]
+    cmd += [] if a.flush_staging == "on" else ["--no-flush-staging"]
     if a.emulate:
         cmd[cmd.index("--gpus") + 1] = "1"
         cmd += ["--emulate", a.emulate]  # one rank of a WORLD-way split, alone (per-rank proxy)

@@ -71,6 +71,7 @@ struct CliConfig {
   std::string ipc_pull = "grid";          // --transport ipc: pull form (grid | single | sdma)
   bool numa_bind = true;                  // N > 1: each rank on its GPU's NUMA node
   bool qualify_staging = true;            // --bench: time every slot's pinned buffers, replace slow ones
+  bool flush_staging = true;              // --bench: clflush the CPU-written input rows out of the CPU caches
 };
 
 // Parse argv.  Throws pconv::Error with the message to print on bad input.

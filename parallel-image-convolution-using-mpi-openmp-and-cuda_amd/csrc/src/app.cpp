@@ -873,6 +873,10 @@ void bench_rank(const CliConfig& c, BenchShared* sh, uint8_t* image, int rank) {
   if (c.qualify_staging) (void)qualify_staging(device, ins, outs, rb, in_rows, b.rows);
   load_rows(c, g, b.y0 - above, in_rows, ins[0].data(), rb);
   for (int k = 1; k < c.slots; ++k) std::memcpy(ins[k].data(), ins[0].data(), ins[0].size());
+  // rows the CPU just wrote out of every CPU cache: the copy engines' reads
+  // then never fetch dirty lines from the cores that wrote them
+  if (c.flush_staging)
+    for (auto& x : ins) flush_host_cache(x.data(), x.size());
   int64_t n = 0;
   auto submit = [&]() {
     const int k = static_cast<int>(n++ % c.slots);

@@ -77,6 +77,7 @@ std::string help_text(const std::string& prog) {
          "  --no-numa-bind            N > 1: leave each rank's CPU affinity alone\n"
          "  --no-qualify-staging      --bench: keep the first pinned staging buffers (default: time each slot's\n"
          "                            buffers at set-up and replace any >5% slower than the best)\n"
+         "  --no-flush-staging        --bench: leave the loaded input rows in the CPU caches (default: clflush)\n"
 
          "\n"
          "       " + prog + " --serve SOCKET [--device D] [--idle-timeout S] [--max-engines N]\n"
@@ -208,6 +209,8 @@ CliConfig parse_cli(const std::vector<std::string>& args) {
       c.numa_bind = false;
     } else if (a == "--no-qualify-staging") {
       c.qualify_staging = false;
+    } else if (a == "--no-flush-staging") {
+      c.flush_staging = false;
     } else if (a == "--warmup") {
       c.warmup = static_cast<int>(parse_int(next("--warmup"), "--warmup", 0, 100));
     } else {

@@ -77,7 +77,7 @@ class DistributedBlur:
                  self_neighbours: bool = False, slot_comm: bool = False, stream_chunks: int = 0,
                  ipc_timeout_s: float = 30.0, ipc_pull: str = "grid", cu_mask_queues: bool = True,
                  head_on_slot_streams: bool = True, stream_min_bytes: Optional[int] = None,
-                 head_alt_uploads: bool = True, qualify_staging: bool = False, flush_staging: bool = False):
+                 head_alt_uploads: bool = True, qualify_staging: bool = True, flush_staging: bool = True):
         """Pipeline policy (native EngineOptions, echoed by bench.py's JSON
         config): `cu_mask_queues` puts every slot stream on its own hardware
         queue; `head_on_slot_streams` runs a streamed head image's copies on
@@ -87,7 +87,12 @@ class DistributedBlur:
         `ipc_pull` is the IPC transport's pull form (grid | single | sdma,
         ipc_halo.hpp).  `qualify_staging`: time every slot's pinned staging
         buffers through the copy engines once and replace any that copies
-        slower than the best (see _qualify_staging)."""
+        slower than the best (see _qualify_staging).  `flush_staging`: after
+        the CPU writes input rows into the pinned buffers (load_*), clflush
+        them out of every CPU cache — the copy engines' reads of lines left
+        dirty in the caches of the cores that wrote them (the OpenMP writers
+        of load_synthetic) ran that buffer's uploads 5-15 % slower for the
+        life of the process (profiles/r06/e/)."""
         n = require_native()
         ctx = env_context()
         self.rank = ctx.rank if rank is None else int(rank)
