@@ -310,7 +310,9 @@ def resident_loop(blur, a, ipc: bool = False) -> dict:
     """The resident loop with `--resident-images` concurrent images (the
     reported ms_per_image), and — when that is more than one — also one
     image alone, the reference's single-image loop ('one_image')."""
-    nimg = max(1, int(a.resident_images))
+    # concurrent images need a capturable transport (RCCL, IPC): a host-staged
+    # one (gloo-host, rehearsals) runs the single-image loop
+    nimg = max(1, int(a.resident_images)) if (ipc or blur.comm is not None) else 1
     out = resident_loop_n(blur, a, ipc, nimg)
     if nimg > 1:
         one = resident_loop_n(blur, a, ipc, 1)

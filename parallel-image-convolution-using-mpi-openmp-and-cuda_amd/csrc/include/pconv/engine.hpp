@@ -236,6 +236,15 @@ class BandEngine {
   hipStream_t cs_ = nullptr, ms_ = nullptr;
   Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_;
   std::vector<Event> up_evs_, dn_evs_;  // streamed images: per chunk, uploaded / rows final
+ public:
+  // Create the streamed-image events for `chunks` chunks now (set-up), not
+  // inside the first streamed image this engine runs.
+  void reserve_stream_events(size_t chunks) {
+    while (up_evs_.size() < chunks) up_evs_.push_back(Event::create());
+    while (dn_evs_.size() < chunks + 1) dn_evs_.push_back(Event::create());
+  }
+
+ private:
   std::shared_ptr<HaloTransport> transport_;
   RunStats stats_;
   double wall_t0_ = 0;

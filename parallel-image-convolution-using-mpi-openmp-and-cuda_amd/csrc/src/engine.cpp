@@ -364,8 +364,7 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
   uint8_t* in_frame = frame_at(c0);
   const uint8_t* out_frame = frame_at(c0 + sp.levels);
   const size_t nc = sp.chunks.size();
-  while (up_evs_.size() < nc) up_evs_.push_back(Event::create());
-  while (dn_evs_.size() < nc + 1) dn_evs_.push_back(Event::create());
+  reserve_stream_events(nc);
   // Host issue order: every upload first (the H2D stream then runs them back
   // to back instead of waiting for the host to issue the next one behind the
   // previous chunk's launches), then each chunk's launches behind its
@@ -571,6 +570,20 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
       ev_head_ = Event::create();
       h2d_wait_ = Event::create();
       head_streaming_ = true;
+      // Every slot may stream a head image (the window's first slot is
+      // count % slots): its events now, and one direct H2D and one direct D2H
+      // of a row on every slot stream — the streams a head image borrows for
+      // its chunk copies — so no first-use set-up of a stream's copies lands
+      // in the first window that borrows it.
+      for (auto& e : slots_) e->reserve_stream_events(static_cast<size_t>(opt.stream_chunks) + 1);
+      const int64_t rb = slots_[0]->layout().row_bytes;
+      PinnedBuffer row(static_cast<size_t>(rb));
+      std::memset(row.data(), 0, row.size());
+      for (auto& e : slots_) {
+        e->upload_rows(row.data(), rb, 0, 1, e->compute_stream());
+        e->download_rows(row.data(), rb, 0, 1, e->compute_stream());
+      }
+      for (auto& e : slots_) e->synchronize();
     }
     used_.assign(slots, false);
     return;

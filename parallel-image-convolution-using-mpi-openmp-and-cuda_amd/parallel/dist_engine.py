@@ -330,6 +330,12 @@ class DistributedBlur:
         """Enqueue one image (slot round-robin); returns the slot whose output
         buffer will hold the result after drain()."""
         k = self._next
+        # An IPC wait that timed out (a stalled or vanished neighbour) is final:
+        # no further image — no graph replay whose copies might read a gone
+        # neighbour's frames (the sdma form) — is issued once it is set.  A
+        # read of host-mapped memory, no device synchronisation.
+        for t in self.ipc:
+            t.check()
         self.pipe.submit(self._in[k].ptr, -self.above, self.band.rows + self.below, self._out[k].ptr, int(reps))
         self._next = (k + 1) % self.slots
         self._pending = True

@@ -1,8 +1,6 @@
 #!/bin/bash
 # Round 6, call G: final-tree evidence on another box — the driver's command
-# x10, the 8-way proxy in every IPC pull form and the other halo modes (300
-# images), the BASELINE large frames on one GPU, and a rocprofv3 kernel +
-# copy trace of the driver's command.
+# x10, then the whole GPU suite and smoke.
 set -o pipefail
 OUT=gpurun_out/r06/g
 mkdir -p $OUT
@@ -14,23 +12,10 @@ one() {  # name, -- bench args
 }
 for r in 0 1 2 3 4 5 6 7 8 9; do one drv_$r --gpus 1 --steps 20 --warmup 5 || exit 1; done
 python tools/r06/summ_windows.py $OUT/drv_*.json
-one s200 --gpus 1 --steps 200 --warmup 30 --diag-windows 0 || exit 1
-one e8_preload --emulate 8:3 --steps 300 --warmup 10 --diag-windows 0 || exit 1
-for p in grid single sdma; do
-  one e8_ipc_$p --emulate 8:3 --emulate-halo ipc --ipc-pull $p --steps 300 --warmup 10 --diag-windows 0 || exit 1
-done
-one e8_slotx --emulate 8:3 --emulate-halo slot_exchange --steps 300 --warmup 10 --diag-windows 0 || exit 1
-python - $OUT <<'PY'
-import glob, json, sys
-for f in sorted(glob.glob(sys.argv[1] + "/*.json")):
-    d = json.loads(open(f).read().strip().splitlines()[-1])
-    r = d.get("resident_loop") or d.get("resident_loop_ipc") or {}
-    print(f.split("/")[-1], d["ms_per_step"], "pair", d["copy_floor"]["pair_ms"], "lat", d.get("latency_ms"),
-          "loop", d["loop_only"]["ms_per_step"], "resident", r.get("ms_per_image"), (r.get("one_image") or {}).get("ms_per_image"),
-          "mism", d.get("mismatches"))
-PY
-one big8192 --gpus 1 --width 8192 --height 8192 --reps 100 --steps 20 --warmup 5 --diag-windows 2 || exit 1
-one big32768 --gpus 1 --width 32768 --height 32768 --channels grey --reps 200 --steps 10 --warmup 3 --diag-windows 1 || exit 1
-python tools/r06/summ_windows.py $OUT/big*.json
-timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $OUT/prof -o drv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --diag-windows 2 > $OUT/prof_bench.json 2> $OUT/prof_bench.err || { echo "rocprof failed"; tail -5 $OUT/prof_bench.err; exit 1; }
-find $OUT/prof -name "*stats*" | head
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+  > $OUT/pytest_gpu.txt 2>&1
+rc=$?
+tail -1 $OUT/pytest_gpu.txt
+if [ $rc -ne 0 ]; then grep -E "^(FAILED|ERROR)" $OUT/pytest_gpu.txt | head -30; [ $rc -eq 1 ] || exit 1; fi
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { echo "smoke failed"; cat $OUT/smoke.txt; exit 1; }
+tail -1 $OUT/smoke.txt
