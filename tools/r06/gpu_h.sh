@@ -11,6 +11,11 @@ one() {  # name, -- bench args
   local name=$1; shift
   timeout -k 10 300 python -u bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "bench $name failed"; tail -5 $OUT/$name.err; return 1; }
 }
+for r in 0 1 2 3 4 5; do
+  one plain_$r --gpus 1 --steps 20 --warmup 5 --diag-windows 2 || exit 1
+  one marked_$r --gpus 1 --steps 20 --warmup 5 --diag-windows 2 --mark-timed || exit 1
+done
+python tools/r06/summ_windows.py $OUT/plain_*.json $OUT/marked_*.json
 one s200 --gpus 1 --steps 200 --warmup 30 --diag-windows 0 || exit 1
 for e in 2:0 4:1 8:3; do
   n=${e%%:*}
