@@ -106,6 +106,11 @@ struct EngineOptions {
   // driver's window 0.334-0.348 vs 0.337-0.351 ms; alternating the downloads
   // too was slower (0.564-0.580, both 0.602-0.625: profiles/r05/l/).
   bool head_alt_uploads = true;
+  // Images of a burst streamed as heads (>= 4 slots): the first (1, the
+  // default) or the first two — the second's repetitions then overlap its
+  // own copies instead of sitting between its H2D and its D2H while the
+  // D2H engine idles (docs/PERFORMANCE.md §1.3).
+  int head_images = 1;
 };
 
 struct RunStats {
@@ -340,7 +345,7 @@ class BandPipeline {
   std::vector<Event> ev_up_, ev_done_, ev_free_, ev_halo_;
   // step-graph mode with stream_chunks > 1: images submitted while nothing is
   // in flight (after construction / drain) are row-streamed (head streaming)
-  bool idle_ = true;
+  int64_t burst_pos_ = 0;  // images submitted since the last drain (0: the pipeline is idle)
   int64_t streamed_heads_ = 0;
   bool head_streaming_ = false;  // stream_chunks > 1 with step graphs
   bool head_on_slots_ = false;   // the head's copies on the next two slots' streams

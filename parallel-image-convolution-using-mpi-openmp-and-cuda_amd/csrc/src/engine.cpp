@@ -716,7 +716,11 @@ void BandPipeline::submit_image(int k, const uint8_t* host_in, int64_t in_r0, in
   if (graphs_) {
     PCONV_CHECK(trace_ev_.empty(), "pipeline trace needs directly issued images (graph capture off)");
     const int64_t in_bytes = (in_r1 - in_r0) * e.layout().row_bytes;
-    if (idle_ && head_streaming_ && in_bytes >= e.options().stream_min_bytes) {
+    // The first `head_images` images of a burst (EngineOptions::head_images;
+    // more than one only with >= 4 slots, whose streams keep the heads'
+    // copies apart) are streamed.
+    const int64_t heads = slots() >= 4 ? std::max(1, e.options().head_images) : 1;
+    if (burst_pos_ < heads && head_streaming_ && in_bytes >= e.options().stream_min_bytes) {
       // Head streaming: nothing is in flight, so this image's rows stream
       // (chunked H2D ‖ launches ‖ D2H of finished rows, schedule.hpp
       // plan_streamed) instead of waiting for its whole upload and its
@@ -735,7 +739,10 @@ void BandPipeline::submit_image(int k, const uint8_t* host_in, int64_t in_r0, in
         hipStream_t up = head_on_slots_ ? computes_[static_cast<size_t>((k + 1) % n)].get() : h2d_.get();
         hipStream_t down = head_on_slots_ ? computes_[static_cast<size_t>((k + n - 1) % n)].get() : d2h_.get();
         // odd chunks' uploads on slot k+2's stream (EngineOptions::head_alt_uploads)
-        hipStream_t up2 = head_on_slots_ && n >= 4 && e.options().head_alt_uploads
+        // — the first head only: a second head's k+2 is the first head's
+        // download stream, so its uploads all go on k+1 (the first head's
+        // k+2), its downloads on k-1 (the first head's own stream)
+        hipStream_t up2 = head_on_slots_ && n >= 4 && e.options().head_alt_uploads && burst_pos_ == 0
                               ? computes_[static_cast<size_t>((k + 2) % n)].get()
                               : nullptr;
         h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
@@ -746,7 +753,7 @@ void BandPipeline::submit_image(int k, const uint8_t* host_in, int64_t in_r0, in
           ev_head_.record(done);
           ev_head_.wait_on(e.compute_stream());
         }
-        idle_ = false;
+        ++burst_pos_;
         used_[k] = true;
         ++count_;
         ++streamed_heads_;
@@ -754,7 +761,7 @@ void BandPipeline::submit_image(int k, const uint8_t* host_in, int64_t in_r0, in
       }
     }
     e.process_graph(host_in, in_r0, in_r1, host_out, reps);
-    idle_ = false;
+    ++burst_pos_;
     used_[k] = true;
     ++count_;
     return;
@@ -834,7 +841,7 @@ void BandPipeline::drain() {
   if (h2d_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(h2d_.get()));
   for (auto& s : slots_) s->synchronize();
   if (d2h_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(d2h_.get()));
-  idle_ = true;
+  burst_pos_ = 0;
 }
 
 // --------------------------------------------------------------- LocalCluster

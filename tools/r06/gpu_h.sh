@@ -11,7 +11,15 @@ one() {  # name, -- bench args
   local name=$1; shift
   timeout -k 10 300 python -u bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "bench $name failed"; tail -5 $OUT/$name.err; return 1; }
 }
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_stream.py -k "two_head or head_stream_modes" \
+  > $OUT/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|ERROR" $OUT/tests.log | head -20; tail -5 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
 for r in 0 1 2 3 4 5; do
+  one h1_$r --gpus 1 --steps 20 --warmup 5 --diag-windows 4 || exit 1
+  one h2_$r --gpus 1 --steps 20 --warmup 5 --diag-windows 4 --head-images 2 || exit 1
+done
+python tools/r06/summ_windows.py $OUT/h1_*.json $OUT/h2_*.json
+for r in 0 1 2 3; do
   one plain_$r --gpus 1 --steps 20 --warmup 5 --diag-windows 2 || exit 1
   one marked_$r --gpus 1 --steps 20 --warmup 5 --diag-windows 2 --mark-timed || exit 1
 done
