@@ -47,5 +47,5 @@ PY
 one big8192 --gpus 1 --width 8192 --height 8192 --reps 100 --steps 20 --warmup 5 --diag-windows 2 || exit 1
 one big32768 --gpus 1 --width 32768 --height 32768 --channels grey --reps 200 --steps 10 --warmup 3 --diag-windows 1 || exit 1
 python tools/r06/summ_windows.py $OUT/big*.json
-timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $OUT/prof -o drv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --diag-windows 2 > $OUT/prof_bench.json 2> $OUT/prof_bench.err || { echo "rocprof failed"; tail -5 $OUT/prof_bench.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $OUT/prof -o drv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --diag-windows 2 > $OUT/prof_bench.json 2> $OUT/prof_bench.err || { echo "rocprof failed"; tail -5 $OUT/prof_bench.err; exit 1; }
 find $OUT/prof -name "*stats*" | head
