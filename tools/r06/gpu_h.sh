@@ -49,3 +49,8 @@ one big32768 --gpus 1 --width 32768 --height 32768 --channels grey --reps 200 --
 python tools/r06/summ_windows.py $OUT/big*.json
 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $OUT/prof -o drv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --diag-windows 2 > $OUT/prof_bench.json 2> $OUT/prof_bench.err || { echo "rocprof failed"; tail -5 $OUT/prof_bench.err; exit 1; }
 find $OUT/prof -name "*stats*" | head
+timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace --output-format csv -d $OUT/lat -o lat -- python3 tools/r06/latency_probe.py --images 12 > $OUT/lat_probe.json 2> $OUT/lat_probe.err || { echo "latency trace failed"; tail -5 $OUT/lat_probe.err; exit 1; }
+cat $OUT/lat_probe.json
+python tools/r06/latency_timeline.py $OUT/lat --images 2 > $OUT/lat_timeline.txt 2>&1 || true
+head -c 20000000 $OUT/lat_timeline.txt > /dev/null
+find $OUT/lat -name "*.csv" -size +20M -delete

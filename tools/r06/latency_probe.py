@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""One head-streamed headline image at a time (the `latency_ms` scope of
+bench.py: submit to an idle pipeline, drain), N times, with a host
+timestamp per image — run under rocprofv3 (kernel + memory-copy + HIP API
+traces) to see where one image's 0.53 ms goes: each chunk copy's start
+against the API call that issued it and the event it waited for.
+
+    rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace \
+        --output-format csv -d OUT -o lat -- python3 tools/r06/latency_probe.py
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--images", type=int, default=30)
+    p.add_argument("--head-images", type=int, default=1)
+    p.add_argument("--chunks", type=int, default=4)
+    a = p.parse_args()
+    import torch
+
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    torch.cuda.set_device(0)
+    blur = DistributedBlur(1920, 2520, "rgb", "gaussian", 40, rank=0, world=1, device=0, slots=4,
+                           stream_chunks=a.chunks, head_images=a.head_images)
+    blur.load_synthetic(1234)
+    for _ in range(5):
+        blur.submit(40)
+    blur.drain()
+    lat = []
+    for _ in range(a.images):
+        t = time.perf_counter()
+        blur.step(40)
+        lat.append((time.perf_counter() - t) * 1e3)
+    lat.sort()
+    print(json.dumps({"latency_ms_median": round(lat[len(lat) // 2], 4), "min": round(lat[0], 4),
+                      "max": round(lat[-1], 4), "streamed_heads": int(blur.pipe.streamed_heads)}))
+
+
+if __name__ == "__main__":
+    main()
