@@ -111,9 +111,6 @@ def parse():
     p.add_argument("--head-one-upload-stream", dest="head_alt_uploads", action="store_false", default=True,
                    help="streamed head image: all chunk uploads on one slot's stream (default with >= 4 slots: "
                         "alternating over two, one image 0.546-0.549 vs 0.559-0.568 ms, profiles/r05/l/)")
-    p.add_argument("--head-images", type=int, default=1,
-                   help="images of a burst streamed as heads (>= 4 slots): 1, or 2 (the second image's repetitions "
-                        "then overlap its own copies)")
     p.add_argument("--stream-min-mb", type=float, default=8.0,
                    help="head-stream only images of at least this many MiB of input: below it the hand-offs of a "
                         "streamed image cost more than they hide (N=4 band 0.32 vs 0.23 ms as one graph, N=8 0.28 "
@@ -288,7 +285,6 @@ def policy_kwargs(a) -> dict:
     return dict(cu_mask_queues=getattr(a, "cu_mask_queues", True),
                 head_on_slot_streams=getattr(a, "head_on_slot_streams", True),
                 head_alt_uploads=getattr(a, "head_alt_uploads", True),
-                head_images=getattr(a, "head_images", 1),
                 ipc_pull=getattr(a, "ipc_pull", "grid"))
 
 
@@ -929,7 +925,6 @@ def main():
                 "cu_mask_queues": bool(a.cu_mask_queues),
                 "head_on_slot_streams": bool(a.head_on_slot_streams),
                 "head_alt_uploads": bool(a.head_alt_uploads),
-                "head_images": int(a.head_images),
                 "ipc_pull": a.ipc_pull,
                 "numa_bind": a.numa_bind == "on",
                 "qualify_staging": a.qualify_staging == "on",

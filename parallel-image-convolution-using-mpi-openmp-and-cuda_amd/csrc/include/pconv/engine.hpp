@@ -106,11 +106,6 @@ struct EngineOptions {
   // driver's window 0.334-0.348 vs 0.337-0.351 ms; alternating the downloads
   // too was slower (0.564-0.580, both 0.602-0.625: profiles/r05/l/).
   bool head_alt_uploads = true;
-  // Images of a burst streamed as heads (>= 4 slots): the first (1, the
-  // default) or the first two — the second's repetitions then overlap its
-  // own copies instead of sitting between its H2D and its D2H while the
-  // D2H engine idles (docs/PERFORMANCE.md §1.3).
-  int head_images = 1;
 };
 
 struct RunStats {
@@ -330,6 +325,10 @@ class BandPipeline {
   // diagnostic pass only (bench.py's window replays), never the timed one.
   void enable_marks(int images);
   std::vector<std::vector<double>> marks();
+  // Slot-stream mode: has slot k's latest image completed (its output buffer
+  // final)?  wait_image(k) blocks until it has — one image, not the drain.
+  bool ready(int k) const;
+  void wait_image(int k) const;
 
  private:
   void trace_mark(int stage, hipStream_t s);
@@ -355,6 +354,7 @@ class BandPipeline {
   std::vector<Event> trace_ev_;  // 4 per traced image
   std::vector<int> trace_slot_;
   int64_t trace_first_ = 0;
+  std::vector<Event> done_;     // slot-stream mode: per slot, its latest image done (timing events)
   std::vector<Event> mark_ev_;  // [0] = before the first image, [1 + i] = image i done
   std::vector<std::pair<int, bool>> mark_info_;  // (slot, head-streamed) per marked image
   int64_t mark_first_ = 0;

@@ -586,6 +586,7 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
       for (auto& e : slots_) e->synchronize();
     }
     used_.assign(slots, false);
+    for (int i = 0; i < slots; ++i) done_.push_back(Event::create(true));
     return;
   }
   // Streams: H2D, D2H, communication (only with neighbours) and compute.
@@ -641,17 +642,29 @@ void BandPipeline::set_transport(std::shared_ptr<HaloTransport> t) {
 void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
   TraceRange tr("pconv.pipeline.submit");
   const int k = static_cast<int>(count_ % static_cast<int64_t>(slots_.size()));
-  if (mark_ev_.empty()) {
-    submit_image(k, host_in, in_r0, in_r1, host_out, reps);
-    return;
-  }
   completion_mark(k, true, false);
   const int64_t heads = streamed_heads_;
   submit_image(k, host_in, in_r0, in_r1, host_out, reps);
   completion_mark(k, false, streamed_heads_ != heads);
+  // The image's completion event, right behind its work on the stream it
+  // completes on (ready() / wait_image()).  Recording it also hands the
+  // image's work to the GPU at once: windows whose images each ended in a
+  // timing event record ran 0.3281-0.3309 ms/step against 0.3323-0.3365
+  // without (4 interleaved pairs, profiles/r06/h/marked_*, plain_*).
+  if (graphs_) done_[static_cast<size_t>(k)].record(slots_[static_cast<size_t>(k)]->compute_stream());
 }
 
+bool BandPipeline::ready(int k) const {
+  const hipError_t e = hipEventQuery(done_.at(static_cast<size_t>(k)).get());
+  if (e == hipErrorNotReady) return false;
+  PCONV_HIP_CHECK(e);
+  return true;
+}
+
+void BandPipeline::wait_image(int k) const { done_.at(static_cast<size_t>(k)).sync(); }
+
 void BandPipeline::completion_mark(int k, bool before, bool streamed) {
+  if (mark_ev_.empty()) return;
   const int64_t i = count_ - mark_first_ - (before ? 0 : 1);  // this image's index among the marked ones
   if (i < 0 || i + 1 >= static_cast<int64_t>(mark_ev_.size())) return;
   if (before && i != 0) return;
@@ -716,11 +729,11 @@ void BandPipeline::submit_image(int k, const uint8_t* host_in, int64_t in_r0, in
   if (graphs_) {
     PCONV_CHECK(trace_ev_.empty(), "pipeline trace needs directly issued images (graph capture off)");
     const int64_t in_bytes = (in_r1 - in_r0) * e.layout().row_bytes;
-    // The first `head_images` images of a burst (EngineOptions::head_images;
-    // more than one only with >= 4 slots, whose streams keep the heads'
-    // copies apart) are streamed.
-    const int64_t heads = slots() >= 4 ? std::max(1, e.options().head_images) : 1;
-    if (burst_pos_ < heads && head_streaming_ && in_bytes >= e.options().stream_min_bytes) {
+    // Only the first image of a burst is streamed: streaming the first two
+    // (the second on the first head's streams) measured no better — 0.3315-
+    // 0.3353 vs 0.3288-0.3328 ms/step, the second head's slot 0.04 ms late
+    // in every window (profiles/r06/h/h2_*) — and was removed.
+    if (burst_pos_ == 0 && head_streaming_ && in_bytes >= e.options().stream_min_bytes) {
       // Head streaming: nothing is in flight, so this image's rows stream
       // (chunked H2D ‖ launches ‖ D2H of finished rows, schedule.hpp
       // plan_streamed) instead of waiting for its whole upload and its
@@ -739,10 +752,7 @@ void BandPipeline::submit_image(int k, const uint8_t* host_in, int64_t in_r0, in
         hipStream_t up = head_on_slots_ ? computes_[static_cast<size_t>((k + 1) % n)].get() : h2d_.get();
         hipStream_t down = head_on_slots_ ? computes_[static_cast<size_t>((k + n - 1) % n)].get() : d2h_.get();
         // odd chunks' uploads on slot k+2's stream (EngineOptions::head_alt_uploads)
-        // — the first head only: a second head's k+2 is the first head's
-        // download stream, so its uploads all go on k+1 (the first head's
-        // k+2), its downloads on k-1 (the first head's own stream)
-        hipStream_t up2 = head_on_slots_ && n >= 4 && e.options().head_alt_uploads && burst_pos_ == 0
+        hipStream_t up2 = head_on_slots_ && n >= 4 && e.options().head_alt_uploads
                               ? computes_[static_cast<size_t>((k + 2) % n)].get()
                               : nullptr;
         h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first

@@ -600,10 +600,9 @@ PYBIND11_MODULE(_pconv_native, m) {
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
                        int concurrent, bool graphs, bool step_graphs, py::object band, bool slot_comm,
                        int stream_chunks, bool cu_mask_queues, bool head_on_slot_streams,
-                       int64_t stream_min_bytes, bool head_alt_uploads, int head_images) {
+                       int64_t stream_min_bytes, bool head_alt_uploads) {
              EngineOptions o;
              o.head_alt_uploads = head_alt_uploads;
-             o.head_images = head_images;
              o.stream_chunks = stream_chunks;
              o.stream_min_bytes = stream_min_bytes;
              o.cu_mask_queues = cu_mask_queues;
@@ -625,8 +624,7 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("graphs") = false, py::arg("step_graphs") = true,
            py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0,
            py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true,
-           py::arg("stream_min_bytes") = EngineOptions{}.stream_min_bytes, py::arg("head_alt_uploads") = true,
-           py::arg("head_images") = 1)
+           py::arg("stream_min_bytes") = EngineOptions{}.stream_min_bytes, py::arg("head_alt_uploads") = true)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -650,6 +648,9 @@ PYBIND11_MODULE(_pconv_native, m) {
           },
           py::arg("in_ptr"), py::arg("in_r0"), py::arg("in_r1"), py::arg("out_ptr"), py::arg("reps"))
       .def("drain", &BandPipeline::drain, py::call_guard<py::gil_scoped_release>())
+      .def("ready", &BandPipeline::ready, py::arg("slot"), "slot-stream mode: the slot's latest image is done")
+      .def("wait_image", &BandPipeline::wait_image, py::arg("slot"), py::call_guard<py::gil_scoped_release>(),
+           "slot-stream mode: block until the slot's latest image is done")
       .def("enable_marks", &BandPipeline::enable_marks, py::arg("images"),
            "Completion marks of the next `images` submits (a diagnostic pass; see marks()).")
       .def("marks", &BandPipeline::marks, py::call_guard<py::gil_scoped_release>(),
@@ -666,7 +667,6 @@ PYBIND11_MODULE(_pconv_native, m) {
                                d["stream_chunks"] = o.stream_chunks;
                                d["stream_min_bytes"] = o.stream_min_bytes;
                                d["head_alt_uploads"] = o.head_alt_uploads;
-                               d["head_images"] = o.head_images;
                                d["cu_mask_queues"] = o.cu_mask_queues;
                                d["head_on_slot_streams"] = o.head_on_slot_streams;
                                return d;

@@ -77,8 +77,7 @@ class DistributedBlur:
                  self_neighbours: bool = False, slot_comm: bool = False, stream_chunks: int = 0,
                  ipc_timeout_s: float = 30.0, ipc_pull: str = "grid", cu_mask_queues: bool = True,
                  head_on_slot_streams: bool = True, stream_min_bytes: Optional[int] = None,
-                 head_alt_uploads: bool = True, qualify_staging: bool = True, flush_staging: bool = True,
-                 head_images: int = 1):
+                 head_alt_uploads: bool = True, qualify_staging: bool = True, flush_staging: bool = True):
         """Pipeline policy (native EngineOptions, echoed by bench.py's JSON
         config): `cu_mask_queues` puts every slot stream on its own hardware
         queue; `head_on_slot_streams` runs a streamed head image's copies on
@@ -112,7 +111,7 @@ class DistributedBlur:
         kw = dict(halo=int(halo), fuse=int(fuse), overlap=bool(overlap), variant=variant, slots=int(slots),
                   concurrent=int(concurrent), stream_chunks=int(stream_chunks),
                   cu_mask_queues=bool(cu_mask_queues), head_on_slot_streams=bool(head_on_slot_streams),
-                  head_alt_uploads=bool(head_alt_uploads), head_images=int(head_images),
+                  head_alt_uploads=bool(head_alt_uploads),
                   **({} if stream_min_bytes is None else {"stream_min_bytes": int(stream_min_bytes)}))
         if self_neighbours:
             # One-GPU emulation of rank `rank` of a `world`-way split whose halos

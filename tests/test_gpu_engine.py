@@ -241,6 +241,30 @@ def test_pipeline_staging_qualification(pconv_mod, rng):
         assert np.array_equal(blur.outputs[k].reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps))
 
 
+def test_pipeline_per_image_completion(pconv_mod, rng):
+    """Slot-stream pipeline: every image ends in its slot's completion event
+    — wait_image(k) makes that image's output final without draining the
+    others, ready(k) reports it; completion marks (the bench's diagnostic
+    pass) give one time per image, increasing."""
+    from pconv.parallel.dist_engine import DistributedBlur
+
+    w, h, reps = 97, 88, 16
+    blur = DistributedBlur(w, h, "rgb", "gaussian", reps, rank=0, world=1, device=0, slots=4, step_graphs=True,
+                           stream_chunks=4, stream_min_bytes=0)
+    imgs = [rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for _ in range(4)]
+    for k, img in enumerate(imgs):
+        blur.load_image(img, slot=k)
+    blur.pipe.enable_marks(4)
+    ks = [blur.submit(reps) for _ in range(4)]
+    for k in ks:
+        blur.pipe.wait_image(k)
+        assert blur.pipe.ready(k)
+        assert np.array_equal(blur.outputs[k].reshape(h, w, 3), pconv_mod.numpy_convolve(imgs[k], reps)), k
+    marks = blur.pipe.marks()
+    assert [int(m[0]) for m in marks] == ks and [int(m[2]) for m in marks] == [1, 0, 0, 0]
+    assert all(b[1] >= a[1] > 0 for a, b in zip(marks, marks[1:])), marks
+
+
 def test_xcd_swizzle_off_and_model_table(pconv_mod, native, rng):
     """Tile order without the XCD remap gives the same bytes; the shape model
     sees the runtime's real VGPR / LDS numbers for every instantiation."""

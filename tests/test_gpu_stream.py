@@ -102,25 +102,6 @@ def test_head_stream_modes(pconv_mod, rng, on_slots, alt, slots):
         assert np.array_equal(blur.step(reps).reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps))
 
 
-@pytest.mark.parametrize("alt", [True, False])
-@pytest.mark.parametrize("slots", [3, 4, 5])
-def test_two_head_images(pconv_mod, rng, alt, slots):
-    """EngineOptions::head_images = 2: the first TWO images of every burst
-    are row-streamed (>= 4 slots; the second on the first head's upload and
-    compute streams), the rest as step graphs; with 3 slots it stays one.
-    Every image of every burst bit-exact, and single images too."""
-    w, h, reps = 96, 120, 40
-    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=slots, mode="head", head_alt_uploads=alt, head_images=2)
-    assert blur.pipe.options["head_images"] == 2
-    _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps, rounds=3)
-    per_burst = 2 if slots >= 4 else 1
-    assert blur.pipe.streamed_heads == 3 * per_burst, blur.pipe.streamed_heads
-    img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
-    blur.load_image(img)
-    for _ in range(3):
-        assert np.array_equal(blur.step(reps).reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps))
-
-
 def test_head_stream_threshold(pconv_mod, rng):
     """EngineOptions::stream_min_bytes (default 8 MiB): the headline frame
     (14.5 MB) is head-streamed, its 8-way band (2.3 MB) runs as one step

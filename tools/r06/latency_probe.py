@@ -20,7 +20,6 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--images", type=int, default=30)
-    p.add_argument("--head-images", type=int, default=1)
     p.add_argument("--chunks", type=int, default=4)
     a = p.parse_args()
     import torch
@@ -29,7 +28,7 @@ def main():
 
     torch.cuda.set_device(0)
     blur = DistributedBlur(1920, 2520, "rgb", "gaussian", 40, rank=0, world=1, device=0, slots=4,
-                           stream_chunks=a.chunks, head_images=a.head_images)
+                           stream_chunks=a.chunks)
     blur.load_synthetic(1234)
     for _ in range(5):
         blur.submit(40)
