@@ -355,6 +355,7 @@ class BandPipeline {
   std::vector<int> trace_slot_;
   int64_t trace_first_ = 0;
   std::vector<Event> done_;     // slot-stream mode: per slot, its latest image done (timing events)
+  Event burst_start_;           // slot-stream mode: before the first image of the latest burst
   std::vector<Event> mark_ev_;  // [0] = before the first image, [1 + i] = image i done
   std::vector<std::pair<int, bool>> mark_info_;  // (slot, head-streamed) per marked image
   int64_t mark_first_ = 0;

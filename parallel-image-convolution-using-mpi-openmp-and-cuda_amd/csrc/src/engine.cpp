@@ -587,6 +587,7 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
     }
     used_.assign(slots, false);
     for (int i = 0; i < slots; ++i) done_.push_back(Event::create(true));
+    burst_start_ = Event::create(true);
     return;
   }
   // Streams: H2D, D2H, communication (only with neighbours) and compute.
@@ -642,15 +643,18 @@ void BandPipeline::set_transport(std::shared_ptr<HaloTransport> t) {
 void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
   TraceRange tr("pconv.pipeline.submit");
   const int k = static_cast<int>(count_ % static_cast<int64_t>(slots_.size()));
+  // A burst's first image (nothing in flight) starts behind a timing event on
+  // its slot's stream (burst_start_): windows whose first image did so ran
+  // 0.3281-0.3309 ms/step against 0.3323-0.3365 without (4 interleaved
+  // pairs each, profiles/r06/h/marked_*, plain_*; profiles/r06/i/ shows the
+  // per-image completion events below alone do not do it).
+  if (graphs_ && burst_pos_ == 0) burst_start_.record(slots_[static_cast<size_t>(k)]->compute_stream());
   completion_mark(k, true, false);
   const int64_t heads = streamed_heads_;
   submit_image(k, host_in, in_r0, in_r1, host_out, reps);
   completion_mark(k, false, streamed_heads_ != heads);
   // The image's completion event, right behind its work on the stream it
-  // completes on (ready() / wait_image()).  Recording it also hands the
-  // image's work to the GPU at once: windows whose images each ended in a
-  // timing event record ran 0.3281-0.3309 ms/step against 0.3323-0.3365
-  // without (4 interleaved pairs, profiles/r06/h/marked_*, plain_*).
+  // completes on (ready() / wait_image()).
   if (graphs_) done_[static_cast<size_t>(k)].record(slots_[static_cast<size_t>(k)]->compute_stream());
 }
 
