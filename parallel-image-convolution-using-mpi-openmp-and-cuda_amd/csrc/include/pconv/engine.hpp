@@ -236,9 +236,18 @@ class BandEngine {
   hipStream_t cs_ = nullptr, ms_ = nullptr;
   Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_;
   std::vector<Event> up_evs_, dn_evs_;  // streamed images: per chunk, uploaded / rows final
+  bool stream_trace_ = false;
+  std::vector<Event> st_ev_;
+  size_t st_chunks_ = 0;
  public:
   // Create the streamed-image events for `chunks` chunks now (set-up), not
   // inside the first streamed image this engine runs.
+  // Diagnostics: time the next streamed images chunk by chunk (timing events
+  // after each chunk's upload, launches and download); stream_trace() gives,
+  // for the latest one, {chunk, upload end, launches end, download end} in
+  // ms from its first upload's issue point (-1: nothing recorded).
+  void set_stream_trace(bool on) { stream_trace_ = on; }
+  std::vector<std::vector<double>> stream_trace();
   void reserve_stream_events(size_t chunks) {
     while (up_evs_.size() < chunks) up_evs_.push_back(Event::create());
     while (dn_evs_.size() < chunks + 1) dn_evs_.push_back(Event::create());

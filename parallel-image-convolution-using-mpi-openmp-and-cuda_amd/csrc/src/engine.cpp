@@ -389,17 +389,27 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
            hipMemcpyDeviceToHost, s);
   };
   auto up_of = [&](size_t c) { return (c & 1) && up2 ? up2 : up; };
+  // diagnostics (stream_trace): timing events at the start, after each
+  // chunk's upload, launches and download — [0] start, then 3 per chunk
+  const bool tr_on = stream_trace_;
+  if (tr_on) {
+    while (st_ev_.size() < 1 + 3 * nc) st_ev_.push_back(Event::create(true));
+    st_chunks_ = nc;
+    st_ev_[0].record(up);
+  }
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     copy(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, ch.up_hi - ch.up_lo,
          hipMemcpyHostToDevice, up_of(c));
     if (up_of(c) != cs_) up_evs_[c].record(up_of(c));
+    if (tr_on) st_ev_[1 + 3 * c].record(up_of(c));
   }
   bool pending = false;  // launches not yet covered by a download-side event
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     if (up_of(c) != cs_) up_evs_[c].wait_on(cs_);
     launches(ch);
+    if (tr_on) st_ev_[2 + 3 * c].record(cs_);
     if (!ch.launches.empty()) pending = true;
     if (ch.down_hi > ch.down_lo && host_out) {
       dn_evs_[c].record(cs_);
@@ -414,11 +424,32 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
     if (!(ch.down_hi > ch.down_lo && host_out)) continue;
     dn_evs_[c].wait_on(down);
     download(ch, down);
+    if (tr_on) st_ev_[3 + 3 * c].record(down);
   }
   if (pending) dn_evs_[nc].wait_on(down);
   cur_ = (c0 + sp.levels) & 1;
   halo_valid_ = false;
   return down;
+}
+
+std::vector<std::vector<double>> BandEngine::stream_trace() {
+  std::vector<std::vector<double>> out;
+  if (!stream_trace_ || st_chunks_ == 0) return out;
+  synchronize();
+  for (size_t c = 0; c < st_chunks_; ++c) {
+    std::vector<double> row{static_cast<double>(c)};
+    for (int k = 1; k <= 3; ++k) {
+      float ms = -1.f;
+      // a chunk without a download never records its event: -1
+      if (hipEventElapsedTime(&ms, st_ev_[0].get(), st_ev_[3 * c + static_cast<size_t>(k)].get()) != hipSuccess) {
+        (void)hipGetLastError();
+        ms = -1.f;
+      }
+      row.push_back(ms);
+    }
+    out.push_back(row);
+  }
+  return out;
 }
 
 void BandEngine::process_graph(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {

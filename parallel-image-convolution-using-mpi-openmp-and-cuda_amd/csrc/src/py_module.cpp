@@ -586,6 +586,10 @@ PYBIND11_MODULE(_pconv_native, m) {
           py::arg("width"), py::arg("height"), py::arg("channels"), py::arg("filter"), py::arg("band"),
           py::arg("device") = 0, py::arg("halo") = 1, py::arg("fuse") = 1, py::arg("overlap") = true,
           py::arg("variant") = "auto", py::arg("graph") = false, py::arg("capture_exchanges") = false)
+      .def("set_stream_trace", &BandEngine::set_stream_trace, py::arg("on"),
+           "diagnostics: time the next streamed images chunk by chunk (stream_trace())")
+      .def("stream_trace", &BandEngine::stream_trace, py::call_guard<py::gil_scoped_release>(),
+           "latest streamed image: [chunk, upload end, launches end, download end] ms from its start")
       .def("attach_rccl",
            [](BandEngine& e, std::shared_ptr<RcclComm> c) {
              e.set_transport(std::make_shared<RcclTransport>(std::move(c)));

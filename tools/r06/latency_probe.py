@@ -21,6 +21,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--images", type=int, default=30)
     p.add_argument("--chunks", type=int, default=4)
+    p.add_argument("--trace", type=int, default=0, help="then this many images with chunk timing events")
     a = p.parse_args()
     import torch
 
@@ -39,8 +40,22 @@ def main():
         blur.step(40)
         lat.append((time.perf_counter() - t) * 1e3)
     lat.sort()
-    print(json.dumps({"latency_ms_median": round(lat[len(lat) // 2], 4), "min": round(lat[0], 4),
-                      "max": round(lat[-1], 4), "streamed_heads": int(blur.pipe.streamed_heads)}))
+    out = {"latency_ms_median": round(lat[len(lat) // 2], 4), "min": round(lat[0], 4), "max": round(lat[-1], 4),
+           "streamed_heads": int(blur.pipe.streamed_heads)}
+    if a.trace:
+        # the same single images with chunk timing events (their own timing shifts slightly)
+        for k in range(blur.slots):
+            blur.pipe.slot(k).set_stream_trace(True)
+        traces, lat2 = [], []
+        for _ in range(a.trace):
+            k = blur._next
+            t = time.perf_counter()
+            blur.step(40)
+            lat2.append((time.perf_counter() - t) * 1e3)
+            traces.append([[round(x, 4) for x in r] for r in blur.pipe.slot(k).stream_trace()])
+        out["traced_latency_ms"] = sorted(lat2)[len(lat2) // 2]
+        out["chunk_trace_ms"] = traces[-3:]  # per chunk: [chunk, upload end, launches end, download end]
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
