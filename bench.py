@@ -108,6 +108,8 @@ def parse():
                         "them, download finished rows meanwhile (H2D, reps and D2H of ONE image overlap; 0 = off). "
                         "With step graphs only an image submitted to an idle pipeline is streamed (the head of a "
                         "burst, every single image: latency_ms 0.56 vs 0.69 ms whole-image, profiles/r04/head/)")
+    p.add_argument("--stream-weights", default=None, metavar="W1,W2,...",
+                   help="relative rows of each streamed chunk (sets the chunk count; default 1,2,...,2,1)")
     p.add_argument("--head-one-upload-stream", dest="head_alt_uploads", action="store_false", default=True,
                    help="streamed head image: all chunk uploads on one slot's stream (default with >= 4 slots: "
                         "alternating over two, one image 0.546-0.549 vs 0.559-0.568 ms, profiles/r05/l/)")
@@ -286,6 +288,12 @@ def policy_kwargs(a) -> dict:
                 head_on_slot_streams=getattr(a, "head_on_slot_streams", True),
                 head_alt_uploads=getattr(a, "head_alt_uploads", True),
                 ipc_pull=getattr(a, "ipc_pull", "grid"))
+
+
+def stream_weights(a) -> list:
+    """--stream-weights "3,4,4,5,5" -> [3, 4, 4, 5, 5] ([]: the default 1, 2, ..., 2, 1)."""
+    w = getattr(a, "stream_weights", None)
+    return [int(x) for x in w.split(",")] if w else []
 
 
 def mode_kwargs(a, mode: str, fuse: int) -> dict:
@@ -772,7 +780,7 @@ def main():
                                transport=head_transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
                                step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
                                graph_capture=a.graph_capture == "on", stream_chunks=a.stream_chunks,
-                               stream_min_bytes=int(a.stream_min_mb * 2 ** 20),
+                               stream_weights=stream_weights(a), stream_min_bytes=int(a.stream_min_mb * 2 ** 20),
                                qualify_staging=a.qualify_staging == "on", flush_staging=a.flush_staging == "on",
                                **policy_kwargs(a))
     blur.load_synthetic(a.seed)
@@ -917,7 +925,8 @@ def main():
                 "step_graphs": bool(blur.pipe.step_graphs),
                 "halo_depth": int(blur.engine.halo),
                 "fuse": int(blur.engine.fuse),
-                "stream_chunks": int(a.stream_chunks),
+                "stream_chunks": int(len(stream_weights(a)) if a.stream_weights else a.stream_chunks),
+                "stream_weights": list(blur.pipe.options["stream_weights"]),
                 "stream_min_mb": a.stream_min_mb,
                 "preload_halo": bool(blur.preload_halo),
                 "launches_per_step": int(stats.launches),

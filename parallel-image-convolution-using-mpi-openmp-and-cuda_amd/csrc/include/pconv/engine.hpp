@@ -83,6 +83,9 @@ struct EngineOptions {
   // fork/join branches it measured 1.4-4.3x slower per image
   // (profiles/r04/stream_a/).
   int stream_chunks = 0;
+  // Relative rows per streamed chunk (one weight per chunk, stream_chunks of
+  // them); empty: 1, 2, ..., 2, 1 (stream_cuts).
+  std::vector<int> stream_weights;
   // Head streaming only for images of at least this many input bytes: the
   // cross-stream hand-offs of a streamed image cost more than they hide on
   // smaller ones.  One image of the headline split N ways, streamed vs one

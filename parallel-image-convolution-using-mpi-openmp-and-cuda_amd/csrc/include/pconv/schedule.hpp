@@ -100,6 +100,9 @@ bool streamable(const std::vector<Phase>& plan);
 // first and the last chunk half the size of the others (the first one starts
 // the compute early, the last one shortens the tail after the final upload).
 std::vector<int64_t> stream_cuts(int64_t in_lo, int64_t in_hi, int chunks);
+// Upload boundaries for chunks of rows in proportion to `weights` (one
+// chunk per weight, each > 0); chunks that would be empty are merged.
+std::vector<int64_t> stream_cuts_weighted(int64_t in_lo, int64_t in_hi, const std::vector<int>& weights);
 
 // cuts: strictly increasing interior boundaries (in_lo < cut < in_hi).
 StreamPlan plan_streamed(const std::vector<Phase>& plan, int64_t in_lo, int64_t in_hi, int64_t owned_rows,

@@ -345,7 +345,10 @@ StreamPlan BandEngine::stream_plan(int reps, int64_t in_r0, int64_t in_r1) const
   c.halo_preloaded = input_preloaded(in_r0, in_r1);
   const std::vector<Phase> ph = plan_band(band_, reps, c);
   if (!streamable(ph)) return sp;
-  return plan_streamed(ph, in_r0, in_r1, band_.rows, stream_cuts(in_r0, in_r1, opt_.stream_chunks));
+  const std::vector<int64_t> cuts = opt_.stream_weights.empty()
+                                        ? stream_cuts(in_r0, in_r1, opt_.stream_chunks)
+                                        : stream_cuts_weighted(in_r0, in_r1, opt_.stream_weights);
+  return plan_streamed(ph, in_r0, in_r1, band_.rows, cuts);
 }
 
 hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,

@@ -181,6 +181,7 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def_readonly("chunks", &StreamPlan::chunks);
   m.def("streamable", &streamable, py::arg("plan"));
   m.def("stream_cuts", &stream_cuts, py::arg("in_lo"), py::arg("in_hi"), py::arg("chunks"));
+  m.def("stream_cuts_weighted", &stream_cuts_weighted, py::arg("in_lo"), py::arg("in_hi"), py::arg("weights"));
   m.def("plan_streamed", &plan_streamed, py::arg("plan"), py::arg("in_lo"), py::arg("in_hi"), py::arg("owned_rows"),
         py::arg("cuts"));
 
@@ -604,10 +605,13 @@ PYBIND11_MODULE(_pconv_native, m) {
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
                        int concurrent, bool graphs, bool step_graphs, py::object band, bool slot_comm,
                        int stream_chunks, bool cu_mask_queues, bool head_on_slot_streams,
-                       int64_t stream_min_bytes, bool head_alt_uploads) {
+                       int64_t stream_min_bytes, bool head_alt_uploads, std::vector<int> stream_weights) {
              EngineOptions o;
              o.head_alt_uploads = head_alt_uploads;
              o.stream_chunks = stream_chunks;
+             PCONV_CHECK(stream_weights.empty() || static_cast<int>(stream_weights.size()) == stream_chunks,
+                         "stream_weights: one weight per chunk (stream_chunks of them)");
+             o.stream_weights = std::move(stream_weights);
              o.stream_min_bytes = stream_min_bytes;
              o.cu_mask_queues = cu_mask_queues;
              o.head_on_slot_streams = head_on_slot_streams;
@@ -628,7 +632,8 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("graphs") = false, py::arg("step_graphs") = true,
            py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0,
            py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true,
-           py::arg("stream_min_bytes") = EngineOptions{}.stream_min_bytes, py::arg("head_alt_uploads") = true)
+           py::arg("stream_min_bytes") = EngineOptions{}.stream_min_bytes, py::arg("head_alt_uploads") = true,
+           py::arg("stream_weights") = std::vector<int>{})
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -669,6 +674,7 @@ PYBIND11_MODULE(_pconv_native, m) {
                                const EngineOptions& o = p.slot(0).options();
                                py::dict d;
                                d["stream_chunks"] = o.stream_chunks;
+                               d["stream_weights"] = o.stream_weights;
                                d["stream_min_bytes"] = o.stream_min_bytes;
                                d["head_alt_uploads"] = o.head_alt_uploads;
                                d["cu_mask_queues"] = o.cu_mask_queues;

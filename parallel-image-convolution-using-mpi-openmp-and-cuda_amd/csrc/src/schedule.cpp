@@ -72,13 +72,24 @@ bool streamable(const std::vector<Phase>& plan) {
 std::vector<int64_t> stream_cuts(int64_t in_lo, int64_t in_hi, int chunks) {
   const int64_t n = in_hi - in_lo;
   chunks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(chunks, n)));
-  std::vector<int64_t> cuts;
-  if (chunks <= 1) return cuts;
+  if (chunks <= 1) return {};
   // weights 1, 2, ..., 2, 1 (two chunks: 1, 1)
-  const int64_t total = chunks == 2 ? 2 : 2 * (chunks - 1);
+  std::vector<int> w(static_cast<size_t>(chunks), chunks == 2 ? 1 : 2);
+  w.front() = w.back() = 1;
+  return stream_cuts_weighted(in_lo, in_hi, w);
+}
+
+std::vector<int64_t> stream_cuts_weighted(int64_t in_lo, int64_t in_hi, const std::vector<int>& weights) {
+  const int64_t n = in_hi - in_lo;
+  int64_t total = 0;
+  for (int w : weights) {
+    PCONV_CHECK(w > 0, "stream_cuts_weighted: weights must be positive");
+    total += w;
+  }
+  std::vector<int64_t> cuts;
   int64_t acc = 0;
-  for (int c = 0; c + 1 < chunks; ++c) {
-    acc += (c == 0 || chunks == 2) ? 1 : 2;
+  for (size_t c = 0; c + 1 < weights.size(); ++c) {
+    acc += weights[c];
     const int64_t cut = in_lo + (n * acc) / total;
     if (cut > in_lo && cut < in_hi && (cuts.empty() || cut > cuts.back())) cuts.push_back(cut);
   }

@@ -204,6 +204,18 @@ def test_stream_cuts_shape(native):
     assert native.stream_cuts(0, 3, 10) == [1, 2] or len(native.stream_cuts(0, 3, 10)) <= 2
 
 
+def test_stream_cuts_weighted(native):
+    # the default weights through the weighted form
+    assert native.stream_cuts_weighted(0, 2520, [1, 2, 2, 2, 2, 1]) == native.stream_cuts(0, 2520, 6)
+    assert native.stream_cuts_weighted(0, 2520, [3, 4, 4, 5, 5]) == [360, 840, 1320, 1920]
+    assert native.stream_cuts_weighted(-40, 2560, [1]) == []
+    # more chunks than rows: empty chunks merged, cuts strictly inside
+    c = native.stream_cuts_weighted(0, 3, [1, 1, 1, 1, 1, 1])
+    assert c == sorted(set(c)) and all(0 < x < 3 for x in c)
+    with pytest.raises(Exception):
+        native.stream_cuts_weighted(0, 100, [1, 0, 1])
+
+
 def test_plan_streamed_rejects_exchanges(native):
     band = native.row_band(100, 2, 0)
     plan = native.plan_band(band, 20, 8, 8, True, False)  # needs exchanges
