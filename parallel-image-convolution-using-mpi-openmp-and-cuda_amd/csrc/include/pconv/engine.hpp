@@ -109,14 +109,6 @@ struct EngineOptions {
   // driver's window 0.334-0.348 vs 0.337-0.351 ms; alternating the downloads
   // too was slower (0.564-0.580, both 0.602-0.625: profiles/r05/l/).
   bool head_alt_uploads = true;
-  // Compute lanes of a streamed head image.  A chunk's launches cost 0.06-
-  // 0.08 ms whatever its rows (per-step latency of a small grid, 40 steps;
-  // profiles/r06/k, l, m), so with >= 5 chunks the one compute stream, not
-  // the copies, paced the image.  2: odd chunks launch on a second
-  // (dedicated) stream — a wavefront over (chunk, level): launch (c, j) after
-  // (c, j - 1) on its lane and after the latest level-j launch on the other;
-  // the plan's lags keep their rows apart (schedule.hpp plan_streamed).
-  int head_lanes = 1;
 };
 
 struct RunStats {
@@ -208,11 +200,9 @@ class BandEngine {
   // stream, downloads of the finished rows on `down` (cross-stream events per
   // chunk).  The caller orders `up` after any earlier use of these frames.
   // Returns the stream whose completion means the whole image is done.
-  // `up2` (optional): odd chunks' uploads alternate onto it.  `lane2`
-  // (optional, EngineOptions::head_lanes): odd chunks' launches run on it.
+  // `up2` (optional): odd chunks' uploads alternate onto it.
   hipStream_t enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
-                               const StreamPlan& sp, hipStream_t up, hipStream_t down, hipStream_t up2 = nullptr,
-                               hipStream_t lane2 = nullptr);
+                               const StreamPlan& sp, hipStream_t up, hipStream_t down, hipStream_t up2 = nullptr);
   // Phase-by-phase execution for multi-band emulation on one device.
   std::vector<Phase> plan(int reps) const;
   void exec_exchange(const Phase& p);
@@ -249,7 +239,6 @@ class BandEngine {
   hipStream_t cs_ = nullptr, ms_ = nullptr;
   Event ev_ready_, ev_halo_, ev_t0_, ev_t1_, ev_sync_;
   std::vector<Event> up_evs_, dn_evs_;  // streamed images: per chunk, uploaded / rows final
-  std::vector<Event> lane_evs_;         // two-lane streamed images: per launch, done
   bool stream_trace_ = false;
   std::vector<Event> st_ev_;
   size_t st_chunks_ = 0;
@@ -260,13 +249,11 @@ class BandEngine {
   // ms from its first upload's issue point (-1: nothing recorded).
   void set_stream_trace(bool on) { stream_trace_ = on; }
   std::vector<std::vector<double>> stream_trace();
-  // Create the streamed-image events for `chunks` chunks (and, for two
-  // compute lanes, `launches` launches) now (set-up), not inside the first
-  // streamed image this engine runs.
-  void reserve_stream_events(size_t chunks, size_t launches = 0) {
+  // Create the streamed-image events for `chunks` chunks now (set-up), not
+  // inside the first streamed image this engine runs.
+  void reserve_stream_events(size_t chunks) {
     while (up_evs_.size() < chunks) up_evs_.push_back(Event::create());
-    while (dn_evs_.size() < chunks + 2) dn_evs_.push_back(Event::create());
-    while (lane_evs_.size() < launches) lane_evs_.push_back(Event::create());
+    while (dn_evs_.size() < chunks + 1) dn_evs_.push_back(Event::create());
   }
 
  private:
@@ -374,7 +361,6 @@ class BandPipeline {
   bool head_streaming_ = false;  // stream_chunks > 1 with step graphs
   bool head_on_slots_ = false;   // the head's copies on the next two slots' streams
   Event ev_head_, h2d_wait_;
-  Stream head_lane_;  // head_lanes == 2: the streamed head's second compute lane
   std::vector<bool> used_;
   int64_t count_ = 0;
   std::vector<Event> trace_ev_;  // 4 per traced image

@@ -353,7 +353,7 @@ StreamPlan BandEngine::stream_plan(int reps, int64_t in_r0, int64_t in_r1) const
 
 hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out,
                                          const StreamPlan& sp, hipStream_t up, hipStream_t down,
-                                         hipStream_t up2, hipStream_t lane2) {
+                                         hipStream_t up2) {
   TraceRange tr("pconv.streamed_image");
   PCONV_CHECK(!sp.chunks.empty(), "enqueue_streamed: empty stream plan");
   PCONV_CHECK(sp.chunks.front().up_lo == in_r0 && sp.chunks.back().up_hi == in_r1,
@@ -367,30 +367,7 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
   uint8_t* in_frame = frame_at(c0);
   const uint8_t* out_frame = frame_at(c0 + sp.levels);
   const size_t nc = sp.chunks.size();
-  // Two compute lanes (EngineOptions::head_lanes): odd chunks launch on
-  // `lane2`.  Launch (c, j) follows (c, j - 1) in its lane's order and waits
-  // for the latest level-j launch on the other lane; with those edges the
-  // plan's lags keep concurrent launches' rows apart (plan_streamed: chunk c's
-  // level j ends max(s_j, s_j-1) rows below level j - 1, so (c + 1, j - 1)
-  // neither reads nor writes rows (c, j) touches, and (c, j) overwrites no
-  // level j - 2 row a launch of the other lane still reads).
-  const bool two = lane2 != nullptr && lane2 != cs_;
-  // event after launch (c, i) only when a later chunk launches its level
-  std::vector<std::vector<char>> need(nc);
-  size_t n_need = 0;
-  if (two) {
-    std::vector<char> later(static_cast<size_t>(sp.levels) + 1, 0);
-    for (size_t c = nc; c-- > 0;) {
-      const StreamChunk& ch = sp.chunks[c];
-      need[c].assign(ch.launches.size(), 0);
-      for (size_t i = 0; i < ch.launches.size(); ++i) {
-        need[c][i] = later[static_cast<size_t>(ch.levels[i])];
-        n_need += need[c][i] ? 1 : 0;
-      }
-      for (int j : ch.levels) later[static_cast<size_t>(j)] = 1;
-    }
-  }
-  reserve_stream_events(nc, n_need);
+  reserve_stream_events(nc);
   // Host issue order: every upload first (the H2D stream then runs them back
   // to back instead of waiting for the host to issue the next one behind the
   // previous chunk's launches), then each chunk's launches behind its
@@ -402,30 +379,11 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
                   hipStream_t s) {
     if (rows > 0) PCONV_HIP_CHECK(hipMemcpy2DAsync(dst, dpitch, src, spitch, rb, rows, kind, s));
   };
-  auto lane_of = [&](size_t c) { return two && (c & 1) ? lane2 : cs_; };
-  // two lanes: per level, the latest launch's lane (-1: none yet) and event
-  std::vector<int> lvl_lane(static_cast<size_t>(sp.levels) + 1, -1);
-  std::vector<size_t> lvl_ev(static_cast<size_t>(sp.levels) + 1, 0);
-  size_t nev = 0;
-  auto launches = [&](size_t c) {
-    const StreamChunk& ch = sp.chunks[c];
-    hipStream_t s = lane_of(c);
-    const int li = two && (c & 1) ? 1 : 0;
+  auto launches = [&](const StreamChunk& ch) {
     for (size_t i = 0; i < ch.launches.size(); ++i) {
-      const size_t j = static_cast<size_t>(ch.levels[i]);
-      if (two && lvl_lane[j] >= 0 && lvl_lane[j] != li) lane_evs_[lvl_ev[j]].wait_on(s);
-      launch_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1), s,
-                     opt_.variant);
+      launch_stencil(filter_, geom_.channels, make_launch(ch.launches[i], (c0 + ch.levels[i] - 1) & 1),
+                     cs_, opt_.variant);
       ++stats_.launches;
-      if (two) {
-        lvl_lane[j] = li;
-        if (need[c][i]) {
-          lane_evs_[nev].record(s);
-          lvl_ev[j] = nev++;
-        } else {
-          lvl_lane[j] = -1;  // no later launch of this level waits for it
-        }
-      }
     }
   };
   auto download = [&](const StreamChunk& ch, hipStream_t s) {
@@ -446,33 +404,24 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
     const StreamChunk& ch = sp.chunks[c];
     copy(in_frame + ch.up_lo * p, p, host_in + (ch.up_lo - in_r0) * rb, rb, ch.up_hi - ch.up_lo,
          hipMemcpyHostToDevice, up_of(c));
-    if (two || up_of(c) != cs_) up_evs_[c].record(up_of(c));
+    if (up_of(c) != cs_) up_evs_[c].record(up_of(c));
     if (tr_on) st_ev_[1 + 3 * c].record(up_of(c));
   }
-  bool pending[2] = {false, false};  // per lane: launches not yet covered by a download-side event
-  // two lanes: uploads from `up_from` on are not yet behind a level-1 event
-  // the other lane waits for (a chunk without launches leaves its upload to
-  // the next chunk's lane)
-  size_t up_from = 0;
+  bool pending = false;  // launches not yet covered by a download-side event
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
-    hipStream_t s = lane_of(c);
-    const int li = two && (c & 1) ? 1 : 0;
-    for (size_t u = two ? up_from : c; u <= c; ++u)
-      if (up_of(u) != s) up_evs_[u].wait_on(s);
-    if (two && !ch.levels.empty() && ch.levels.front() == 1) up_from = c + 1;
-    launches(c);
-    if (tr_on) st_ev_[2 + 3 * c].record(s);
-    if (!ch.launches.empty()) pending[li] = true;
+    if (up_of(c) != cs_) up_evs_[c].wait_on(cs_);
+    launches(ch);
+    if (tr_on) st_ev_[2 + 3 * c].record(cs_);
+    if (!ch.launches.empty()) pending = true;
     if (ch.down_hi > ch.down_lo && host_out) {
-      dn_evs_[c].record(s);
-      pending[li] = false;
+      dn_evs_[c].record(cs_);
+      pending = false;
     }
   }
   // `down` finishing must mean the whole image is done (the next image of
   // these frames waits on it), also when launches follow the last download.
-  for (int li = 0; li < 2; ++li)
-    if (pending[li]) dn_evs_[nc + static_cast<size_t>(li)].record(li ? lane2 : cs_);
+  if (pending) dn_evs_[nc].record(cs_);
   for (size_t c = 0; c < nc; ++c) {
     const StreamChunk& ch = sp.chunks[c];
     if (!(ch.down_hi > ch.down_lo && host_out)) continue;
@@ -480,8 +429,7 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
     download(ch, down);
     if (tr_on) st_ev_[3 + 3 * c].record(down);
   }
-  for (int li = 0; li < 2; ++li)
-    if (pending[li]) dn_evs_[nc + static_cast<size_t>(li)].wait_on(down);
+  if (pending) dn_evs_[nc].wait_on(down);
   cur_ = (c0 + sp.levels) & 1;
   halo_valid_ = false;
   return down;
@@ -665,12 +613,8 @@ BandPipeline::BandPipeline(const ImageGeom& geom, const Band& band, const Filter
       // of a row on every slot stream — the streams a head image borrows for
       // its chunk copies — so no first-use set-up of a stream's copies lands
       // in the first window that borrows it.
-      const size_t nchunks = static_cast<size_t>(std::max<int>(opt.stream_chunks, static_cast<int>(opt.stream_weights.size())));
-      for (auto& e : slots_) e->reserve_stream_events(nchunks + 1, opt.head_lanes >= 2 ? 8 * (nchunks + 1) : 0);
-      if (opt.head_lanes >= 2) {
-        // the second compute lane: its own hardware queue like the slots'
-        head_lane_ = opt.cu_mask_queues ? own_queue_stream(opt.device) : Stream::create(0);
-      }
+      const size_t nchunks = std::max(static_cast<size_t>(std::max(opt.stream_chunks, 0)), opt.stream_weights.size());
+      for (auto& e : slots_) e->reserve_stream_events(nchunks + 1);
       const int64_t rb = slots_[0]->layout().row_bytes;
       PinnedBuffer row(static_cast<size_t>(rb));
       std::memset(row.data(), 0, row.size());
@@ -857,7 +801,7 @@ void BandPipeline::submit_image(int k, const uint8_t* host_in, int64_t in_r0, in
         h2d_wait_.record(e.compute_stream());  // earlier work of this slot (its previous graph) first
         h2d_wait_.wait_on(up);
         if (up2) h2d_wait_.wait_on(up2);
-        hipStream_t done = e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down, up2, head_lane_.get());
+        hipStream_t done = e.enqueue_streamed(host_in, in_r0, in_r1, host_out, sp, up, down, up2);
         if (done != e.compute_stream()) {
           ev_head_.record(done);
           ev_head_.wait_on(e.compute_stream());

@@ -605,11 +605,8 @@ PYBIND11_MODULE(_pconv_native, m) {
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
                        int concurrent, bool graphs, bool step_graphs, py::object band, bool slot_comm,
                        int stream_chunks, bool cu_mask_queues, bool head_on_slot_streams,
-                       int64_t stream_min_bytes, bool head_alt_uploads, std::vector<int> stream_weights,
-                       int head_lanes) {
+                       int64_t stream_min_bytes, bool head_alt_uploads, std::vector<int> stream_weights) {
              EngineOptions o;
-             PCONV_CHECK(head_lanes == 1 || head_lanes == 2, "head_lanes must be 1 or 2");
-             o.head_lanes = head_lanes;
              o.head_alt_uploads = head_alt_uploads;
              o.stream_chunks = stream_chunks;
              PCONV_CHECK(stream_weights.empty() || static_cast<int>(stream_weights.size()) == stream_chunks,
@@ -636,7 +633,7 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0,
            py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true,
            py::arg("stream_min_bytes") = EngineOptions{}.stream_min_bytes, py::arg("head_alt_uploads") = true,
-           py::arg("stream_weights") = std::vector<int>{}, py::arg("head_lanes") = EngineOptions{}.head_lanes)
+           py::arg("stream_weights") = std::vector<int>{})
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -678,7 +675,6 @@ PYBIND11_MODULE(_pconv_native, m) {
                                py::dict d;
                                d["stream_chunks"] = o.stream_chunks;
                                d["stream_weights"] = o.stream_weights;
-                               d["head_lanes"] = o.head_lanes;
                                d["stream_min_bytes"] = o.stream_min_bytes;
                                d["head_alt_uploads"] = o.head_alt_uploads;
                                d["cu_mask_queues"] = o.cu_mask_queues;

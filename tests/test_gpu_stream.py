@@ -102,19 +102,17 @@ def test_head_stream_modes(pconv_mod, rng, on_slots, alt, slots):
         assert np.array_equal(blur.step(reps).reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps))
 
 
-@pytest.mark.parametrize("weights", [None, [3, 4, 4, 5, 5], [1, 1, 1, 1, 1, 1, 1, 1, 1], [5, 1, 1, 5]])
+@pytest.mark.parametrize("weights", [[3, 4, 4, 5, 5], [1, 1, 1, 1, 1, 1, 1, 1, 1], [5, 1, 1, 5]])
 @pytest.mark.parametrize("w,h,ch,filt,reps,fuse", [(96, 120, "rgb", "gaussian", 40, 8),
                                                    (33, 37, "grey", "gaussian", 41, 8),
                                                    (59, 83, "rgb", "box", 11, None)])
-def test_head_two_lanes(pconv_mod, rng, weights, w, h, ch, filt, reps, fuse):
-    """head_lanes=2: a streamed head's odd chunks launch on a second stream
-    (a wavefront over chunks and levels), with default and uneven chunk
-    weights (stream_weights) and chunks thinner than the plan's lag (chunks
-    without launches); bursts and single images bit-exact."""
+def test_head_stream_weights(pconv_mod, rng, weights, w, h, ch, filt, reps, fuse):
+    """stream_weights: uneven streamed chunks, including chunks thinner than
+    the plan's lag (chunks without launches); bursts and single images
+    bit-exact."""
     kw = {} if fuse is None else dict(fuse=fuse, halo=fuse)
-    blur = _blur(w, h, ch, filt, reps, 4, slots=4, mode="head", head_lanes=2, stream_weights=weights, **kw)
-    assert blur.pipe.options["head_lanes"] == 2
-    assert blur.pipe.options["stream_weights"] == (weights or [])
+    blur = _blur(w, h, ch, filt, reps, 4, slots=4, mode="head", stream_weights=weights, **kw)
+    assert blur.pipe.options["stream_weights"] == weights
     _run_images(pconv_mod, rng, blur, w, h, ch, filt, reps, rounds=2)
     c = CH[ch]
     img = rng.integers(0, 256, size=(h, w, c), dtype=np.uint8)
@@ -125,17 +123,17 @@ def test_head_two_lanes(pconv_mod, rng, weights, w, h, ch, filt, reps, fuse):
     assert blur.pipe.streamed_heads >= 5
 
 
-@pytest.mark.parametrize("lanes,weights", [(1, [2, 3, 3, 4]), (2, None), (2, [2, 3, 3, 4]), (2, [1, 2, 2, 2, 2, 1])])
-def test_head_lanes_headline_frame(pconv_mod, rng, lanes, weights):
+@pytest.mark.parametrize("weights", [None, [2, 3, 3, 4], [1, 2, 2, 2, 2, 1]])
+def test_head_stream_weights_headline_frame(pconv_mod, rng, weights):
     """The headline frame (1920x2520 RGB, 40 reps) through the chunk weights
-    and compute lanes the latency runs use: single images and a burst of
-    four, against the CPU oracle (OpenMP, bit-exact to the NumPy one)."""
+    the latency runs use: single images and a burst of four, against the CPU
+    oracle (OpenMP, bit-exact to the NumPy one)."""
     from pconv.ops.stencil import convolve
 
     w, h, reps = 1920, 2520, 40
     img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
     ref = convolve(img, reps, backend="omp")
-    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=4, mode="head", head_lanes=lanes, stream_weights=weights,
+    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=4, mode="head", stream_weights=weights,
                  stream_min_bytes=None)
     blur.load_image(img)
     for _ in range(3):
