@@ -109,7 +109,7 @@ def parse():
                         "With step graphs only an image submitted to an idle pipeline is streamed (the head of a "
                         "burst, every single image: latency_ms 0.56 vs 0.69 ms whole-image, profiles/r04/head/)")
     p.add_argument("--stream-weights", default=None, metavar="W1,W2,...",
-                   help="relative rows of each streamed chunk (sets the chunk count; default 1,2,...,2,1)")
+                   help="relative rows of each streamed chunk (sets the chunk count; default 5,...,5,6)")
     p.add_argument("--head-one-upload-stream", dest="head_alt_uploads", action="store_false", default=True,
                    help="streamed head image: all chunk uploads on one slot's stream (default with >= 4 slots: "
                         "alternating over two, one image 0.546-0.549 vs 0.559-0.568 ms, profiles/r05/l/)")
@@ -291,7 +291,7 @@ def policy_kwargs(a) -> dict:
 
 
 def stream_weights(a) -> list:
-    """--stream-weights "3,4,4,5,5" -> [3, 4, 4, 5, 5] ([]: the default 1, 2, ..., 2, 1)."""
+    """--stream-weights "3,4,4,5,5" -> [3, 4, 4, 5, 5] ([]: the native default 5, ..., 5, 6)."""
     w = getattr(a, "stream_weights", None)
     return [int(x) for x in w.split(",")] if w else []
 

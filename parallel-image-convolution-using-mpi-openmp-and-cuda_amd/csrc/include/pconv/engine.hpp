@@ -84,7 +84,7 @@ struct EngineOptions {
   // (profiles/r04/stream_a/).
   int stream_chunks = 0;
   // Relative rows per streamed chunk (one weight per chunk, stream_chunks of
-  // them); empty: 1, 2, ..., 2, 1 (stream_cuts).
+  // them); empty: 5, ..., 5, 6 (stream_cuts).
   std::vector<int> stream_weights;
   // Head streaming only for images of at least this many input bytes: the
   // cross-stream hand-offs of a streamed image cost more than they hide on
@@ -244,9 +244,11 @@ class BandEngine {
   size_t st_chunks_ = 0;
  public:
   // Diagnostics: time the next streamed images chunk by chunk (timing events
-  // after each chunk's upload, launches and download); stream_trace() gives,
-  // for the latest one, {chunk, upload end, launches end, download end} in
-  // ms from its first upload's issue point (-1: nothing recorded).
+  // after each chunk's upload, its launches' wait, launches, its download's
+  // wait and download); stream_trace() gives, for the latest one, {chunk,
+  // upload end, launch wait passed, launches end, download wait passed,
+  // download end} in ms from its first upload's issue point (-1: nothing
+  // recorded).
   void set_stream_trace(bool on) { stream_trace_ = on; }
   std::vector<std::vector<double>> stream_trace();
   // Create the streamed-image events for `chunks` chunks now (set-up), not

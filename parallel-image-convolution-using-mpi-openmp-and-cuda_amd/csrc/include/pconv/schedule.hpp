@@ -96,9 +96,13 @@ struct StreamPlan {
 // True when `plan` can be streamed: >= 1 phase, no exchange, one launch each.
 bool streamable(const std::vector<Phase>& plan);
 
-// Upload boundaries for `chunks` chunks of input rows [in_lo, in_hi): the
-// first and the last chunk half the size of the others (the first one starts
-// the compute early, the last one shortens the tail after the final upload).
+// Upload boundaries for `chunks` chunks of input rows [in_lo, in_hi): even
+// chunks, the last one 6/5 as tall (weights 5, ..., 5, 6).  A chunk's
+// launches cost about the same whatever its rows (the kernel's per-step
+// latency on a small grid), so small chunks only lengthen the compute chain:
+// one headline image 0.5325-0.5376 ms with 3,3,3,4 / 4,4,4,5 / 5,5,5,6 /
+// 4,5,5,5 against 0.5480-0.5517 with the former 1, 2, 2, 1 (half-size first
+// and last chunks), window ms/step unchanged (profiles/r06/o, p).
 std::vector<int64_t> stream_cuts(int64_t in_lo, int64_t in_hi, int chunks);
 // Upload boundaries for chunks of rows in proportion to `weights` (one
 // chunk per weight, each > 0); chunks that would be empty are merged.

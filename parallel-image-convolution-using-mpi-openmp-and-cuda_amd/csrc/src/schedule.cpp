@@ -73,9 +73,8 @@ std::vector<int64_t> stream_cuts(int64_t in_lo, int64_t in_hi, int chunks) {
   const int64_t n = in_hi - in_lo;
   chunks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(chunks, n)));
   if (chunks <= 1) return {};
-  // weights 1, 2, ..., 2, 1 (two chunks: 1, 1)
-  std::vector<int> w(static_cast<size_t>(chunks), chunks == 2 ? 1 : 2);
-  w.front() = w.back() = 1;
+  std::vector<int> w(static_cast<size_t>(chunks), 5);  // 5, ..., 5, 6
+  w.back() = 6;
   return stream_cuts_weighted(in_lo, in_hi, w);
 }
 

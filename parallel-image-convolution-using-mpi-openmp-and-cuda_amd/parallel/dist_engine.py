@@ -86,7 +86,7 @@ class DistributedBlur:
         uploads over two of them (>= 4 slots); `stream_min_bytes` (None: the
         native default, 8 MiB) is the smallest input head-streamed;
         `stream_weights` (one per chunk; sets the chunk count) sizes the
-        streamed chunks (None: 1, 2, ..., 2, 1);
+        streamed chunks (None: the native default, schedule.hpp stream_cuts);
         `ipc_pull` is the IPC transport's pull form (grid | single | sdma,
         ipc_halo.hpp).  `qualify_staging`: time every slot's pinned staging
         buffers through the copy engines once and replace any that copies

@@ -196,9 +196,9 @@ def test_stream_plan_values(native, rng, ch, height, world, reps, fuse, chunks):
 
 def test_stream_cuts_shape(native):
     assert native.stream_cuts(0, 2520, 1) == []
-    assert native.stream_cuts(0, 100, 2) == [50]
-    c = native.stream_cuts(0, 2520, 6)  # weights 1,2,2,2,2,1 / 10
-    assert c == [252, 756, 1260, 1764, 2268]
+    assert native.stream_cuts(0, 110, 2) == [50]  # 5, 6
+    c = native.stream_cuts(0, 2520, 4)  # weights 5,5,5,6 / 21
+    assert c == [600, 1200, 1800]
     c = native.stream_cuts(-40, 355, 4)
     assert all(-40 < x < 355 for x in c) and c == sorted(set(c))
     assert native.stream_cuts(0, 3, 10) == [1, 2] or len(native.stream_cuts(0, 3, 10)) <= 2
@@ -206,7 +206,8 @@ def test_stream_cuts_shape(native):
 
 def test_stream_cuts_weighted(native):
     # the default weights through the weighted form
-    assert native.stream_cuts_weighted(0, 2520, [1, 2, 2, 2, 2, 1]) == native.stream_cuts(0, 2520, 6)
+    assert native.stream_cuts_weighted(0, 2520, [5, 5, 5, 5, 5, 6]) == native.stream_cuts(0, 2520, 6)
+    assert native.stream_cuts_weighted(0, 2520, [1, 2, 2, 2, 2, 1]) == [252, 756, 1260, 1764, 2268]
     assert native.stream_cuts_weighted(0, 2520, [3, 4, 4, 5, 5]) == [360, 840, 1320, 1920]
     assert native.stream_cuts_weighted(-40, 2560, [1]) == []
     # more chunks than rows: empty chunks merged, cuts strictly inside

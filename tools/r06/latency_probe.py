@@ -58,7 +58,8 @@ def main():
             lat2.append((time.perf_counter() - t) * 1e3)
             traces.append([[round(x, 4) for x in r] for r in blur.pipe.slot(k).stream_trace()])
         out["traced_latency_ms"] = sorted(lat2)[len(lat2) // 2]
-        out["chunk_trace_ms"] = traces[-3:]  # per chunk: [chunk, upload end, launches end, download end]
+        # per chunk: [chunk, upload end, launch wait passed, launches end, download wait passed, download end]
+        out["chunk_trace_ms"] = traces[-3:]
     print(json.dumps(out))
 
 
