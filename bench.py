@@ -112,8 +112,6 @@ def parse():
                    help="relative rows of each streamed chunk (sets the chunk count; default 5,...,5,6)")
     p.add_argument("--spin-wait", choices=["on", "off"], default=None,
                    help="drain() polls the streams instead of blocking on them (default: the native default)")
-    p.add_argument("--interleave-downloads", choices=["on", "off"], default=None,
-                   help="streamed image: each chunk's download issued right after its launches (default: native)")
     p.add_argument("--head-one-upload-stream", dest="head_alt_uploads", action="store_false", default=True,
                    help="streamed head image: all chunk uploads on one slot's stream (default with >= 4 slots: "
                         "alternating over two, one image 0.546-0.549 vs 0.559-0.568 ms, profiles/r05/l/)")
@@ -785,9 +783,7 @@ def main():
                                transport=head_transport, concurrent={"auto": -1, "on": 1, "off": 0}[a.concurrent],
                                step_graphs={"auto": None, "on": True, "off": False}[a.step_graphs],
                                graph_capture=a.graph_capture == "on", stream_chunks=a.stream_chunks,
-                               stream_weights=stream_weights(a),
-                               interleave_downloads=None if a.interleave_downloads is None
-                               else a.interleave_downloads == "on", stream_min_bytes=int(a.stream_min_mb * 2 ** 20),
+                               stream_weights=stream_weights(a), stream_min_bytes=int(a.stream_min_mb * 2 ** 20),
                                qualify_staging=a.qualify_staging == "on", flush_staging=a.flush_staging == "on",
                                **policy_kwargs(a))
     blur.load_synthetic(a.seed)
@@ -935,7 +931,6 @@ def main():
                 "stream_chunks": int(len(stream_weights(a)) if a.stream_weights else a.stream_chunks),
                 "stream_weights": list(blur.pipe.options["stream_weights"]),
                 "spin_wait": bool(blur.pipe.options["spin_wait"]),
-                "interleave_downloads": bool(blur.pipe.options["interleave_downloads"]),
                 "stream_min_mb": a.stream_min_mb,
                 "preload_halo": bool(blur.preload_halo),
                 "launches_per_step": int(stats.launches),

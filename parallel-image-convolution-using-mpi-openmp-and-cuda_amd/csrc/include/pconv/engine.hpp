@@ -113,10 +113,6 @@ struct EngineOptions {
   // spins) instead of a blocking synchronize, whose wake-up after a wait of
   // a few hundred µs lands late.
   bool spin_wait = false;
-  // Streamed images: issue each chunk's download right after its own
-  // launches instead of after every chunk's launches (the host's ~0.1 ms of
-  // launch calls then no longer sits in front of the first download).
-  bool interleave_downloads = false;
 };
 
 struct RunStats {

@@ -378,10 +378,8 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
   // Host issue order: every upload first (the H2D stream then runs them back
   // to back instead of waiting for the host to issue the next one behind the
   // previous chunk's launches), then each chunk's launches behind its
-  // upload's event, then each download behind its chunk's event — after all
-  // the launches, or (EngineOptions::interleave_downloads) right after its
-  // own chunk's launches.  One event per chunk and direction (no re-recorded
-  // event is waited on).
+  // upload's event, then each download behind its chunk's event.  One event
+  // per chunk and direction (no re-recorded event is waited on).
   // Chunk copies are SDMA copies: CU copy kernels beside the launches
   // measured slower (0.76-1.02 vs 0.55 ms per image, profiles/r04/verify/).
   auto copy = [&](uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, int64_t rows, hipMemcpyKind kind,
@@ -401,17 +399,8 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
            hipMemcpyDeviceToHost, s);
   };
   auto up_of = [&](size_t c) { return (c & 1) && up2 ? up2 : up; };
-  auto download_chunk = [&](size_t c) {
-    const StreamChunk& ch = sp.chunks[c];
-    if (!(ch.down_hi > ch.down_lo && host_out)) return;
-    dn_evs_[c].wait_on(down);
-    if (stream_trace_) st_ev_[4 + 5 * c].record(down);
-    download(ch, down);
-    if (stream_trace_) st_ev_[5 + 5 * c].record(down);
-  };
-  const bool inter = opt_.interleave_downloads;
-  // diagnostics (stream_trace): timing events at the start, then after each
-  // chunk's upload, launch wait, launches, download wait and download
+  // diagnostics (stream_trace): timing events at the start, after each
+  // chunk's upload, launches and download — [0] start, then 3 per chunk
   const bool tr_on = stream_trace_;
   if (tr_on) {
     while (st_ev_.size() < 1 + 5 * nc) st_ev_.push_back(Event::create(true));
@@ -436,14 +425,19 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
     if (ch.down_hi > ch.down_lo && host_out) {
       dn_evs_[c].record(cs_);
       pending = false;
-      if (inter) download_chunk(c);
     }
   }
   // `down` finishing must mean the whole image is done (the next image of
   // these frames waits on it), also when launches follow the last download.
   if (pending) dn_evs_[nc].record(cs_);
-  if (!inter)
-    for (size_t c = 0; c < nc; ++c) download_chunk(c);
+  for (size_t c = 0; c < nc; ++c) {
+    const StreamChunk& ch = sp.chunks[c];
+    if (!(ch.down_hi > ch.down_lo && host_out)) continue;
+    dn_evs_[c].wait_on(down);
+    if (tr_on) st_ev_[4 + 5 * c].record(down);
+    download(ch, down);
+    if (tr_on) st_ev_[5 + 5 * c].record(down);
+  }
   if (pending) dn_evs_[nc].wait_on(down);
   cur_ = (c0 + sp.levels) & 1;
   halo_valid_ = false;

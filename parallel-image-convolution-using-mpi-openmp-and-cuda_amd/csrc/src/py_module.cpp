@@ -606,10 +606,9 @@ PYBIND11_MODULE(_pconv_native, m) {
                        int concurrent, bool graphs, bool step_graphs, py::object band, bool slot_comm,
                        int stream_chunks, bool cu_mask_queues, bool head_on_slot_streams,
                        int64_t stream_min_bytes, bool head_alt_uploads, std::vector<int> stream_weights,
-                       bool spin_wait, bool interleave_downloads) {
+                       bool spin_wait) {
              EngineOptions o;
              o.spin_wait = spin_wait;
-             o.interleave_downloads = interleave_downloads;
              o.head_alt_uploads = head_alt_uploads;
              o.stream_chunks = stream_chunks;
              PCONV_CHECK(stream_weights.empty() || static_cast<int>(stream_weights.size()) == stream_chunks,
@@ -636,8 +635,7 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0,
            py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true,
            py::arg("stream_min_bytes") = EngineOptions{}.stream_min_bytes, py::arg("head_alt_uploads") = true,
-           py::arg("stream_weights") = std::vector<int>{}, py::arg("spin_wait") = EngineOptions{}.spin_wait,
-           py::arg("interleave_downloads") = EngineOptions{}.interleave_downloads)
+           py::arg("stream_weights") = std::vector<int>{}, py::arg("spin_wait") = EngineOptions{}.spin_wait)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -680,7 +678,6 @@ PYBIND11_MODULE(_pconv_native, m) {
                                d["stream_chunks"] = o.stream_chunks;
                                d["stream_weights"] = o.stream_weights;
                                d["spin_wait"] = o.spin_wait;
-                               d["interleave_downloads"] = o.interleave_downloads;
                                d["stream_min_bytes"] = o.stream_min_bytes;
                                d["head_alt_uploads"] = o.head_alt_uploads;
                                d["cu_mask_queues"] = o.cu_mask_queues;

@@ -145,16 +145,13 @@ def test_head_stream_weights_headline_frame(pconv_mod, rng, weights):
     assert blur.pipe.streamed_heads == 4
 
 
-@pytest.mark.parametrize("inter", [False, True])
 @pytest.mark.parametrize("mode", ["direct", "head"])
-def test_spin_wait_interleaved_downloads(pconv_mod, rng, mode, inter):
-    """spin_wait: drain() and wait_image() poll instead of blocking;
-    interleave_downloads: each streamed chunk's download issued right after
-    its launches — same bytes, every image complete when they return."""
+def test_spin_wait(pconv_mod, rng, mode):
+    """spin_wait: drain() and wait_image() poll instead of blocking — same
+    bytes, every image complete when they return."""
     w, h, reps = 96, 120, 40
-    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=4 if mode == "head" else 2, mode=mode, spin_wait=True,
-                 interleave_downloads=inter)
-    assert blur.pipe.options["spin_wait"] is True and blur.pipe.options["interleave_downloads"] is inter
+    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=4 if mode == "head" else 2, mode=mode, spin_wait=True)
+    assert blur.pipe.options["spin_wait"] is True
     _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps, rounds=3)
     img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
     ref = pconv_mod.numpy_convolve(img, reps)
