@@ -110,8 +110,6 @@ def parse():
                         "burst, every single image: latency_ms 0.56 vs 0.69 ms whole-image, profiles/r04/head/)")
     p.add_argument("--stream-weights", default=None, metavar="W1,W2,...",
                    help="relative rows of each streamed chunk (sets the chunk count; default 5,...,5,6)")
-    p.add_argument("--spin-wait", choices=["on", "off"], default=None,
-                   help="drain() polls the streams instead of blocking on them (default: the native default)")
     p.add_argument("--head-one-upload-stream", dest="head_alt_uploads", action="store_false", default=True,
                    help="streamed head image: all chunk uploads on one slot's stream (default with >= 4 slots: "
                         "alternating over two, one image 0.546-0.549 vs 0.559-0.568 ms, profiles/r05/l/)")
@@ -289,7 +287,6 @@ def policy_kwargs(a) -> dict:
     return dict(cu_mask_queues=getattr(a, "cu_mask_queues", True),
                 head_on_slot_streams=getattr(a, "head_on_slot_streams", True),
                 head_alt_uploads=getattr(a, "head_alt_uploads", True),
-                spin_wait=None if getattr(a, "spin_wait", None) is None else a.spin_wait == "on",
                 ipc_pull=getattr(a, "ipc_pull", "grid"))
 
 
@@ -930,7 +927,6 @@ def main():
                 "fuse": int(blur.engine.fuse),
                 "stream_chunks": int(len(stream_weights(a)) if a.stream_weights else a.stream_chunks),
                 "stream_weights": list(blur.pipe.options["stream_weights"]),
-                "spin_wait": bool(blur.pipe.options["spin_wait"]),
                 "stream_min_mb": a.stream_min_mb,
                 "preload_halo": bool(blur.preload_halo),
                 "launches_per_step": int(stats.launches),

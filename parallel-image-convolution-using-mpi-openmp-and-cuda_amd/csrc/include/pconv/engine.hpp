@@ -109,10 +109,6 @@ struct EngineOptions {
   // driver's window 0.334-0.348 vs 0.337-0.351 ms; alternating the downloads
   // too was slower (0.564-0.580, both 0.602-0.625: profiles/r05/l/).
   bool head_alt_uploads = true;
-  // BandPipeline::drain / wait_image poll the streams / event (a CPU core
-  // spins) instead of a blocking synchronize, whose wake-up after a wait of
-  // a few hundred µs lands late.
-  bool spin_wait = false;
 };
 
 struct RunStats {
@@ -212,8 +208,7 @@ class BandEngine {
   void exec_exchange(const Phase& p);
   void exec_compute(const Phase& p);
 
-  // spin: poll the streams (hipStreamQuery) instead of blocking on them.
-  void synchronize(bool spin = false);
+  void synchronize();
   const RunStats& last_stats() const { return stats_; }
 
   // Zero both frames (ghost rows, pads and data).

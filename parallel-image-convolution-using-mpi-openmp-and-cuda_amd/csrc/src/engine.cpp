@@ -10,8 +10,6 @@
 #include <cstdlib>
 #include <thread>
 
-#include <immintrin.h>
-
 namespace pconv {
 
 namespace {
@@ -539,27 +537,9 @@ void BandEngine::exec_compute(const Phase& p) {
   cur_ ^= 1;
 }
 
-namespace {
-// Poll until the stream has no work left (a spinning core instead of a
-// blocking wait and its wake-up).
-void spin_sync(hipStream_t s) {
-  for (;;) {
-    const hipError_t e = hipStreamQuery(s);
-    if (e == hipSuccess) return;
-    if (e != hipErrorNotReady) PCONV_HIP_CHECK(e);
-    _mm_pause();
-  }
-}
-}  // namespace
-
-void BandEngine::synchronize(bool spin) {
-  if (spin) {
-    spin_sync(cs_);
-    if (ms_ != cs_) spin_sync(ms_);
-  } else {
-    PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
-    if (ms_ != cs_) PCONV_HIP_CHECK(hipStreamSynchronize(ms_));
-  }
+void BandEngine::synchronize() {
+  PCONV_HIP_CHECK(hipStreamSynchronize(cs_));
+  if (ms_ != cs_) PCONV_HIP_CHECK(hipStreamSynchronize(ms_));
   if (timing_pending_) {
     stats_.loop_ms = Event::elapsed_ms(ev_t0_, ev_t1_);
     stats_.wall_ms = (wall_seconds() - wall_t0_) * 1e3;
@@ -731,13 +711,7 @@ bool BandPipeline::ready(int k) const {
   return true;
 }
 
-void BandPipeline::wait_image(int k) const {
-  if (!slots_[0]->options().spin_wait) {
-    done_.at(static_cast<size_t>(k)).sync();
-    return;
-  }
-  while (!ready(k)) _mm_pause();
-}
+void BandPipeline::wait_image(int k) const { done_.at(static_cast<size_t>(k)).sync(); }
 
 void BandPipeline::completion_mark(int k, bool before, bool streamed) {
   if (mark_ev_.empty()) return;
@@ -924,16 +898,9 @@ std::vector<std::vector<double>> BandPipeline::trace() {
 }
 
 void BandPipeline::drain() {
-  const bool spin = slots_[0]->options().spin_wait;
-  auto sync = [&](hipStream_t s) {
-    if (spin)
-      spin_sync(s);
-    else
-      PCONV_HIP_CHECK(hipStreamSynchronize(s));
-  };
-  if (h2d_.get()) sync(h2d_.get());
-  for (auto& s : slots_) s->synchronize(spin);
-  if (d2h_.get()) sync(d2h_.get());
+  if (h2d_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(h2d_.get()));
+  for (auto& s : slots_) s->synchronize();
+  if (d2h_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(d2h_.get()));
   burst_pos_ = 0;
 }
 

@@ -527,7 +527,7 @@ PYBIND11_MODULE(_pconv_native, m) {
       .def("wait_stream", [](BandEngine& e, uintptr_t s) { e.wait_stream(reinterpret_cast<hipStream_t>(s)); })
       .def("signal_stream", [](BandEngine& e, uintptr_t s) { e.signal_stream(reinterpret_cast<hipStream_t>(s)); })
       .def("run", &BandEngine::run, py::arg("reps"), py::call_guard<py::gil_scoped_release>())
-      .def("synchronize", &BandEngine::synchronize, py::arg("spin") = false, py::call_guard<py::gil_scoped_release>())
+      .def("synchronize", &BandEngine::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("clear", &BandEngine::clear)
       .def_property_readonly("stats", &BandEngine::last_stats)
       .def(
@@ -605,10 +605,8 @@ PYBIND11_MODULE(_pconv_native, m) {
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
                        int concurrent, bool graphs, bool step_graphs, py::object band, bool slot_comm,
                        int stream_chunks, bool cu_mask_queues, bool head_on_slot_streams,
-                       int64_t stream_min_bytes, bool head_alt_uploads, std::vector<int> stream_weights,
-                       bool spin_wait) {
+                       int64_t stream_min_bytes, bool head_alt_uploads, std::vector<int> stream_weights) {
              EngineOptions o;
-             o.spin_wait = spin_wait;
              o.head_alt_uploads = head_alt_uploads;
              o.stream_chunks = stream_chunks;
              PCONV_CHECK(stream_weights.empty() || static_cast<int>(stream_weights.size()) == stream_chunks,
@@ -635,7 +633,7 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0,
            py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true,
            py::arg("stream_min_bytes") = EngineOptions{}.stream_min_bytes, py::arg("head_alt_uploads") = true,
-           py::arg("stream_weights") = std::vector<int>{}, py::arg("spin_wait") = EngineOptions{}.spin_wait)
+           py::arg("stream_weights") = std::vector<int>{})
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -677,7 +675,6 @@ PYBIND11_MODULE(_pconv_native, m) {
                                py::dict d;
                                d["stream_chunks"] = o.stream_chunks;
                                d["stream_weights"] = o.stream_weights;
-                               d["spin_wait"] = o.spin_wait;
                                d["stream_min_bytes"] = o.stream_min_bytes;
                                d["head_alt_uploads"] = o.head_alt_uploads;
                                d["cu_mask_queues"] = o.cu_mask_queues;

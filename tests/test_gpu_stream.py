@@ -145,28 +145,6 @@ def test_head_stream_weights_headline_frame(pconv_mod, rng, weights):
     assert blur.pipe.streamed_heads == 4
 
 
-@pytest.mark.parametrize("mode", ["direct", "head"])
-def test_spin_wait(pconv_mod, rng, mode):
-    """spin_wait: drain() and wait_image() poll instead of blocking — same
-    bytes, every image complete when they return."""
-    w, h, reps = 96, 120, 40
-    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=4 if mode == "head" else 2, mode=mode, spin_wait=True)
-    assert blur.pipe.options["spin_wait"] is True
-    _run_images(pconv_mod, rng, blur, w, h, "rgb", "gaussian", reps, rounds=3)
-    img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
-    ref = pconv_mod.numpy_convolve(img, reps)
-    blur.load_image(img)
-    for _ in range(3):
-        assert np.array_equal(blur.step(reps).reshape(h, w, 3), ref)
-    if mode == "head":
-        ks = [blur.submit(reps) for _ in range(4)]
-        for k in ks:
-            blur.pipe.wait_image(k)
-            assert blur.pipe.ready(k)
-            assert np.array_equal(blur.outputs[k].reshape(h, w, 3), ref), k
-        blur.drain()
-
-
 def test_head_stream_threshold(pconv_mod, rng):
     """EngineOptions::stream_min_bytes (default 8 MiB): the headline frame
     (14.5 MB) is head-streamed, its 8-way band (2.3 MB) runs as one step

@@ -22,7 +22,6 @@ def main():
     p.add_argument("--images", type=int, default=30)
     p.add_argument("--chunks", type=int, default=4)
     p.add_argument("--weights", default=None, help="streamed chunk weights, e.g. 3,4,4,5,5 (sets --chunks)")
-    p.add_argument("--spin", action="store_true", help="drain() polls the streams")
     p.add_argument("--fuse", type=int, default=None, help="reps per launch (default: the engine's pick)")
     p.add_argument("--trace", type=int, default=0, help="then this many images with chunk timing events")
     a = p.parse_args()
@@ -33,8 +32,7 @@ def main():
     torch.cuda.set_device(0)
     blur = DistributedBlur(1920, 2520, "rgb", "gaussian", 40, rank=0, world=1, device=0, slots=4,
                            stream_chunks=a.chunks, fuse=a.fuse,
-                           stream_weights=[int(x) for x in a.weights.split(",")] if a.weights else None,
-                           spin_wait=a.spin)
+                           stream_weights=[int(x) for x in a.weights.split(",")] if a.weights else None)
     blur.load_synthetic(1234)
     for _ in range(5):
         blur.submit(40)
@@ -47,8 +45,7 @@ def main():
     lat.sort()
     out = {"latency_ms_median": round(lat[len(lat) // 2], 4), "min": round(lat[0], 4), "max": round(lat[-1], 4),
            "streamed_heads": int(blur.pipe.streamed_heads), "chunks": a.chunks, "fuse": a.fuse,
-           "weights": a.weights,
-           "spin": a.spin}
+           "weights": a.weights}
     if a.trace:
         # the same single images with chunk timing events (their own timing shifts slightly)
         for k in range(blur.slots):
