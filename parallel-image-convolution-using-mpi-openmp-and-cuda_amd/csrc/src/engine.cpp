@@ -376,7 +376,9 @@ hipStream_t BandEngine::enqueue_streamed(const uint8_t* host_in, int64_t in_r0, 
   // Host issue order: every upload first (the H2D stream then runs them back
   // to back instead of waiting for the host to issue the next one behind the
   // previous chunk's launches), then each chunk's launches behind its
-  // upload's event, then each download behind its chunk's event.  One event
+  // upload's event, then each download behind its chunk's event (issuing
+  // each download right after its own chunk's launches measured no better:
+  // 0.5375-0.5378 vs 0.5197-0.5377 ms per image, profiles/r06/r/).  One event
   // per chunk and direction (no re-recorded event is waited on).
   // Chunk copies are SDMA copies: CU copy kernels beside the launches
   // measured slower (0.76-1.02 vs 0.55 ms per image, profiles/r04/verify/).
@@ -897,6 +899,9 @@ std::vector<std::vector<double>> BandPipeline::trace() {
   return out;
 }
 
+// Blocking syncs: polling the streams instead (hipStreamQuery in a loop)
+// measured within noise for one image (0.5169-0.5411 vs 0.5197-0.5377 ms,
+// profiles/r06/r/) and costs a core.
 void BandPipeline::drain() {
   if (h2d_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(h2d_.get()));
   for (auto& s : slots_) s->synchronize();
