@@ -22,6 +22,7 @@ def main():
     p.add_argument("--images", type=int, default=30)
     p.add_argument("--chunks", type=int, default=4)
     p.add_argument("--weights", default=None, help="streamed chunk weights, e.g. 3,4,4,5,5 (sets --chunks)")
+    p.add_argument("--tune-candidates", type=int, default=None, help="shapes timed per launch geometry")
     p.add_argument("--fuse", type=int, default=None, help="reps per launch (default: the engine's pick)")
     p.add_argument("--trace", type=int, default=0, help="then this many images with chunk timing events")
     a = p.parse_args()
@@ -30,6 +31,9 @@ def main():
     from pconv.parallel.dist_engine import DistributedBlur
 
     torch.cuda.set_device(0)
+    if a.tune_candidates:
+        import pconv
+        pconv.native.set_tune_candidates(a.tune_candidates)
     blur = DistributedBlur(1920, 2520, "rgb", "gaussian", 40, rank=0, world=1, device=0, slots=4,
                            stream_chunks=a.chunks, fuse=a.fuse,
                            stream_weights=[int(x) for x in a.weights.split(",")] if a.weights else None)
@@ -45,7 +49,8 @@ def main():
     lat.sort()
     out = {"latency_ms_median": round(lat[len(lat) // 2], 4), "min": round(lat[0], 4), "max": round(lat[-1], 4),
            "streamed_heads": int(blur.pipe.streamed_heads), "chunks": a.chunks, "fuse": a.fuse,
-           "weights": a.weights}
+           "weights": a.weights,
+           "tune_candidates": a.tune_candidates}
     if a.trace:
         # the same single images with chunk timing events (their own timing shifts slightly)
         for k in range(blur.slots):
@@ -60,6 +65,9 @@ def main():
         out["traced_latency_ms"] = sorted(lat2)[len(lat2) // 2]
         # per chunk: [chunk, upload end, launch wait passed, launches end, download wait passed, download end]
         out["chunk_trace_ms"] = traces[-3:]
+    import pconv
+    # the tuner's pick per launch key: [ch, steps, rows, row bytes, form, pf, lanes, rows/wave, waves]
+    out["tuned"] = [list(k) + list(sh) for k, sh in pconv.native.swar_tuned()]
     print(json.dumps(out))
 
 
