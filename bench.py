@@ -545,25 +545,39 @@ def copy_floor_ms(in_bytes: int, out_bytes: int, device: int, iters: int = 8):
     return h2d, d2h
 
 
-def copy_floors(measure, world: int, rank: int):
-    """A copy floor per rank twice: SOLO (rank r measures while every other
-    rank waits between barriers, one rank at a time) and CONCURRENT (every
-    rank at once, between two barriers).  With one GPU per rank on its own
-    PCIe link, concurrent = solo; a larger concurrent floor means the ranks
-    share something on the host side (host DRAM bandwidth, a PCIe switch) —
-    what the first 8-GPU line must separate from link rates.  Every rank must
-    call it; returns (solo per rank, concurrent per rank)."""
+CONCURRENT_FLOOR_MS = 20.0  # each rank's concurrent copies span at least this long at its solo rate
+
+
+def copy_floors(run, world: int, rank: int):
+    """A copy floor per rank twice: SOLO (rank r runs while every other rank
+    waits between barriers, one rank at a time; the better of two runs of 8
+    pairs) and CONCURRENT (every rank at once between two barriers, one run
+    long enough — CONCURRENT_FLOOR_MS at the slowest solo rate — that the
+    barrier's release skew is small against the span the ranks overlap, and
+    its mean, not a minimum).  `run(n)` times n copy pairs, ms per pair.
+    With one GPU per rank on its own PCIe link, concurrent = solo; a larger
+    concurrent floor means the ranks share something on the host side (host
+    DRAM bandwidth, a PCIe switch) — what the first 8-GPU line must separate
+    from link rates.  Every rank must call it; returns (solo per rank,
+    concurrent per rank); one rank: concurrent = solo."""
+    import math
+
     from pconv.parallel.bootstrap import barrier
 
     solo = -1.0
     for r in range(world):
         barrier()
         if r == rank:
-            solo = measure()
+            solo = min(run(8), run(8))
+    solos = gather_floats(solo)
+    if world == 1:
+        return solos, solos
+    valid = [s for s in solos if s > 0]
+    n = min(4000, max(8, math.ceil(CONCURRENT_FLOOR_MS / max(valid)))) if valid else 8
     barrier()
-    conc = measure() if world > 1 else solo
+    conc = run(n)
     barrier()
-    return gather_floats(solo), gather_floats(conc)
+    return solos, gather_floats(conc)
 
 
 def staging_numa(blur) -> dict:
@@ -851,17 +865,23 @@ def main():
     d2h_ms = max_over_ranks(d2h_ms / 1e3) * 1e3
     # ... and both directions at once, pitched like the pipeline's copies: the
     # floor a PCIe-bound step converges to (diagnostic only: never fatal)
-    def pair_floor():
+    try:
+        probe = pconv.native.CopyProbe(device, blur.row_bytes, blur.inputs[0].size // blur.row_bytes, b.rows)
+    except Exception as e:  # noqa: BLE001
+        print(f"bench: copy pair floor not measured: {e}", file=sys.stderr)
+        probe = None
+
+    def pair_run(n):
         try:
-            return pconv.native.copy_pair_floor_ms(device, blur.row_bytes, blur.inputs[0].size // blur.row_bytes,
-                                                   b.rows, 8)
+            return probe.run(n) if probe is not None else -1.0
         except Exception as e:  # noqa: BLE001
             print(f"bench: copy pair floor not measured: {e}", file=sys.stderr)
             return -1.0
 
     # per rank: alone on the node (one rank at a time) and with every rank copying at once (N > 1: whether
     # the ranks' host paths are independent, or share host DRAM / a switch)
-    pair_solo, pair_conc = copy_floors(pair_floor, ctx.world, ctx.rank)
+    pair_solo, pair_conc = copy_floors(pair_run, ctx.world, ctx.rank)
+    del probe  # its pinned rows and device frames
     pair_ms = max(pair_conc)
     if a.emulate:
         world = 1

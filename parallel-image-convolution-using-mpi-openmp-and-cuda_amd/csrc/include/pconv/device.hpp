@@ -56,9 +56,6 @@ int bind_to_device_numa(int device);
 // (~94 GB/s in both directions together on the measured boxes), so this, not
 // the slower solo copy, is what a PCIe-bound step converges to.
 double copy_pair_floor_ms(int device, int64_t row_bytes, int64_t rows_in, int64_t rows_out, int iters);
-// The same copies from / into GIVEN pinned host buffers (nullptr: fresh
-// ones), each direction alone and both together, ms per copy / pair: whether
-// one slot's staging buffers are slower than another's.
 // NUMA node of every page of a host range (move_pages(2) query, nothing
 // moved): node -> pages; a negative key is -errno for pages the kernel could
 // not report, <= -1000 when the query itself failed.  And a GPU's own node
@@ -72,6 +69,10 @@ void flush_host_cache(const void* p, size_t bytes);
 struct CopyFloor {
   double h2d_ms = 0, d2h_ms = 0, pair_ms = 0;
 };
+// The same copies from / into GIVEN pinned host buffers (nullptr: fresh
+// ones), each direction alone and both together, ms per copy / pair (the
+// best of two runs of `iters`): whether one slot's staging buffers are
+// slower than another's.
 CopyFloor copy_floor_on(int device, uint8_t* host_in, uint8_t* host_out, int64_t row_bytes, int64_t rows_in,
                         int64_t rows_out, int iters);
 
@@ -167,6 +168,28 @@ class Event {
 
  private:
   hipEvent_t e_ = nullptr;
+};
+
+// The copies behind the copy floors, set up once (device frames, pinned host
+// rows unless given, two streams; first-use costs paid in the constructor),
+// then timed on demand: run(n, up, down) issues n pitched H2D copies on one
+// stream and / or n pitched D2H copies on another and returns ms per copy
+// (pair) over the whole run — no minimum taken, so ranks that run at once
+// see each other's traffic (bench.py's concurrent floors).
+class CopyProbe {
+ public:
+  CopyProbe(int device, uint8_t* host_in, uint8_t* host_out, int64_t row_bytes, int64_t rows_in, int64_t rows_out);
+  double run(int n, bool up, bool down);
+
+ private:
+  int device_;
+  int64_t row_bytes_, rows_in_, rows_out_, pitch_;
+  DeviceBuffer din_, dout_;
+  PinnedBuffer hin_own_, hout_own_;
+  uint8_t* host_in_;
+  uint8_t* host_out_;
+  Stream s1_, s2_;
+  Event e0_, a_, b_;
 };
 
 }  // namespace pconv

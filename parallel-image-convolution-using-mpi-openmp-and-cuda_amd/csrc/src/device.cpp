@@ -118,48 +118,62 @@ int device_numa_node(int device) {
   return n;
 }
 
-CopyFloor copy_floor_on(int device, uint8_t* host_in, uint8_t* host_out, int64_t row_bytes, int64_t rows_in,
-                        int64_t rows_out, int iters) {
-  PCONV_CHECK(row_bytes > 0 && rows_in > 0 && rows_out > 0 && iters > 0, "copy floor: empty copy");
+CopyProbe::CopyProbe(int device, uint8_t* host_in, uint8_t* host_out, int64_t row_bytes, int64_t rows_in,
+                     int64_t rows_out)
+    : device_(device), row_bytes_(row_bytes), rows_in_(rows_in), rows_out_(rows_out) {
+  PCONV_CHECK(row_bytes > 0 && rows_in > 0 && rows_out > 0, "copy probe: empty copy");
   set_device(device);
-  const int64_t pitch = (row_bytes + 16 + 127) / 128 * 128;  // a padded frame pitch like the engine's
-  DeviceBuffer din(static_cast<size_t>(pitch * rows_in)), dout(static_cast<size_t>(pitch * rows_out));
-  PinnedBuffer hin_own, hout_own;
+  pitch_ = (row_bytes + 16 + 127) / 128 * 128;  // a padded frame pitch like the engine's
+  din_ = DeviceBuffer(static_cast<size_t>(pitch_ * rows_in));
+  dout_ = DeviceBuffer(static_cast<size_t>(pitch_ * rows_out));
   if (!host_in) {
-    hin_own = PinnedBuffer(static_cast<size_t>(row_bytes * rows_in));
-    host_in = hin_own.data();
+    hin_own_ = PinnedBuffer(static_cast<size_t>(row_bytes * rows_in));
+    host_in = hin_own_.data();
   }
   if (!host_out) {
-    hout_own = PinnedBuffer(static_cast<size_t>(row_bytes * rows_out));
-    host_out = hout_own.data();
+    hout_own_ = PinnedBuffer(static_cast<size_t>(row_bytes * rows_out));
+    host_out = hout_own_.data();
   }
-  Stream s1 = Stream::create(0), s2 = Stream::create(0);
-  Event e0 = Event::create(true), a = Event::create(true), b = Event::create(true);
-  auto run = [&](int n, bool up, bool down) {
-    PCONV_HIP_CHECK(hipDeviceSynchronize());
-    e0.record(s1.get());
-    e0.wait_on(s2.get());
-    for (int i = 0; i < n; ++i) {
-      if (up)
-        PCONV_HIP_CHECK(hipMemcpy2DAsync(din.data() + 16, static_cast<size_t>(pitch), host_in,
-                                         static_cast<size_t>(row_bytes), static_cast<size_t>(row_bytes),
-                                         static_cast<size_t>(rows_in), hipMemcpyHostToDevice, s1.get()));
-      if (down)
-        PCONV_HIP_CHECK(hipMemcpy2DAsync(host_out, static_cast<size_t>(row_bytes), dout.data() + 16,
-                                         static_cast<size_t>(pitch), static_cast<size_t>(row_bytes),
-                                         static_cast<size_t>(rows_out), hipMemcpyDeviceToHost, s2.get()));
-    }
-    a.record(s1.get());
-    b.record(s2.get());
-    a.sync();
-    b.sync();
-    return std::max(Event::elapsed_ms(e0, a), Event::elapsed_ms(e0, b)) / n;
-  };
+  host_in_ = host_in;
+  host_out_ = host_out;
+  s1_ = Stream::create(0);
+  s2_ = Stream::create(0);
+  e0_ = Event::create(true);
+  a_ = Event::create(true);
+  b_ = Event::create(true);
   (void)run(2, true, true);  // warm: first-use queue / engine set-up
+}
+
+double CopyProbe::run(int n, bool up, bool down) {
+  PCONV_CHECK(n > 0 && (up || down), "copy probe: nothing to run");
+  set_device(device_);
+  PCONV_HIP_CHECK(hipDeviceSynchronize());
+  e0_.record(s1_.get());
+  e0_.wait_on(s2_.get());
+  const size_t rb = static_cast<size_t>(row_bytes_), p = static_cast<size_t>(pitch_);
+  for (int i = 0; i < n; ++i) {
+    if (up)
+      PCONV_HIP_CHECK(hipMemcpy2DAsync(din_.data() + 16, p, host_in_, rb, rb, static_cast<size_t>(rows_in_),
+                                       hipMemcpyHostToDevice, s1_.get()));
+    if (down)
+      PCONV_HIP_CHECK(hipMemcpy2DAsync(host_out_, rb, dout_.data() + 16, p, rb, static_cast<size_t>(rows_out_),
+                                       hipMemcpyDeviceToHost, s2_.get()));
+  }
+  a_.record(s1_.get());
+  b_.record(s2_.get());
+  a_.sync();
+  b_.sync();
+  return std::max(Event::elapsed_ms(e0_, a_), Event::elapsed_ms(e0_, b_)) / n;
+}
+
+CopyFloor copy_floor_on(int device, uint8_t* host_in, uint8_t* host_out, int64_t row_bytes, int64_t rows_in,
+                        int64_t rows_out, int iters) {
+  PCONV_CHECK(iters > 0, "copy floor: iters must be > 0");
+  CopyProbe probe(device, host_in, host_out, row_bytes, rows_in, rows_out);
   CopyFloor f;
-  f.h2d_ms = std::min(run(iters, true, false), run(iters, true, false));
-  f.d2h_ms = std::min(run(iters, false, true), run(iters, false, true));
-  f.pair_ms = std::min(run(iters, true, true), run(iters, true, true));
+  f.h2d_ms = std::min(probe.run(iters, true, false), probe.run(iters, true, false));
+  f.d2h_ms = std::min(probe.run(iters, false, true), probe.run(iters, false, true));
+  f.pair_ms = std::min(probe.run(iters, true, true), probe.run(iters, true, true));
   return f;
 }
 

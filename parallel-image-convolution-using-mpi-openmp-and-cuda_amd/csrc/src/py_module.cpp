@@ -327,6 +327,15 @@ PYBIND11_MODULE(_pconv_native, m) {
       py::arg("device"), py::arg("host_in"), py::arg("host_out"), py::arg("row_bytes"), py::arg("rows_in"),
       py::arg("rows_out"), py::arg("iters") = 8,
       "(H2D alone, D2H alone, concurrent pair) ms with the given pinned host buffers (0: fresh ones)");
+  py::class_<CopyProbe>(m, "CopyProbe")
+      .def(py::init([](int device, int64_t row_bytes, int64_t rows_in, int64_t rows_out) {
+             py::gil_scoped_release nogil;
+             return std::make_unique<CopyProbe>(device, nullptr, nullptr, row_bytes, rows_in, rows_out);
+           }),
+           py::arg("device"), py::arg("row_bytes"), py::arg("rows_in"), py::arg("rows_out"))
+      .def("run", &CopyProbe::run, py::arg("n"), py::arg("up") = true, py::arg("down") = true,
+           py::call_guard<py::gil_scoped_release>(),
+           "ms per copy (pair) over n pitched H2D and / or D2H copies issued on two streams");
   m.def("bind_to_device_numa", &bind_to_device_numa,
         "Restrict this process to the CPUs local to the GPU (returns the CPUs kept; 0: unchanged)");
 

@@ -299,13 +299,13 @@ def _floor_worker(rank, world, port, q):
         spec.loader.exec_module(bench)
         spans = []
 
-        def measure():  # a stand-in copy floor: 0.2 s of "copying", returns ms
+        def run(n):  # a stand-in copy run: 0.2 s of "copying", returns ms per pair
             t0 = time.time()
             time.sleep(0.2)
-            spans.append((t0, time.time()))
-            return 200.0 + rank
+            spans.append((t0, time.time(), n))
+            return 200.0 + rank + (0.5 if len(spans) == 1 else 0.0)
 
-        solo, conc = bench.copy_floors(measure, world, rank)
+        solo, conc = bench.copy_floors(run, world, rank)
         q.put((rank, solo, conc, spans))
     finally:
         dist.destroy_process_group()
@@ -315,8 +315,9 @@ def test_bench_copy_floors_solo_and_concurrent():
     """bench.py's copy floors at N > 1: every rank measures
     once ALONE (one rank at a time between barriers: no two solo spans
     overlap) and once with all ranks AT ONCE (the concurrent spans all
-    overlap); both come back as per-rank lists on every rank, the fields
-    `pair_ms_solo` / `pair_ms_concurrent` of every N > 1 line."""
+    overlap, one run long enough for the barrier skew not to matter); both
+    come back as per-rank lists on every rank, the fields `pair_ms_solo` /
+    `pair_ms_concurrent` of every N > 1 line."""
     world = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -329,10 +330,11 @@ def test_bench_copy_floors_solo_and_concurrent():
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
     for rank, solo, conc, spans in res:
+        # solo: the better of two runs of 8; concurrent: one run, its own value
         assert solo == [200.0, 201.0, 202.0] and conc == [200.0, 201.0, 202.0]
-        assert len(spans) == 2
-    solo_spans = sorted(r[3][0] for r in res)
+        assert [s[2] for s in spans] == [8, 8, 8]  # >= 20 ms at a 202 ms "rate": the minimum 8
+    solo_spans = sorted((r[3][0][0], r[3][1][1]) for r in res)
     for (a0, a1), (b0, b1) in zip(solo_spans, solo_spans[1:]):
         assert a1 <= b0, "solo floors overlapped"
-    conc_spans = [r[3][1] for r in res]
+    conc_spans = [r[3][2] for r in res]
     assert max(s[0] for s in conc_spans) < min(s[1] for s in conc_spans), "concurrent floors did not overlap"

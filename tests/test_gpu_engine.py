@@ -383,6 +383,23 @@ def test_copy_pair_floor(native):
         native.copy_pair_floor_ms(0, rb, 0, rows, 4)
 
 
+def test_copy_probe(native):
+    """CopyProbe (bench.py's solo and concurrent floors): set up once, then
+    timed runs of H2D alone, D2H alone and both together, ms per copy —
+    each at most the link's one-way peak, a pair no faster than its slower
+    copy could be; an empty run refused."""
+    rb, rows = 5760, 630
+    p = native.CopyProbe(0, rb, rows, rows)
+    floor = rb * rows / 64e9 * 1e3
+    h2d, d2h, pair = p.run(8, True, False), p.run(8, False, True), p.run(8)
+    assert all(floor <= ms < 50 for ms in (h2d, d2h, pair))
+    assert pair >= 0.9 * max(h2d, d2h)
+    with pytest.raises(Exception):
+        p.run(0)
+    with pytest.raises(Exception):
+        p.run(4, False, False)
+
+
 @pytest.mark.parametrize("typ,filt,reps", [("rgb", "gaussian", 40), ("grey", "edge", 9)])
 def test_cli_auto_backend_gpu_path(pconv_mod, tmp_path, typ, filt, reps):
     """`--backend auto` on a job priced above the GPU's start-up (forced with
