@@ -55,17 +55,29 @@ __device__ __forceinline__ u32 keep(u32 v) {
 // either way (the tile's halo is sized for the CH bytes per step that enter
 // at a strip edge, whatever their values), and columns outside the image are
 // real zeros inside the strip, where the two forms agree exactly.
+#ifndef PCONV_XLANE_LDS
+#define PCONV_XLANE_LDS 0
+#endif
+// The neighbouring lane's value (DIR +1: lane + 1, -1: lane - 1).
+template <int DIR>
+__device__ __forceinline__ u32 xlane(u32 v) {
+#if PCONV_XLANE_LDS
+  const int lane = static_cast<int>(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
+  return static_cast<u32>(__builtin_amdgcn_ds_bpermute(((lane + DIR) & 63) << 2, static_cast<int>(v)));
+#else
+  return __builtin_amdgcn_mov_dpp(v, DIR > 0 ? 0x130 : 0x138, 0xf, 0xf, true);
+#endif
+}
+
 template <int CH, int NP>
 __device__ __forceinline__ void horiz(const u32 (&X)[NP], u32 (&H)[NP]) {
   static_assert(CH <= NP, "tap distance must not exceed the pairs per lane");
   u32 P[NP];
 #pragma unroll
   for (int j = 0; j < NP; ++j)
-    P[j] = keep(j + CH < NP ? X[j] + X[j + CH]
-                            : __builtin_amdgcn_mov_dpp(X[j + CH - NP], 0x130, 0xf, 0xf, true) + X[j]);
+    P[j] = keep(j + CH < NP ? X[j] + X[j + CH] : xlane<1>(X[j + CH - NP]) + X[j]);
 #pragma unroll
-  for (int k = 0; k < NP; ++k)
-    H[k] = keep(k >= CH ? P[k - CH] + P[k] : __builtin_amdgcn_mov_dpp(P[k - CH + NP], 0x138, 0xf, 0xf, true) + P[k]);
+  for (int k = 0; k < NP; ++k) H[k] = keep(k >= CH ? P[k - CH] + P[k] : xlane<-1>(P[k - CH + NP]) + P[k]);
 }
 
 template <int NP>
