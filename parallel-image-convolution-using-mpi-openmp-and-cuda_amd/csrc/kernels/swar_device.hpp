@@ -55,18 +55,15 @@ __device__ __forceinline__ u32 keep(u32 v) {
 // either way (the tile's halo is sized for the CH bytes per step that enter
 // at a strip edge, whatever their values), and columns outside the image are
 // real zeros inside the strip, where the two forms agree exactly.
-#ifndef PCONV_XLANE_LDS
-#define PCONV_XLANE_LDS 0
-#endif
-// The neighbouring lane's value (DIR +1: lane + 1, -1: lane - 1).
+// The neighbouring lane's value (DIR +1: lane + 1, -1: lane - 1) as the DPP
+// source of the add that consumes it.  Read with an LDS permute instead
+// (ds_bpermute, off the VALU, the add a plain VOP2): bit-exact but slower —
+// us per repetition, headline 4.78 vs 3.32, 8-way band 2.17 vs 1.47, 32768^2
+// grey 105.7-108.2 vs 105.0-108.7 (the permute's latency waits;
+// profiles/r06/w/).
 template <int DIR>
 __device__ __forceinline__ u32 xlane(u32 v) {
-#if PCONV_XLANE_LDS
-  const int lane = static_cast<int>(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
-  return static_cast<u32>(__builtin_amdgcn_ds_bpermute(((lane + DIR) & 63) << 2, static_cast<int>(v)));
-#else
   return __builtin_amdgcn_mov_dpp(v, DIR > 0 ? 0x130 : 0x138, 0xf, 0xf, true);
-#endif
 }
 
 template <int CH, int NP>
