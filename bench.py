@@ -110,6 +110,8 @@ def parse():
                         "burst, every single image: latency_ms 0.56 vs 0.69 ms whole-image, profiles/r04/head/)")
     p.add_argument("--stream-weights", default=None, metavar="W1,W2,...",
                    help="relative rows of each streamed chunk (sets the chunk count; default 5,...,5,6)")
+    p.add_argument("--lazy-head", choices=["on", "off"], default=None,
+                   help="hold a burst's first image until the next submit (step graph) or drain (row-streamed)")
     p.add_argument("--head-one-upload-stream", dest="head_alt_uploads", action="store_false", default=True,
                    help="streamed head image: all chunk uploads on one slot's stream (default with >= 4 slots: "
                         "alternating over two, one image 0.546-0.549 vs 0.559-0.568 ms, profiles/r05/l/)")
@@ -287,6 +289,7 @@ def policy_kwargs(a) -> dict:
     return dict(cu_mask_queues=getattr(a, "cu_mask_queues", True),
                 head_on_slot_streams=getattr(a, "head_on_slot_streams", True),
                 head_alt_uploads=getattr(a, "head_alt_uploads", True),
+                lazy_head=None if getattr(a, "lazy_head", None) is None else a.lazy_head == "on",
                 ipc_pull=getattr(a, "ipc_pull", "grid"))
 
 
@@ -947,6 +950,7 @@ def main():
                 "fuse": int(blur.engine.fuse),
                 "stream_chunks": int(len(stream_weights(a)) if a.stream_weights else a.stream_chunks),
                 "stream_weights": list(blur.pipe.options["stream_weights"]),
+                "lazy_head": bool(blur.pipe.options["lazy_head"]),
                 "stream_min_mb": a.stream_min_mb,
                 "preload_halo": bool(blur.preload_halo),
                 "launches_per_step": int(stats.launches),

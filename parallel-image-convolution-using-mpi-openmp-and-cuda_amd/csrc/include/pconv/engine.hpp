@@ -109,6 +109,11 @@ struct EngineOptions {
   // driver's window 0.334-0.348 vs 0.337-0.351 ms; alternating the downloads
   // too was slower (0.564-0.580, both 0.602-0.625: profiles/r05/l/).
   bool head_alt_uploads = true;
+  // Slot-stream mode with head streaming: a burst's first image is held back
+  // until the pipeline knows whether more follow — the next submit issues it
+  // as a step graph (a burst), drain / ready / wait_image / marks issue it
+  // row-streamed (a single image, the latency case).
+  bool lazy_head = false;
 };
 
 struct RunStats {
@@ -341,13 +346,25 @@ class BandPipeline {
   std::vector<std::vector<double>> marks();
   // Slot-stream mode: has slot k's latest image completed (its output buffer
   // final)?  wait_image(k) blocks until it has — one image, not the drain.
-  bool ready(int k) const;
-  void wait_image(int k) const;
+  bool ready(int k);
+  void wait_image(int k);
 
  private:
   void trace_mark(int stage, hipStream_t s);
   void completion_mark(int k, bool before, bool streamed);
   void submit_image(int k, const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps);
+  // EngineOptions::lazy_head: the held-back first image of a burst; issue it
+  // streamed (nothing follows) or as a step graph (a burst follows).
+  struct HeldImage {
+    const uint8_t* in = nullptr;
+    int64_t r0 = 0, r1 = 0;
+    uint8_t* out = nullptr;
+    int reps = 0;
+    bool valid = false;
+  };
+  HeldImage held_;
+  bool force_graph_ = false;
+  void issue_held(bool streamed);
   Stream h2d_, d2h_, comm_;
   std::vector<Stream> computes_;
   std::vector<Stream> slot_comms_;  // slot_comm: one communication stream per slot

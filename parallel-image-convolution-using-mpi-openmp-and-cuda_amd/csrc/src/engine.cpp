@@ -690,7 +690,14 @@ void BandPipeline::set_transport(std::shared_ptr<HaloTransport> t) {
 
 void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, uint8_t* host_out, int reps) {
   TraceRange tr("pconv.pipeline.submit");
+  if (held_.valid) issue_held(false);  // a burst: its first image as a step graph
   const int k = static_cast<int>(count_ % static_cast<int64_t>(slots_.size()));
+  if (graphs_ && step_graphs_ && head_streaming_ && burst_pos_ == 0 && slots_[0]->options().lazy_head) {
+    burst_start_.record(slots_[static_cast<size_t>(k)]->compute_stream());
+    completion_mark(k, true, false);
+    held_ = HeldImage{host_in, in_r0, in_r1, host_out, reps, true};
+    return;
+  }
   // A burst's first image (nothing in flight) starts behind a timing event on
   // its slot's stream (burst_start_): windows whose first image did so ran
   // 0.3281-0.3309 ms/step against 0.3323-0.3365 without (4 interleaved
@@ -706,14 +713,30 @@ void BandPipeline::submit(const uint8_t* host_in, int64_t in_r0, int64_t in_r1, 
   if (graphs_) done_[static_cast<size_t>(k)].record(slots_[static_cast<size_t>(k)]->compute_stream());
 }
 
-bool BandPipeline::ready(int k) const {
+void BandPipeline::issue_held(bool streamed) {
+  const HeldImage h = held_;
+  held_.valid = false;
+  const int k = static_cast<int>(count_ % static_cast<int64_t>(slots_.size()));
+  const int64_t heads = streamed_heads_;
+  force_graph_ = !streamed;
+  submit_image(k, h.in, h.r0, h.r1, h.out, h.reps);
+  force_graph_ = false;
+  completion_mark(k, false, streamed_heads_ != heads);
+  done_[static_cast<size_t>(k)].record(slots_[static_cast<size_t>(k)]->compute_stream());
+}
+
+bool BandPipeline::ready(int k) {
+  if (held_.valid) issue_held(true);
   const hipError_t e = hipEventQuery(done_.at(static_cast<size_t>(k)).get());
   if (e == hipErrorNotReady) return false;
   PCONV_HIP_CHECK(e);
   return true;
 }
 
-void BandPipeline::wait_image(int k) const { done_.at(static_cast<size_t>(k)).sync(); }
+void BandPipeline::wait_image(int k) {
+  if (held_.valid) issue_held(true);
+  done_.at(static_cast<size_t>(k)).sync();
+}
 
 void BandPipeline::completion_mark(int k, bool before, bool streamed) {
   if (mark_ev_.empty()) return;
@@ -785,7 +808,7 @@ void BandPipeline::submit_image(int k, const uint8_t* host_in, int64_t in_r0, in
     // (the second on the first head's streams) measured no better — 0.3315-
     // 0.3353 vs 0.3288-0.3328 ms/step, the second head's slot 0.04 ms late
     // in every window (profiles/r06/h/h2_*) — and was removed.
-    if (burst_pos_ == 0 && head_streaming_ && in_bytes >= e.options().stream_min_bytes) {
+    if (burst_pos_ == 0 && head_streaming_ && !force_graph_ && in_bytes >= e.options().stream_min_bytes) {
       // Head streaming: nothing is in flight, so this image's rows stream
       // (chunked H2D ‖ launches ‖ D2H of finished rows, schedule.hpp
       // plan_streamed) instead of waiting for its whole upload and its
@@ -903,6 +926,7 @@ std::vector<std::vector<double>> BandPipeline::trace() {
 // measured within noise for one image (0.5169-0.5411 vs 0.5197-0.5377 ms,
 // profiles/r06/r/) and costs a core.
 void BandPipeline::drain() {
+  if (held_.valid) issue_held(true);  // a single image: row-streamed
   if (h2d_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(h2d_.get()));
   for (auto& s : slots_) s->synchronize();
   if (d2h_.get()) PCONV_HIP_CHECK(hipStreamSynchronize(d2h_.get()));

@@ -614,8 +614,10 @@ PYBIND11_MODULE(_pconv_native, m) {
                        int device, int halo, int fuse, bool overlap, const std::string& variant, int slots,
                        int concurrent, bool graphs, bool step_graphs, py::object band, bool slot_comm,
                        int stream_chunks, bool cu_mask_queues, bool head_on_slot_streams,
-                       int64_t stream_min_bytes, bool head_alt_uploads, std::vector<int> stream_weights) {
+                       int64_t stream_min_bytes, bool head_alt_uploads, std::vector<int> stream_weights,
+                       bool lazy_head) {
              EngineOptions o;
+             o.lazy_head = lazy_head;
              o.head_alt_uploads = head_alt_uploads;
              o.stream_chunks = stream_chunks;
              PCONV_CHECK(stream_weights.empty() || static_cast<int>(stream_weights.size()) == stream_chunks,
@@ -642,7 +644,7 @@ PYBIND11_MODULE(_pconv_native, m) {
            py::arg("band") = py::none(), py::arg("slot_comm") = false, py::arg("stream_chunks") = 0,
            py::arg("cu_mask_queues") = true, py::arg("head_on_slot_streams") = true,
            py::arg("stream_min_bytes") = EngineOptions{}.stream_min_bytes, py::arg("head_alt_uploads") = true,
-           py::arg("stream_weights") = std::vector<int>{})
+           py::arg("stream_weights") = std::vector<int>{}, py::arg("lazy_head") = EngineOptions{}.lazy_head)
       .def_property_readonly("slots", &BandPipeline::slots)
       .def("slot", &BandPipeline::slot, py::return_value_policy::reference_internal)
       .def("attach_rccl",
@@ -684,6 +686,7 @@ PYBIND11_MODULE(_pconv_native, m) {
                                py::dict d;
                                d["stream_chunks"] = o.stream_chunks;
                                d["stream_weights"] = o.stream_weights;
+                               d["lazy_head"] = o.lazy_head;
                                d["stream_min_bytes"] = o.stream_min_bytes;
                                d["head_alt_uploads"] = o.head_alt_uploads;
                                d["cu_mask_queues"] = o.cu_mask_queues;

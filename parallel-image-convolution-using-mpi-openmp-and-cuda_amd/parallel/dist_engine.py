@@ -78,7 +78,7 @@ class DistributedBlur:
                  ipc_timeout_s: float = 30.0, ipc_pull: str = "grid", cu_mask_queues: bool = True,
                  head_on_slot_streams: bool = True, stream_min_bytes: Optional[int] = None,
                  head_alt_uploads: bool = True, qualify_staging: bool = True, flush_staging: bool = True,
-                 stream_weights: Optional[Sequence[int]] = None):
+                 stream_weights: Optional[Sequence[int]] = None, lazy_head: Optional[bool] = None):
         """Pipeline policy (native EngineOptions, echoed by bench.py's JSON
         config): `cu_mask_queues` puts every slot stream on its own hardware
         queue; `head_on_slot_streams` runs a streamed head image's copies on
@@ -87,6 +87,8 @@ class DistributedBlur:
         native default, 8 MiB) is the smallest input head-streamed;
         `stream_weights` (one per chunk; sets the chunk count) sizes the
         streamed chunks (None: the native default, schedule.hpp stream_cuts);
+        `lazy_head` holds a burst's first image back until the next submit
+        (then a step graph) or drain (then row-streamed) (None: native default);
         `ipc_pull` is the IPC transport's pull form (grid | single | sdma,
         ipc_halo.hpp).  `qualify_staging`: time every slot's pinned staging
         buffers through the copy engines once and replace any that copies
@@ -118,6 +120,7 @@ class DistributedBlur:
                   cu_mask_queues=bool(cu_mask_queues), head_on_slot_streams=bool(head_on_slot_streams),
                   head_alt_uploads=bool(head_alt_uploads),
                   stream_weights=[int(w) for w in (stream_weights or [])],
+                  **({} if lazy_head is None else {"lazy_head": bool(lazy_head)}),
                   **({} if stream_min_bytes is None else {"stream_min_bytes": int(stream_min_bytes)}))
         if self_neighbours:
             # One-GPU emulation of rank `rank` of a `world`-way split whose halos

@@ -278,7 +278,8 @@ def test_bench_policy_flags():
     finally:
         sys.argv = old
     kw = bench.policy_kwargs(a)
-    assert kw == dict(cu_mask_queues=False, head_on_slot_streams=False, head_alt_uploads=True, ipc_pull="sdma")
+    assert kw == dict(cu_mask_queues=False, head_on_slot_streams=False, head_alt_uploads=True, lazy_head=None,
+                      ipc_pull="sdma")
     assert bench.mode_kwargs(a, "ipc", 8)["ipc_pull"] == "sdma"
 
 

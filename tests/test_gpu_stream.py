@@ -145,6 +145,42 @@ def test_head_stream_weights_headline_frame(pconv_mod, rng, weights):
     assert blur.pipe.streamed_heads == 4
 
 
+@pytest.mark.parametrize("slots", [3, 4])
+def test_lazy_head(pconv_mod, rng, slots):
+    """lazy_head: a burst's first image is held until the next submit (then a
+    step graph: no streamed head) or until drain / wait_image / ready (then
+    row-streamed); bursts, single images and per-image waits bit-exact."""
+    w, h, reps = 96, 120, 40
+    blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=slots, mode="head", lazy_head=True)
+    assert blur.pipe.options["lazy_head"] is True
+    for rnd in range(3):  # bursts: every slot loaded first, then submitted back to back
+        imgs = [rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for _ in range(slots)]
+        for k, img in enumerate(imgs):
+            blur.load_image(img, slot=k)
+            blur.outputs[k][:] = 0xAB
+        ks = [blur.submit(reps) for _ in imgs]
+        blur.drain()
+        for k in ks:
+            assert np.array_equal(blur.outputs[k].reshape(h, w, 3), pconv_mod.numpy_convolve(imgs[k], reps)), (rnd, k)
+    assert blur.pipe.streamed_heads == 0  # every burst's first image ran as a step graph
+    img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+    ref = pconv_mod.numpy_convolve(img, reps)
+    blur.load_image(img)
+    for i in range(3):
+        assert np.array_equal(blur.step(reps).reshape(h, w, 3), ref)
+        assert blur.pipe.streamed_heads == i + 1  # single images: streamed at drain
+    k = blur.submit(reps)  # held
+    blur.pipe.wait_image(k)  # issues it (streamed) and waits for it
+    assert blur.pipe.ready(k) and blur.pipe.streamed_heads == 4
+    assert np.array_equal(blur.outputs[k].reshape(h, w, 3), ref)
+    blur.drain()
+    ks = [blur.submit(reps) for _ in range(2 * slots)]
+    blur.drain()
+    for k in ks:
+        assert np.array_equal(blur.outputs[k].reshape(h, w, 3), ref), k
+    assert blur.pipe.streamed_heads == 4
+
+
 def test_head_stream_threshold(pconv_mod, rng):
     """EngineOptions::stream_min_bytes (default 8 MiB): the headline frame
     (14.5 MB) is head-streamed, its 8-way band (2.3 MB) runs as one step
