@@ -106,12 +106,14 @@ def parse():
     p.add_argument("--stream-chunks", type=int, default=4,
                    help="rows streamed within each image: upload in this many row chunks, advance every level behind "
                         "them, download finished rows meanwhile (H2D, reps and D2H of ONE image overlap; 0 = off). "
-                        "With step graphs only an image submitted to an idle pipeline is streamed (the head of a "
-                        "burst, every single image: latency_ms 0.56 vs 0.69 ms whole-image, profiles/r04/head/)")
+                        "With step graphs only an image submitted to an idle pipeline is streamed, and with "
+                        "--lazy-head (default) only when no second image follows before the drain: every single "
+                        "image (latency_ms 0.53 vs 0.69 ms whole-image)")
     p.add_argument("--stream-weights", default=None, metavar="W1,W2,...",
                    help="relative rows of each streamed chunk (sets the chunk count; default 5,...,5,6)")
     p.add_argument("--lazy-head", choices=["on", "off"], default=None,
-                   help="hold a burst's first image until the next submit (step graph) or drain (row-streamed)")
+                   help="hold a burst's first image until the next submit (step graph) or drain (row-streamed); "
+                        "default (native) on: window 0.3290 vs 0.3315 ms/step median, profiles/r06/z/")
     p.add_argument("--head-one-upload-stream", dest="head_alt_uploads", action="store_false", default=True,
                    help="streamed head image: all chunk uploads on one slot's stream (default with >= 4 slots: "
                         "alternating over two, one image 0.546-0.549 vs 0.559-0.568 ms, profiles/r05/l/)")

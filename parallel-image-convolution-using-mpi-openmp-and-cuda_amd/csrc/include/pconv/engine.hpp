@@ -112,8 +112,11 @@ struct EngineOptions {
   // Slot-stream mode with head streaming: a burst's first image is held back
   // until the pipeline knows whether more follow — the next submit issues it
   // as a step graph (a burst), drain / ready / wait_image / marks issue it
-  // row-streamed (a single image, the latency case).
-  bool lazy_head = false;
+  // row-streamed (a single image, the latency case).  The driver's 20-image
+  // window 0.3282 / 0.3290 / 0.3300 vs 0.3292 / 0.3315 / 0.3335 ms/step
+  // eager (6 interleaved pairs, faster in each), one image 0.5349 vs 0.5351
+  // ms (profiles/r06/z/).
+  bool lazy_head = true;
 };
 
 struct RunStats {

@@ -241,16 +241,18 @@ def test_pipeline_staging_qualification(pconv_mod, rng):
         assert np.array_equal(blur.outputs[k].reshape(h, w, 3), pconv_mod.numpy_convolve(img, reps))
 
 
-def test_pipeline_per_image_completion(pconv_mod, rng):
+@pytest.mark.parametrize("lazy", [False, True])
+def test_pipeline_per_image_completion(pconv_mod, rng, lazy):
     """Slot-stream pipeline: every image ends in its slot's completion event
     — wait_image(k) makes that image's output final without draining the
     others, ready(k) reports it; completion marks (the bench's diagnostic
-    pass) give one time per image, increasing."""
+    pass) give one time per image, increasing.  The burst's first image is
+    row-streamed when issued eagerly, a step graph when held (lazy_head)."""
     from pconv.parallel.dist_engine import DistributedBlur
 
     w, h, reps = 97, 88, 16
     blur = DistributedBlur(w, h, "rgb", "gaussian", reps, rank=0, world=1, device=0, slots=4, step_graphs=True,
-                           stream_chunks=4, stream_min_bytes=0)
+                           stream_chunks=4, stream_min_bytes=0, lazy_head=lazy)
     imgs = [rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for _ in range(4)]
     for k, img in enumerate(imgs):
         blur.load_image(img, slot=k)
@@ -261,7 +263,7 @@ def test_pipeline_per_image_completion(pconv_mod, rng):
         assert blur.pipe.ready(k)
         assert np.array_equal(blur.outputs[k].reshape(h, w, 3), pconv_mod.numpy_convolve(imgs[k], reps)), k
     marks = blur.pipe.marks()
-    assert [int(m[0]) for m in marks] == ks and [int(m[2]) for m in marks] == [1, 0, 0, 0]
+    assert [int(m[0]) for m in marks] == ks and [int(m[2]) for m in marks] == [0 if lazy else 1, 0, 0, 0]
     assert all(b[1] >= a[1] > 0 for a, b in zip(marks, marks[1:])), marks
 
 

@@ -134,7 +134,7 @@ def test_head_stream_weights_headline_frame(pconv_mod, rng, weights):
     img = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
     ref = convolve(img, reps, backend="omp")
     blur = _blur(w, h, "rgb", "gaussian", reps, 4, slots=4, mode="head", stream_weights=weights,
-                 stream_min_bytes=None)
+                 stream_min_bytes=None, lazy_head=False)  # the burst's head streamed too
     blur.load_image(img)
     for _ in range(3):
         assert np.array_equal(blur.step(reps).reshape(h, w, 3), ref)
