@@ -86,6 +86,7 @@ class PinnedBuffer;
 // paces a whole pipeline (docs/ROUND6.md §1).
 struct StagingReport {
   std::vector<CopyFloor> first, final;
+  CopyFloor fresh;  // the same copies through freshly allocated buffers (the reference)
   int replaced = 0;
 };
 StagingReport qualify_staging(int device, std::vector<PinnedBuffer>& ins, std::vector<PinnedBuffer>& outs,

@@ -244,7 +244,10 @@ class DistributedBlur:
         the slow mode of the driver's 20-image window (profiles/r06/).  So
         every slot's buffers go through the copy engines once (H2D alone,
         D2H alone: copy_floor_on), and a buffer more than `tolerance` slower
-        than the best of its direction is replaced by a fresh allocation —
+        than the best of its direction — over the slots AND a freshly
+        allocated pair, since in one process every slot's output buffer ran
+        D2H at 0.41 ms against 0.26 for fresh buffers (profiles/r06/aa/
+        drv_0.json) — is replaced by a fresh allocation —
         the rejected ones stay allocated until the search ends, so the
         allocator cannot hand the same pages back — up to `attempts` rounds.
         Set-up only (before any image is loaded); returns what it measured."""
@@ -256,9 +259,10 @@ class DistributedBlur:
                     for k in range(self.slots)]
 
         held, first, replaced = [], rates(), 0
+        fresh = n.copy_floor_on(self.device, 0, 0, rb, in_rows, out_rows, 4)
         now = first
         for _ in range(attempts):
-            best_h, best_d = min(r[0] for r in now), min(r[1] for r in now)
+            best_h, best_d = min([fresh[0]] + [r[0] for r in now]), min([fresh[1]] + [r[1] for r in now])
             bad_in = [k for k, r in enumerate(now) if r[0] > tolerance * best_h]
             bad_out = [k for k, r in enumerate(now) if r[1] > tolerance * best_d]
             if not bad_in and not bad_out:
@@ -273,7 +277,8 @@ class DistributedBlur:
             now = rates()
         del held
         r4 = lambda v: [[round(x, 4) for x in r] for r in v]  # noqa: E731
-        return {"h2d_d2h_pair_ms_first": r4(first), "h2d_d2h_pair_ms": r4(now), "replaced": replaced}
+        return {"h2d_d2h_pair_ms_first": r4(first), "h2d_d2h_pair_ms": r4(now), "fresh_ms": r4([fresh])[0],
+                "replaced": replaced}
 
     # ------------------------------------------------------------ inputs
     @property

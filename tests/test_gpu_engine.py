@@ -229,6 +229,7 @@ def test_pipeline_staging_qualification(pconv_mod, rng):
     assert st is not None and st["replaced"] >= 0
     for key in ("h2d_d2h_pair_ms_first", "h2d_d2h_pair_ms"):
         assert len(st[key]) == 4 and all(len(r) == 3 and min(r) > 0 for r in st[key]), st
+    assert len(st["fresh_ms"]) == 3 and min(st["fresh_ms"]) > 0  # the fresh-buffer reference
     for k in range(4):
         assert blur.inputs[k].ctypes.data == blur._in[k].ptr and blur.outputs[k].ctypes.data == blur._out[k].ptr
     imgs = [rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8) for _ in range(4)]
